@@ -1,0 +1,216 @@
+"""bench.py — cell-updates/s of the MI355X Game of Life engine (libgolhip.so).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload 16384|65536|262144]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+A "step" is one pass of the hot path over the whole board: `--turns-per-step`
+B3/S23 turns (default 1000) of the synthetic torus, run as fused launches of
+`--tb-depth` turns.  Timed region: exactly K steps, bracketed by a barrier and
+torch.cuda.synchronize() on both sides, max over ranks.
+
+Workloads (BASELINE.json configs; synthetic boards, data="synthetic"):
+  16384  (default, configs[1]) 16384 x 16384 per GPU, seed 0x5EED0001, 10 steps = 10k turns
+  65536  (configs[2])          65536 x 65536 per GPU, seed 0x5EED0002
+  262144 (configs[3])          262144 x 262144 total, strong-scaled over N GPUs, seed 0x5EED0003
+For N > 1 the 16384/65536 workloads are weak-scaled: the torus is N boards
+tall, rank r owns rows [r*S, (r+1)*S) and exchanges halo rows with its ring
+neighbours over RCCL every fused launch (the only collective on the path).
+
+Rank 0 prints ONE JSON line; `roofline` is measured on the step kernel with
+HIP events on the engine's stream; `cpu_baseline` times the oracle's port of
+the reference worker pool on a bounded sample (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "game-of-life-distributed_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import golhip  # noqa: E402
+
+METRIC = "cell-updates/sec (GCUPS) at 1/2/4/8 MI355X; % of HBM roofline"
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+ALG_BYTES_PER_UPDATE = 0.25  # 1 bit read + 1 bit written per cell-update
+WORKLOADS = {
+    16384: dict(seed=0x5EED0001, scaling="weak", desc="configs[1]: 16384^2 random 25% per GPU"),
+    65536: dict(seed=0x5EED0002, scaling="weak", desc="configs[2]: 65536^2 random 25% per GPU"),
+    262144: dict(seed=0x5EED0003, scaling="strong", desc="configs[3]: 262144^2 random 25%, strong-scaled"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", type=int, default=16384, choices=sorted(WORKLOADS))
+    ap.add_argument("--turns-per-step", type=int, default=None)
+    ap.add_argument("--tb-depth", type=int, default=16)
+    ap.add_argument("--rows-per-wave", type=int, default=512)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                    help="measured HBM traffic per launch (from rocprofv3 --pmc), keyed by workload")
+    return ap.parse_args()
+
+
+def cpu_baseline(W: int, target_s: float) -> dict:
+    """Oracle port of the reference worker pool (distributor.go:116-173) on a
+    bounded sample of the same synthetic board: a 4096-row band of the board,
+    as many turns as fit in ~target_s."""
+    from oracle.oracle import COracle
+
+    o = COracle()
+    rows = min(4096, W)
+    board = o.fill_random(W, rows, WORKLOADS.get(W, WORKLOADS[16384])["seed"])
+    threads = max(1, min(16, (os.cpu_count() or 2)) - 1)  # Threads; the pool runs Threads+1 workers
+    t0 = time.perf_counter()
+    o.run_workerpool(board, 1, threads)
+    one = time.perf_counter() - t0
+    turns = max(1, int(target_s / max(one, 1e-6)))
+    t0 = time.perf_counter()
+    o.run_workerpool(board, turns, threads)
+    dt = time.perf_counter() - t0
+    return {
+        "value": W * rows * turns / dt / 1e9,
+        "unit": "GCUPS",
+        "cores": threads + 1,
+        "kind": "port",
+        "sample": f"{rows}x{W} band of the workload board (torus), {turns} turns, oracle/gol_oracle.c "
+                  f"worker-pool port (Threads={threads}, Threads+1 workers), {dt:.1f} s",
+    }
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    wl = WORKLOADS[a.workload]
+    N = a.workload
+    if wl["scaling"] == "weak":
+        W, H, rows = N, N * world, N
+    else:
+        W = H = N
+        rows = H // world
+    row0 = rank * rows
+    turns_per_step = a.turns_per_step or (1000 if N <= 16384 else (100 if N <= 65536 else 10))
+
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    board = golhip.Board(W, H, device=local, row0=row0, rows=rows, timing=True) if world > 1 \
+        else golhip.Board(W, H, device=local, timing=True)
+    board.set_tb_depth(a.tb_depth)
+    board.set_rows_per_wave(a.rows_per_wave)
+    if world > 1:
+        uid = [golhip.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        board.comm_init(uid[0], world, rank)
+    board.fill_random(wl["seed"])
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        board.sync()
+        torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        board.step(turns_per_step)
+    barrier()
+    board.perf_reset()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        board.step(turns_per_step)
+    board.sync()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        dist.barrier()
+    perf = board.perf()
+    alive, at_turn = board.alive_count(global_sum=world > 1)
+
+    total_updates = W * H * turns_per_step * a.steps if wl["scaling"] == "weak" or world == 1 \
+        else W * H * turns_per_step * a.steps
+    gcups = total_updates / dt / 1e9
+    # dominant kernel: the fused step launch, timed with HIP events on the engine stream
+    launches = max(1, perf["step_launches"])
+    avg_ms = perf["step_kernel_ms"] / launches
+    alg_bytes_per_launch = W * rows * (perf["step_turns"] / launches) * ALG_BYTES_PER_UPDATE
+    achieved = alg_bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else None
+    traffic = None
+    try:
+        with open(a.pmc) as f:
+            rec = json.load(f).get(f"{N}x{a.tb_depth}")
+        if rec:
+            traffic = rec["hbm_bytes_per_launch"]
+    except (OSError, ValueError):
+        pass
+
+    out = {
+        "metric": METRIC,
+        "value": round(gcups, 3),
+        "unit": "GCUPS",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(dt / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": wl["scaling"],
+        "vs_baseline": None,
+        "dtype": "u32 bit-sliced (1 bit/cell)",
+        "data": "synthetic (splitmix64 counter-hash board, 25% alive)",
+        "config": {
+            "workload": wl["desc"],
+            "board": [H, W],
+            "rows_per_rank": rows,
+            "turns_per_step": turns_per_step,
+            "tb_depth": a.tb_depth,
+            "rows_per_wave": a.rows_per_wave,
+            "parallelism": f"row-strips x{world} (RCCL halo ring)" if world > 1 else "single GPU torus",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1) if achieved else None,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+            "traffic": traffic,
+            "kernel": f"gol_tb_kernel<{perf['tb_depth']}>",
+            "avg_launch_ms": round(avg_ms, 5),
+            "launches": perf["step_launches"],
+            "alg_bytes_per_launch": alg_bytes_per_launch,
+            "note": "achieved = 0.25 B/cell-update x updates per launch / avg launch time; "
+                    "one launch fuses tb_depth turns, so frac > 1 means temporal blocking beat "
+                    "the single-pass HBM roofline",
+        },
+        "final_alive": alive,
+        "final_turn": at_turn,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(W, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    board.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,62 @@
+// gol_kernels.h — internal launchers for the gfx950 kernels of libgolhip.so.
+// Not part of the C-ABI (include/golhip.h is).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace golk {
+
+// Physical board buffers hold `rows + 2*kHalo` rows of Ww uint32 words; local
+// row i lives at physical row kHalo + i.  Halo rows are filled by the ring
+// exchange (strip mode) and unused in torus mode.
+constexpr int kHalo = 32;        // == GOLHIP_MAX_TB_DEPTH
+constexpr int kWave = 64;
+constexpr int kTileValid = 62;   // words per wavefront tile that are stored (lanes 1..62)
+
+// How a step kernel finds input row i (logical, may be outside 0..rows-1).
+//   torus mode : phys = base + mod(i, wrap)                 (whole board on one device)
+//   halo  mode : phys = min(i + off, rmax)  (wrap == 0)     (row strip, halos filled)
+struct RowMap {
+    int base;
+    int wrap;
+    int off;
+    int rmax;
+};
+
+struct StepArgs {
+    const uint32_t *src;
+    uint32_t *dst;
+    int W;            // cells per row
+    int Ww;           // words per row
+    int rows_out;     // output rows (logical 0..rows_out-1)
+    int dst_base;     // physical row of logical output row 0
+    RowMap in;
+    int rows_per_wave;
+    unsigned long long *alive;  // nullable: += popcount of the output
+};
+
+// Bit-sliced temporal-blocked step: `depth` in {1,2,4,8,16,32}; requires W % 32 == 0.
+hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s);
+// One turn for any width (W % 32 != 0 boards such as 16x16).
+hipError_t launch_step_generic(const StepArgs &a, hipStream_t s);
+int tb_waves(const StepArgs &a, int depth);
+
+hipError_t launch_pack(const uint8_t *bytes, uint32_t *words, int W, int Ww, int rows, hipStream_t s);
+hipError_t launch_unpack(const uint32_t *words, uint8_t *bytes, int W, int Ww, int rows, hipStream_t s);
+hipError_t launch_fill_random(uint32_t *words, int W, int Ww, int rows, int64_t row0, uint64_t seed,
+                              hipStream_t s);
+hipError_t launch_popcount(const uint32_t *words, int64_t nwords, unsigned long long *out, hipStream_t s);
+hipError_t launch_hash(const uint32_t *words, int64_t nwords, int64_t word0, unsigned long long *out,
+                       hipStream_t s);
+
+// Row-major compaction of set bits of (a ^ b) (b nullable -> a alone) into
+// (x, y) int32 pairs.  Three phases: per-block counts, one-block scan,
+// ordered scatter.  compact_blocks() = per-block slots needed.
+int64_t compact_blocks(int64_t nwords);
+hipError_t launch_compact_count(const uint32_t *a, const uint32_t *b, int64_t nwords, unsigned long long *blk,
+                                hipStream_t s);
+hipError_t launch_compact_scan(unsigned long long *blk, int64_t nblk, unsigned long long *total, hipStream_t s);
+hipError_t launch_compact_scatter(const uint32_t *a, const uint32_t *b, int64_t nwords, int Ww,
+                                  int64_t row0, const unsigned long long *blk_off, int32_t *xy, hipStream_t s);
+
+}  // namespace golk

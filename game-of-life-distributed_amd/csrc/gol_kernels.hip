@@ -1,0 +1,528 @@
+// gol_kernels.hip — gfx950 kernels of libgolhip.so.
+//
+// K1 gol_tb_kernel   : the B3/S23 torus turn (distributor.go:350-417, worker
+//                      pool :304-347) for `DEPTH` fused turns per launch.
+// K1g generic kernel : same turn for widths that are not a multiple of 32.
+// K2 popcount        : len(calculateAliveCells(world)) (:420-432, ticker :292).
+// K3 compaction      : initializeAliveCells flip list (:212-220) and the
+//                      FinalTurnComplete alive list (:180), row-major.
+// K4 pack / unpack   : 0/255 bytes <-> bits at the io boundary (:66-80, :186-191).
+// K6 fill_random     : synthetic boards (BASELINE configs 2-5).
+//
+// Layout (DESIGN.md "Layout in HBM"): rows of Ww = ceil(W/32) uint32 words;
+// cell (y, x) = bit x%32 of word x/32.  Everything here is integer work bound
+// by HBM or VALU; none of it is matrix-shaped, so there is no MFMA.
+#include "gol_kernels.h"
+
+#include <algorithm>
+#include <climits>
+
+namespace golk {
+
+// ---------------------------------------------------------------------------
+// bit-sliced helpers
+// ---------------------------------------------------------------------------
+template <typename F>
+constexpr unsigned tt3(F f) {
+    unsigned r = 0;
+    for (int i = 0; i < 8; ++i)
+        if (f((i >> 2) & 1, (i >> 1) & 1, i & 1)) r |= 1u << i;
+    return r;
+}
+// v_bitop3_b32 truth tables, operand order (a, b, c) -> index a*4 + b*2 + c.
+constexpr unsigned kXor3 = tt3([](int a, int b, int c) { return (a ^ b ^ c) != 0; });       // 0x96
+constexpr unsigned kMaj = tt3([](int a, int b, int c) { return a + b + c >= 2; });          // 0xE8
+// Column sum of three 2-bit row sums: sum9 = u0 + 2*(u1 + v0) + 4*v1 (centre included).
+// next = (sum9 == 3) | (centre & sum9 == 4)  <=>  B3/S23.
+constexpr unsigned kT1 = tt3([](int u1, int v0, int v1) { return ((u1 ^ v0) & !v1) != 0; });          // twos == 1
+constexpr unsigned kT2 = tt3([](int u1, int v0, int v1) { return ((!(u1 ^ v0)) & ((u1 & v0) ^ v1)) != 0; });  // twos == 2
+constexpr unsigned kBorn = tt3([](int c, int t2, int u0) { return (c & t2 & !u0) != 0; });
+constexpr unsigned kNext = tt3([](int u0, int t1, int b) { return ((u0 & t1) | b) != 0; });
+static_assert(kXor3 == 0x96 && kMaj == 0xE8, "bitop3 table order");
+
+template <unsigned IMM>
+__device__ __forceinline__ uint32_t bop(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, IMM);
+}
+// Whole-wavefront lane shifts (DPP wave_shr:1 / wave_shl:1): lane i receives
+// lane i-1 / i+1; bound_ctrl zero-fills the edge lane (no `old` operand, so
+// no extra v_mov).  Edge lanes are the tile halo.
+__device__ __forceinline__ uint32_t from_left_lane(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t from_right_lane(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xF, 0xF, true);
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// ---------------------------------------------------------------------------
+// K1: temporal-blocked bit-sliced step.
+//
+// One wavefront = one tile of 64 consecutive words of a row band (lane j
+// holds word t0 + j - 1); it streams the band's rows top to bottom through a
+// DEPTH-stage register pipeline.  Stage t turns generation t-1 row i into
+// generation t row i-1, so after 2*DEPTH rows of fill every input row yields
+// one row DEPTH generations ahead.  Horizontal neighbours come from the
+// adjacent lanes (DPP); lanes 0 and 63 are the halo: their error front moves
+// one cell per turn, so with DEPTH <= 32 lanes 1..62 are exact and stored.
+// Vertically a wave reads DEPTH extra rows above and below its band.
+// Per stage and row: 2 DPP + 2 alignbit + 2 bitop3 (3-cell row sum, shared by
+// the three output rows that use it) + 8 bitop3 (column sum + rule) = 14 VALU
+// per 32 cells.  HBM traffic per launch ~ 2 bits per cell (read + write) for
+// DEPTH turns.
+// ---------------------------------------------------------------------------
+template <int D, int R>
+__device__ __forceinline__ uint32_t push_row(uint32_t x, uint32_t (&h0)[3][D], uint32_t (&h1)[3][D],
+                                             uint32_t (&cc)[3][D]) {
+    constexpr int N = R;            // slot of the row entering now
+    constexpr int C = (R + 2) % 3;  // previous row (the one we emit)
+    constexpr int P = (R + 1) % 3;  // the row before it
+#pragma unroll
+    for (int t = 0; t < D; ++t) {
+        const uint32_t l = from_left_lane(x);
+        const uint32_t r = from_right_lane(x);
+        const uint32_t west = __builtin_amdgcn_alignbit(x, l, 31);  // bit k = cell k-1
+        const uint32_t east = __builtin_amdgcn_alignbit(r, x, 1);   // bit k = cell k+1
+        h0[N][t] = bop<kXor3>(west, x, east);
+        h1[N][t] = bop<kMaj>(west, x, east);
+        const uint32_t u0 = bop<kXor3>(h0[P][t], h0[C][t], h0[N][t]);
+        const uint32_t u1 = bop<kMaj>(h0[P][t], h0[C][t], h0[N][t]);
+        const uint32_t v0 = bop<kXor3>(h1[P][t], h1[C][t], h1[N][t]);
+        const uint32_t v1 = bop<kMaj>(h1[P][t], h1[C][t], h1[N][t]);
+        const uint32_t t1 = bop<kT1>(u1, v0, v1);
+        const uint32_t t2 = bop<kT2>(u1, v0, v1);
+        const uint32_t born = bop<kBorn>(cc[C][t], t2, u0);
+        const uint32_t nx = bop<kNext>(u0, t1, born);
+        cc[N][t] = x;
+        x = nx;
+    }
+    return x;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int Ww = a.Ww;
+    const int tiles_x = (Ww + kTileValid - 1) / kTileValid;
+    const int S = a.rows_per_wave;
+    const int strip = wave / tiles_x;
+    const int tile = wave - strip * tiles_x;
+    const int r0 = strip * S;
+    if (r0 >= a.rows_out) return;  // wave-uniform
+
+    const int t0 = tile * kTileValid;
+    int col = (t0 + lane - 1) % Ww;
+    if (col < 0) col += Ww;
+    const bool keep = lane >= 1 && lane <= kTileValid && (t0 + lane - 1) < Ww;
+
+    const int rows_here = min(S, a.rows_out - r0);
+    const int n_in = rows_here + 2 * D;
+    const int n_groups = (n_in + 2) / 3;
+
+    // input row cursor (wave-uniform)
+    int r = r0 - D + a.in.off;
+    const int wrap = a.in.wrap > 0 ? a.in.wrap : INT_MAX;
+    if (a.in.wrap > 0) {
+        r %= a.in.wrap;
+        if (r < 0) r += a.in.wrap;
+    }
+    const uint32_t *__restrict__ src = a.src + col;
+    auto load_next = [&]() -> uint32_t {
+        const int pr = a.in.base + min(r, a.in.rmax);
+        const uint32_t v = src[(size_t)pr * Ww];
+        r = (r + 1 == wrap) ? 0 : r + 1;
+        return v;
+    };
+
+    uint32_t *__restrict__ dp = a.dst + (size_t)(a.dst_base + r0) * Ww + col;
+    uint32_t cnt = 0;
+
+    uint32_t h0[3][D], h1[3][D], cc[3][D];
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int t = 0; t < D; ++t) h0[s][t] = h1[s][t] = cc[s][t] = 0u;
+
+    uint32_t p0 = load_next(), p1 = load_next(), p2 = load_next();
+    int out_idx = -2 * D;  // output row of the group's first input row
+    for (int g = 0; g < n_groups; ++g) {
+        const uint32_t x0 = p0, x1 = p1, x2 = p2;
+        p0 = load_next();
+        p1 = load_next();
+        p2 = load_next();
+        uint32_t y;
+        y = push_row<D, 0>(x0, h0, h1, cc);
+        if (out_idx >= 0 && out_idx < rows_here) {
+            if (keep) { *dp = y; cnt += __builtin_popcount(y); }
+            dp += Ww;
+        }
+        ++out_idx;
+        y = push_row<D, 1>(x1, h0, h1, cc);
+        if (out_idx >= 0 && out_idx < rows_here) {
+            if (keep) { *dp = y; cnt += __builtin_popcount(y); }
+            dp += Ww;
+        }
+        ++out_idx;
+        y = push_row<D, 2>(x2, h0, h1, cc);
+        if (out_idx >= 0 && out_idx < rows_here) {
+            if (keep) { *dp = y; cnt += __builtin_popcount(y); }
+            dp += Ww;
+        }
+        ++out_idx;
+    }
+    if (a.alive) {
+        const uint32_t tot = wave_sum_u32(cnt);
+        if (lane == 0) atomicAdd(a.alive, (unsigned long long)tot);
+    }
+}
+
+int tb_waves(const StepArgs &a, int depth) {
+    (void)depth;
+    const int tiles_x = (a.Ww + kTileValid - 1) / kTileValid;
+    const int strips = (a.rows_out + a.rows_per_wave - 1) / a.rows_per_wave;
+    return tiles_x * strips;
+}
+
+hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s) {
+    const int waves = tb_waves(a, depth);
+    const dim3 grid((waves + 3) / 4), block(256);
+    switch (depth) {
+        case 1: hipLaunchKernelGGL(gol_tb_kernel<1>, grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL(gol_tb_kernel<2>, grid, block, 0, s, a); break;
+        case 4: hipLaunchKernelGGL(gol_tb_kernel<4>, grid, block, 0, s, a); break;
+        case 8: hipLaunchKernelGGL(gol_tb_kernel<8>, grid, block, 0, s, a); break;
+        case 16: hipLaunchKernelGGL(gol_tb_kernel<16>, grid, block, 0, s, a); break;
+        case 32: hipLaunchKernelGGL(gol_tb_kernel<32>, grid, block, 0, s, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// K1g: one turn, any width (bit-by-bit neighbour fetch with column wrap).
+// Only used for widths that are not a multiple of 32 (the 16x16 fixture).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int map_in_row(const RowMap &m, int i) {
+    int r = i + m.off;
+    if (m.wrap > 0) {
+        r %= m.wrap;
+        if (r < 0) r += m.wrap;
+    }
+    return m.base + min(r, m.rmax);
+}
+
+__global__ __launch_bounds__(256) void gol_generic_kernel(StepArgs a) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int Ww = a.Ww, W = a.W;
+    uint32_t cnt = 0;
+    if (idx < (int64_t)a.rows_out * Ww) {
+        const int row = (int)(idx / Ww);
+        const int wc = (int)(idx - (int64_t)row * Ww);
+        const uint32_t *up = a.src + (size_t)map_in_row(a.in, row - 1) * Ww;
+        const uint32_t *mid = a.src + (size_t)map_in_row(a.in, row) * Ww;
+        const uint32_t *dn = a.src + (size_t)map_in_row(a.in, row + 1) * Ww;
+        auto bit = [&](const uint32_t *p, int x) -> int {
+            x = x < 0 ? x + W : (x >= W ? x - W : x);
+            return (p[x >> 5] >> (x & 31)) & 1;
+        };
+        uint32_t out = 0;
+        for (int b = 0; b < 32; ++b) {
+            const int x = wc * 32 + b;
+            if (x >= W) break;
+            const int n = bit(up, x - 1) + bit(up, x) + bit(up, x + 1) + bit(mid, x - 1) + bit(mid, x + 1) +
+                          bit(dn, x - 1) + bit(dn, x) + bit(dn, x + 1);
+            const int c = bit(mid, x);
+            if (n == 3 || (c && n == 2)) out |= 1u << b;
+        }
+        a.dst[(size_t)(a.dst_base + row) * Ww + wc] = out;
+        cnt = __builtin_popcount(out);
+    }
+    if (a.alive) {
+        const uint32_t tot = wave_sum_u32(cnt);
+        if ((threadIdx.x & 63) == 0 && tot) atomicAdd(a.alive, (unsigned long long)tot);
+    }
+}
+
+hipError_t launch_step_generic(const StepArgs &a, hipStream_t s) {
+    const int64_t n = (int64_t)a.rows_out * a.Ww;
+    hipLaunchKernelGGL(gol_generic_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// K4: pack (0/255 bytes -> bits, alive <=> == 255) and unpack (bits -> 0/255).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pack_kernel(const uint8_t *__restrict__ bytes, uint32_t *__restrict__ words,
+                                                    int W, int Ww, int rows) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)rows * Ww) return;
+    const int row = (int)(idx / Ww);
+    const int wc = (int)(idx - (int64_t)row * Ww);
+    const uint8_t *p = bytes + (size_t)row * W + (size_t)wc * 32;
+    const int n = min(32, W - wc * 32);
+    uint32_t w = 0;
+    if (n == 32 && (W & 15) == 0) {
+        const uint4 *q = reinterpret_cast<const uint4 *>(p);
+        const uint4 v0 = q[0], v1 = q[1];
+        const uint32_t d[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (((d[k] >> (8 * j)) & 0xFFu) == 0xFFu) w |= 1u << (4 * k + j);
+    } else {
+        for (int b = 0; b < n; ++b)
+            if (p[b] == 0xFF) w |= 1u << b;
+    }
+    words[idx] = w;
+}
+
+__global__ __launch_bounds__(256) void unpack_kernel(const uint32_t *__restrict__ words, uint8_t *__restrict__ bytes,
+                                                      int W, int Ww, int rows) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)rows * Ww) return;
+    const int row = (int)(idx / Ww);
+    const int wc = (int)(idx - (int64_t)row * Ww);
+    uint8_t *p = bytes + (size_t)row * W + (size_t)wc * 32;
+    const int n = min(32, W - wc * 32);
+    const uint32_t w = words[idx];
+    if (n == 32 && (W & 15) == 0) {
+        uint32_t d[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v |= ((w >> (4 * k + j)) & 1u) ? (0xFFu << (8 * j)) : 0u;
+            d[k] = v;
+        }
+        uint4 *q = reinterpret_cast<uint4 *>(p);
+        q[0] = make_uint4(d[0], d[1], d[2], d[3]);
+        q[1] = make_uint4(d[4], d[5], d[6], d[7]);
+    } else {
+        for (int b = 0; b < n; ++b) p[b] = ((w >> b) & 1u) ? 0xFF : 0x00;
+    }
+}
+
+hipError_t launch_pack(const uint8_t *bytes, uint32_t *words, int W, int Ww, int rows, hipStream_t s) {
+    const int64_t n = (int64_t)rows * Ww;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, bytes, words, W, Ww, rows);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack(const uint32_t *words, uint8_t *bytes, int W, int Ww, int rows, hipStream_t s) {
+    const int64_t n = (int64_t)rows * Ww;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, words, bytes, W, Ww,
+                       rows);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// K6: synthetic board, cell (y, x) alive <=> (splitmix64(seed ^ (y*W + x)) & 3) == 0.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void fill_random_kernel(uint32_t *__restrict__ words, int W, int Ww, int rows,
+                                                           int64_t row0, uint64_t seed) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)rows * Ww) return;
+    const int64_t row = idx / Ww;
+    const int wc = (int)(idx - row * Ww);
+    const uint64_t base = (uint64_t)(row0 + row) * (uint64_t)W + (uint64_t)wc * 32u;
+    const int n = min(32, W - wc * 32);
+    uint32_t w = 0;
+    for (int b = 0; b < n; ++b)
+        if ((splitmix64(seed ^ (base + (uint64_t)b)) & 3u) == 0) w |= 1u << b;
+    words[idx] = w;
+}
+
+hipError_t launch_fill_random(uint32_t *words, int W, int Ww, int rows, int64_t row0, uint64_t seed,
+                              hipStream_t s) {
+    const int64_t n = (int64_t)rows * Ww;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(fill_random_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, words, W, Ww, rows,
+                       row0, seed);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// K2: popcount reduction (one atomic per wave) and the board digest.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void popcount_kernel(const uint32_t *__restrict__ w, int64_t n,
+                                                        unsigned long long *out) {
+    uint32_t c = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        c += __builtin_popcount(w[i]);
+    const uint32_t tot = wave_sum_u32(c);
+    if ((threadIdx.x & 63) == 0 && tot) atomicAdd(out, (unsigned long long)tot);
+}
+
+hipError_t launch_popcount(const uint32_t *words, int64_t nwords, unsigned long long *out, hipStream_t s) {
+    if (nwords == 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((nwords + 255) / 256, 4096);
+    hipLaunchKernelGGL(popcount_kernel, dim3((unsigned)blocks), dim3(256), 0, s, words, nwords, out);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void hash_kernel(const uint32_t *__restrict__ w, int64_t n, int64_t word0,
+                                                    unsigned long long *out) {
+    unsigned long long h = 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        h += splitmix64(((uint64_t)(word0 + i) << 32) | (uint64_t)w[i]);
+    h = wave_sum_u64(h);
+    if ((threadIdx.x & 63) == 0) atomicAdd(out, h);
+}
+
+hipError_t launch_hash(const uint32_t *words, int64_t nwords, int64_t word0, unsigned long long *out,
+                       hipStream_t s) {
+    if (nwords == 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((nwords + 255) / 256, 4096);
+    hipLaunchKernelGGL(hash_kernel, dim3((unsigned)blocks), dim3(256), 0, s, words, nwords, word0, out);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// K3: ordered stream compaction of set bits (flip list / alive list).
+// Thread t of block b owns words [b*kBlkWords + t*kWpt, +kWpt): a block
+// count pass, a single-block exclusive scan of block counts, and a scatter
+// pass that re-scans inside the block keep the output strictly row-major.
+// ---------------------------------------------------------------------------
+constexpr int kWpt = 16;
+constexpr int kBlkWords = 256 * kWpt;
+
+int64_t compact_blocks(int64_t nwords) { return (nwords + kBlkWords - 1) / kBlkWords; }
+
+__device__ __forceinline__ uint32_t cword(const uint32_t *a, const uint32_t *b, int64_t i) {
+    return b ? (a[i] ^ b[i]) : a[i];
+}
+
+__device__ uint32_t block_excl_scan(uint32_t v, uint32_t *total) {
+    __shared__ uint32_t wsum[4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+    }
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        if (w < wid) pre += wsum[w];
+        tot += wsum[w];
+    }
+    if (total) *total = tot;
+    return pre + inc - v;
+}
+
+__global__ __launch_bounds__(256) void compact_count_kernel(const uint32_t *__restrict__ a,
+                                                             const uint32_t *__restrict__ b, int64_t n,
+                                                             unsigned long long *blk) {
+    const int64_t base = (int64_t)blockIdx.x * kBlkWords + (int64_t)threadIdx.x * kWpt;
+    uint32_t c = 0;
+    for (int k = 0; k < kWpt; ++k)
+        if (base + k < n) c += __builtin_popcount(cword(a, b, base + k));
+    __shared__ uint32_t ws[4];
+    const uint32_t tot = wave_sum_u32(c);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = tot;
+    __syncthreads();
+    if (threadIdx.x == 0) blk[blockIdx.x] = (unsigned long long)ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ __launch_bounds__(1024) void compact_scan_kernel(unsigned long long *blk, int64_t nblk,
+                                                             unsigned long long *total) {
+    __shared__ unsigned long long part[1024];
+    const int64_t per = (nblk + 1023) / 1024;
+    const int64_t beg = (int64_t)threadIdx.x * per;
+    const int64_t end = min<int64_t>(beg + per, nblk);
+    unsigned long long s = 0;
+    for (int64_t i = beg; i < end; ++i) s += blk[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    // Hillis-Steele inclusive scan over 1024 partials
+    for (int o = 1; o < 1024; o <<= 1) {
+        const unsigned long long t = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0ull;
+        __syncthreads();
+        part[threadIdx.x] += t;
+        __syncthreads();
+    }
+    unsigned long long run = part[threadIdx.x] - s;  // exclusive
+    for (int64_t i = beg; i < end; ++i) {
+        const unsigned long long v = blk[i];
+        blk[i] = run;
+        run += v;
+    }
+    if (threadIdx.x == 1023) *total = part[1023];
+}
+
+__global__ __launch_bounds__(256) void compact_scatter_kernel(const uint32_t *__restrict__ a,
+                                                               const uint32_t *__restrict__ b, int64_t n, int Ww,
+                                                               int64_t row0, const unsigned long long *blk_off,
+                                                               int32_t *__restrict__ xy) {
+    const int64_t base = (int64_t)blockIdx.x * kBlkWords + (int64_t)threadIdx.x * kWpt;
+    uint32_t c = 0;
+    for (int k = 0; k < kWpt; ++k)
+        if (base + k < n) c += __builtin_popcount(cword(a, b, base + k));
+    const uint32_t pre = block_excl_scan(c, nullptr);
+    unsigned long long o = blk_off[blockIdx.x] + pre;
+    for (int k = 0; k < kWpt; ++k) {
+        const int64_t i = base + k;
+        if (i >= n) break;
+        uint32_t m = cword(a, b, i);
+        if (!m) continue;
+        const int64_t row = i / Ww;
+        const int wc = (int)(i - row * Ww);
+        while (m) {
+            const int bit = __builtin_ctz(m);
+            m &= m - 1;
+            xy[2 * o] = wc * 32 + bit;
+            xy[2 * o + 1] = (int32_t)(row0 + row);
+            ++o;
+        }
+    }
+}
+
+hipError_t launch_compact_count(const uint32_t *a, const uint32_t *b, int64_t nwords, unsigned long long *blk,
+                                hipStream_t s) {
+    const int64_t nb = compact_blocks(nwords);
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, b, nwords, blk);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact_scan(unsigned long long *blk, int64_t nblk, unsigned long long *total, hipStream_t s) {
+    hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, s, blk, nblk, total);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact_scatter(const uint32_t *a, const uint32_t *b, int64_t nwords, int Ww, int64_t row0,
+                                  const unsigned long long *blk_off, int32_t *xy, hipStream_t s) {
+    const int64_t nb = compact_blocks(nwords);
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(compact_scatter_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, b, nwords, Ww, row0, blk_off,
+                       xy);
+    return hipGetLastError();
+}
+
+}  // namespace golk

@@ -1,0 +1,767 @@
+// golhip.hip — the C-ABI of libgolhip.so (include/golhip.h).
+//
+// Host side of the MI355X engine: owns the device boards, sequences the
+// step kernels (gol_kernels.hip) on one HIP stream, exchanges halo rows with
+// the neighbouring strips (RCCL ring or peer copies) and serves the side
+// channels (alive count, flip list, alive list, snapshots).
+//
+// What each entry point replaces in the reference (gol/distributor.go):
+//   golhip_create / _load_bytes  world allocation + fill          :66-80
+//   golhip_step                  the turn loop                    :93-173
+//   golhip_flips                 initializeAliveCells             :212-220
+//   golhip_alive_count           len(calculateAliveCells) ticker  :283-302
+//   golhip_alive_cells           calculateAliveCells (final)      :180, :420-432
+//   golhip_snapshot_bytes        final/s/q raster streams         :186-191, :234-238
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/golhip.h"
+#include "gol_kernels.h"
+
+using golk::kHalo;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_OR_FAIL(expr)                                                                      \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess) return fail(GOLHIP_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+// Accumulating form for loops that must finish their cleanup: sets `rc` once.
+#define HIP_RC(expr)                                                                            \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess && rc == GOLHIP_OK)                                                \
+            rc = fail(GOLHIP_EHIP, "%s: %s", #expr, hipGetErrorString(e_));                     \
+    } while (0)
+
+#define NCCL_OR_FAIL(expr)                                                                          \
+    do {                                                                                            \
+        ncclResult_t r_ = (expr);                                                                   \
+        if (r_ != ncclSuccess) return fail(GOLHIP_ERCCL, "%s: %s", #expr, ncclGetErrorString(r_)); \
+    } while (0)
+
+constexpr int kDepths[] = {32, 16, 8, 4, 2, 1};
+
+}  // namespace
+
+struct golhip {
+    int W = 0, H = 0, Ww = 0;
+    int row0 = 0, rows = 0;  // this handle's rows of the torus
+    bool strip = false;      // created by golhip_create_strip
+    int device = 0;
+    uint32_t flags = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+
+    uint32_t *buf[2] = {nullptr, nullptr};
+    int cur = 0;
+    int64_t phys_rows = 0;
+
+    int tb_depth = 16;
+    int rows_per_wave = 512;
+    bool loaded = false;
+    std::atomic<int64_t> turns{0};
+
+    // side-channel scratch
+    unsigned long long *d_scalars = nullptr;  // [0] alive, [1] compaction total, [2] hash
+    unsigned long long *h_scalars = nullptr;  // pinned mirror
+    int64_t alive_turn = -1;                  // turn whose count sits in d_scalars[0]
+    unsigned long long *d_blk = nullptr;
+    int64_t blk_cap = 0;
+    int32_t *d_xy = nullptr;
+    int64_t xy_cap = 0;
+    uint8_t *d_stage = nullptr;  // byte staging for load/snapshot
+    int64_t stage_cap = 0;
+    bool flips_valid = false;
+    int64_t flips_turn = -1;
+
+    // ring
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+
+    // measurement
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
+    double step_ms = 0;
+    int64_t step_launches = 0, step_turns = 0, halo_bytes = 0;
+
+    std::mutex mu;
+
+    int64_t local_words() const { return (int64_t)rows * Ww; }
+    uint32_t *cur_rows() const { return buf[cur] + (int64_t)kHalo * Ww; }
+    uint32_t *prev_rows() const { return buf[cur ^ 1] + (int64_t)kHalo * Ww; }
+    bool torus() const { return nranks == 1 && rows == H; }
+};
+
+// ---------------------------------------------------------------------------
+// helpers
+// ---------------------------------------------------------------------------
+namespace {
+
+int check(golhip_t h) {
+    if (!h) return fail(GOLHIP_EINVAL, "null handle");
+    return GOLHIP_OK;
+}
+
+int set_dev(golhip_t h) {
+    HIP_OR_FAIL(hipSetDevice(h->device));
+    return GOLHIP_OK;
+}
+
+int ensure_stage(golhip_t h, int64_t bytes) {
+    if (h->stage_cap >= bytes) return GOLHIP_OK;
+    if (h->d_stage) HIP_OR_FAIL(hipFree(h->d_stage));
+    h->d_stage = nullptr;
+    h->stage_cap = 0;
+    HIP_OR_FAIL(hipMalloc(&h->d_stage, (size_t)bytes));
+    h->stage_cap = bytes;
+    return GOLHIP_OK;
+}
+
+int ensure_blk(golhip_t h, int64_t n) {
+    if (h->blk_cap >= n) return GOLHIP_OK;
+    if (h->d_blk) HIP_OR_FAIL(hipFree(h->d_blk));
+    h->d_blk = nullptr;
+    h->blk_cap = 0;
+    HIP_OR_FAIL(hipMalloc(&h->d_blk, (size_t)std::max<int64_t>(n, 1) * sizeof(unsigned long long)));
+    h->blk_cap = n;
+    return GOLHIP_OK;
+}
+
+int ensure_xy(golhip_t h, int64_t n) {
+    if (h->xy_cap >= n) return GOLHIP_OK;
+    if (h->d_xy) HIP_OR_FAIL(hipFree(h->d_xy));
+    h->d_xy = nullptr;
+    h->xy_cap = 0;
+    const int64_t cap = std::max<int64_t>(n, 4096);
+    HIP_OR_FAIL(hipMalloc(&h->d_xy, (size_t)cap * 2 * sizeof(int32_t)));
+    h->xy_cap = cap;
+    return GOLHIP_OK;
+}
+
+// Rows per launch chunk for byte staging (<= 64 MiB of bytes).
+int64_t stage_rows(golhip_t h) {
+    const int64_t per = std::max<int64_t>(1, (64ll << 20) / std::max(1, h->W));
+    return std::min<int64_t>(per, h->rows);
+}
+
+int largest_depth(int64_t want) {
+    for (int d : kDepths)
+        if (d <= want) return d;
+    return 1;
+}
+
+// How many turns the next launch fuses.  In halo mode the `depth` halo rows
+// must all come from one neighbour strip, so depth <= strip rows.
+int next_depth(golhip_t h, int64_t remaining, bool halo) {
+    if (h->W % 32 != 0) return 1;  // generic kernel: one turn per launch
+    int64_t cap = std::min<int64_t>(h->tb_depth, remaining);
+    if (halo) cap = std::min<int64_t>(cap, h->rows);
+    return largest_depth(cap);
+}
+
+// torus mode: the handle holds the whole board and wraps rows itself;
+// halo mode: rows outside the strip come from the halo rows.
+golk::StepArgs step_args(golhip_t h, unsigned long long *alive, bool halo) {
+    golk::StepArgs a{};
+    a.src = h->buf[h->cur];
+    a.dst = h->buf[h->cur ^ 1];
+    a.W = h->W;
+    a.Ww = h->Ww;
+    a.rows_out = h->rows;
+    a.dst_base = kHalo;
+    if (!halo) {
+        a.in.base = kHalo;
+        a.in.wrap = h->H;
+        a.in.off = 0;
+        a.in.rmax = h->H - 1;
+    } else {
+        a.in.base = 0;
+        a.in.wrap = 0;
+        a.in.off = kHalo;
+        a.in.rmax = (int)h->phys_rows - 1;
+    }
+    a.rows_per_wave = h->rows_per_wave;
+    a.alive = alive;
+    return a;
+}
+
+hipEvent_t take_event(golhip_t h) {
+    if (!h->ev_pool.empty()) {
+        hipEvent_t e = h->ev_pool.back();
+        h->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+int drain_events(golhip_t h) {
+    for (auto &p : h->ev_pending) {
+        HIP_OR_FAIL(hipEventSynchronize(p.second));
+        float ms = 0;
+        HIP_OR_FAIL(hipEventElapsedTime(&ms, p.first, p.second));
+        h->step_ms += ms;
+        h->ev_pool.push_back(p.first);
+        h->ev_pool.push_back(p.second);
+    }
+    h->ev_pending.clear();
+    return GOLHIP_OK;
+}
+
+// Halo plan shared by the RCCL ring and the in-process group.
+void plan(int strip_rows, int nranks, int rank, int depth, int Ww, golhip_halo_plan_t *p) {
+    p->prev_rank = (rank - 1 + nranks) % nranks;
+    p->next_rank = (rank + 1) % nranks;
+    p->rows = depth;
+    p->send_up_row = kHalo;                               // my first `depth` rows -> prev's bottom halo
+    p->recv_bottom_row = kHalo + strip_rows;              // <- next's first rows
+    p->send_down_row = kHalo + strip_rows - depth;        // my last rows -> next's top halo
+    p->recv_top_row = kHalo - depth;                      // <- prev's last rows
+    p->bytes = (int64_t)depth * Ww * 4;
+}
+
+// RCCL halo exchange for a launch of `depth` turns.  Posting order pairs
+// correctly even when prev == next (2 ranks): on every A->B channel the
+// first message is A's top rows (B's bottom halo), the second A's bottom rows.
+int exchange_rccl(golhip_t h, int depth) {
+    golhip_halo_plan_t p;
+    plan(h->rows, h->nranks, h->rank, depth, h->Ww, &p);
+    uint32_t *b = h->buf[h->cur];
+    const size_t n = (size_t)depth * h->Ww;
+    NCCL_OR_FAIL(ncclGroupStart());
+    NCCL_OR_FAIL(ncclSend(b + (int64_t)p.send_up_row * h->Ww, n, ncclUint32, p.prev_rank, h->comm, h->stream));
+    NCCL_OR_FAIL(ncclRecv(b + (int64_t)p.recv_bottom_row * h->Ww, n, ncclUint32, p.next_rank, h->comm, h->stream));
+    NCCL_OR_FAIL(ncclSend(b + (int64_t)p.send_down_row * h->Ww, n, ncclUint32, p.next_rank, h->comm, h->stream));
+    NCCL_OR_FAIL(ncclRecv(b + (int64_t)p.recv_top_row * h->Ww, n, ncclUint32, p.prev_rank, h->comm, h->stream));
+    NCCL_OR_FAIL(ncclGroupEnd());
+    h->halo_bytes += 2 * (int64_t)n * 4;
+    return GOLHIP_OK;
+}
+
+// One step launch of `depth` turns (halos already in place).
+int launch_depth(golhip_t h, int depth, bool count, bool halo) {
+    unsigned long long *alive = nullptr;
+    if (count) {
+        alive = h->d_scalars;
+        HIP_OR_FAIL(hipMemsetAsync(alive, 0, sizeof(unsigned long long), h->stream));
+    }
+    golk::StepArgs a = step_args(h, alive, halo);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (h->flags & GOLHIP_FLAG_TIMING) {
+        e0 = take_event(h);
+        e1 = take_event(h);
+        if (!e0 || !e1) return fail(GOLHIP_EHIP, "hipEventCreate failed");
+        HIP_OR_FAIL(hipEventRecord(e0, h->stream));
+    }
+    hipError_t e;
+    if (h->W % 32 == 0)
+        e = golk::launch_step_tb(a, depth, h->stream);
+    else
+        e = golk::launch_step_generic(a, h->stream);
+    if (e != hipSuccess) return fail(GOLHIP_EHIP, "step launch: %s", hipGetErrorString(e));
+    if (e1) {
+        HIP_OR_FAIL(hipEventRecord(e1, h->stream));
+        h->ev_pending.emplace_back(e0, e1);
+        if (h->ev_pending.size() >= 4096) {
+            int rc = drain_events(h);
+            if (rc) return rc;
+        }
+    }
+    h->cur ^= 1;
+    h->turns += depth;
+    h->step_launches++;
+    h->step_turns += depth;
+    if (count) h->alive_turn = h->turns;
+    return GOLHIP_OK;
+}
+
+int start_flips(golhip_t h) {
+    const int64_t nw = h->local_words();
+    const int64_t nb = golk::compact_blocks(nw);
+    int rc = ensure_blk(h, nb);
+    if (rc) return rc;
+    HIP_OR_FAIL(golk::launch_compact_count(h->cur_rows(), h->prev_rows(), nw, h->d_blk, h->stream));
+    HIP_OR_FAIL(golk::launch_compact_scan(h->d_blk, nb, h->d_scalars + 1, h->stream));
+    h->flips_valid = true;
+    h->flips_turn = h->turns;
+    return GOLHIP_OK;
+}
+
+// Finish a compaction started with count+scan: read the total, scatter, copy out.
+int finish_compact(golhip_t h, const uint32_t *a, const uint32_t *b, int32_t *xy, uint64_t cap, uint64_t *n) {
+    HIP_OR_FAIL(hipMemcpyAsync(h->h_scalars + 1, h->d_scalars + 1, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                               h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    const uint64_t total = h->h_scalars[1];
+    if (n) *n = total;
+    if (total > cap || (!xy && total > 0))
+        return fail(GOLHIP_ERANGE, "buffer holds %llu cells, %llu needed", (unsigned long long)cap,
+                    (unsigned long long)total);
+    if (total == 0) return GOLHIP_OK;
+    int rc = ensure_xy(h, (int64_t)total);
+    if (rc) return rc;
+    HIP_OR_FAIL(golk::launch_compact_scatter(a, b, h->local_words(), h->Ww, h->row0, h->d_blk, h->d_xy, h->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(xy, h->d_xy, total * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    return GOLHIP_OK;
+}
+
+int create_common(int32_t width, int32_t height, int32_t row0, int32_t rows, int32_t device, uint32_t flags,
+                  bool strip, golhip_t *out) {
+    if (!out) return fail(GOLHIP_EINVAL, "out is null");
+    *out = nullptr;
+    if (width <= 0 || height <= 0) return fail(GOLHIP_EINVAL, "bad board %dx%d", width, height);
+    if (rows <= 0 || row0 < 0 || (int64_t)row0 + rows > height)
+        return fail(GOLHIP_EINVAL, "bad strip rows [%d, %d) of %d", row0, row0 + rows, height);
+    int ndev = 0;
+    HIP_OR_FAIL(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(GOLHIP_EINVAL, "device %d of %d", device, ndev);
+    HIP_OR_FAIL(hipSetDevice(device));
+    golhip *h = new golhip();
+    h->W = width;
+    h->H = height;
+    h->Ww = (width + 31) / 32;
+    h->row0 = row0;
+    h->rows = rows;
+    h->strip = strip;
+    h->device = device;
+    h->flags = flags;
+    h->phys_rows = (int64_t)rows + 2 * kHalo;
+    const size_t bytes = (size_t)h->phys_rows * h->Ww * sizeof(uint32_t);
+    hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) h->own_stream = true;
+    if (e == hipSuccess) e = hipMalloc(&h->buf[0], bytes);
+    if (e == hipSuccess) e = hipMalloc(&h->buf[1], bytes);
+    if (e == hipSuccess) e = hipMemset(h->buf[0], 0, bytes);
+    if (e == hipSuccess) e = hipMemset(h->buf[1], 0, bytes);
+    if (e == hipSuccess) e = hipMalloc(&h->d_scalars, 4 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipHostMalloc(&h->h_scalars, 4 * sizeof(unsigned long long), hipHostMallocDefault);
+    if (e != hipSuccess) {
+        int code = (e == hipErrorOutOfMemory) ? GOLHIP_ENOMEM : GOLHIP_EHIP;
+        fail(code, "allocating %zu bytes x2: %s", bytes, hipGetErrorString(e));
+        golhip_destroy(h);
+        return code;
+    }
+    *out = h;
+    return GOLHIP_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char *golhip_version(void) { return "golhip 0.1 (gfx950)"; }
+
+const char *golhip_last_error(void) { return g_err.c_str(); }
+
+int golhip_device_count(int32_t *n) {
+    if (!n) return fail(GOLHIP_EINVAL, "n is null");
+    int c = 0;
+    HIP_OR_FAIL(hipGetDeviceCount(&c));
+    *n = c;
+    return GOLHIP_OK;
+}
+
+int golhip_create(int32_t width, int32_t height, int32_t device, uint32_t flags, golhip_t *out) {
+    return create_common(width, height, 0, height, device, flags, false, out);
+}
+
+int golhip_create_strip(int32_t width, int32_t height, int32_t row0, int32_t rows, int32_t device, uint32_t flags,
+                        golhip_t *out) {
+    return create_common(width, height, row0, rows, device, flags, true, out);
+}
+
+int golhip_destroy(golhip_t h) {
+    if (!h) return GOLHIP_OK;
+    int rc = GOLHIP_OK;
+    HIP_RC(hipSetDevice(h->device));
+    if (h->stream) HIP_RC(hipStreamSynchronize(h->stream));
+    for (auto &p : h->ev_pending) {
+        HIP_RC(hipEventDestroy(p.first));
+        HIP_RC(hipEventDestroy(p.second));
+    }
+    for (auto e : h->ev_pool) HIP_RC(hipEventDestroy(e));
+    if (h->comm && ncclCommDestroy(h->comm) != ncclSuccess && rc == GOLHIP_OK)
+        rc = fail(GOLHIP_ERCCL, "ncclCommDestroy failed");
+    HIP_RC(hipFree(h->buf[0]));
+    HIP_RC(hipFree(h->buf[1]));
+    HIP_RC(hipFree(h->d_scalars));
+    if (h->h_scalars) HIP_RC(hipHostFree(h->h_scalars));
+    HIP_RC(hipFree(h->d_blk));
+    HIP_RC(hipFree(h->d_xy));
+    HIP_RC(hipFree(h->d_stage));
+    if (h->own_stream && h->stream) HIP_RC(hipStreamDestroy(h->stream));
+    delete h;
+    return rc;
+}
+
+int golhip_set_stream(golhip_t h, void *s) {
+    if (int rc = check(h)) return rc;
+    std::lock_guard<std::mutex> g(h->mu);
+    if (int rc = set_dev(h)) return rc;
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (h->own_stream) HIP_OR_FAIL(hipStreamDestroy(h->stream));
+    h->own_stream = false;
+    h->stream = (hipStream_t)s;
+    return GOLHIP_OK;
+}
+
+void *golhip_stream(golhip_t h) { return h ? (void *)h->stream : nullptr; }
+
+int golhip_set_tb_depth(golhip_t h, int32_t t) {
+    if (int rc = check(h)) return rc;
+    if (t < 1 || t > GOLHIP_MAX_TB_DEPTH) return fail(GOLHIP_EINVAL, "tb depth %d not in 1..%d", t, GOLHIP_MAX_TB_DEPTH);
+    std::lock_guard<std::mutex> g(h->mu);
+    h->tb_depth = t;
+    return GOLHIP_OK;
+}
+
+int golhip_set_rows_per_wave(golhip_t h, int32_t r) {
+    if (int rc = check(h)) return rc;
+    if (r < 1) return fail(GOLHIP_EINVAL, "rows per wave %d", r);
+    std::lock_guard<std::mutex> g(h->mu);
+    h->rows_per_wave = r;
+    return GOLHIP_OK;
+}
+
+int golhip_comm_unique_id(uint8_t id[GOLHIP_UNIQUE_ID_BYTES]) {
+    static_assert(sizeof(ncclUniqueId) == GOLHIP_UNIQUE_ID_BYTES, "ncclUniqueId size");
+    if (!id) return fail(GOLHIP_EINVAL, "id is null");
+    ncclUniqueId u;
+    NCCL_OR_FAIL(ncclGetUniqueId(&u));
+    memcpy(id, &u, sizeof u);
+    return GOLHIP_OK;
+}
+
+int golhip_comm_init(golhip_t h, const uint8_t id[GOLHIP_UNIQUE_ID_BYTES], int32_t nranks, int32_t rank) {
+    if (int rc = check(h)) return rc;
+    if (!id || nranks < 1 || rank < 0 || rank >= nranks) return fail(GOLHIP_EINVAL, "rank %d of %d", rank, nranks);
+    std::lock_guard<std::mutex> g(h->mu);
+    if (int rc = set_dev(h)) return rc;
+    if (h->comm) return fail(GOLHIP_EINVAL, "comm already initialised");
+    if (nranks > 1 && h->rows < 1) return fail(GOLHIP_EINVAL, "empty strip");
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof u);
+    NCCL_OR_FAIL(ncclCommInitRank(&h->comm, nranks, u, rank));
+    h->nranks = nranks;
+    h->rank = rank;
+    return GOLHIP_OK;
+}
+
+int golhip_halo_plan(int32_t width, int32_t strip_rows, int32_t nranks, int32_t rank, int32_t depth,
+                     golhip_halo_plan_t *out) {
+    if (!out || width <= 0 || strip_rows <= 0 || nranks < 1 || rank < 0 || rank >= nranks || depth < 1 ||
+        depth > GOLHIP_MAX_TB_DEPTH || depth > strip_rows)
+        return fail(GOLHIP_EINVAL, "bad halo plan request");
+    plan(strip_rows, nranks, rank, depth, (width + 31) / 32, out);
+    return GOLHIP_OK;
+}
+
+int golhip_load_bytes(golhip_t h, const uint8_t *cells) {
+    if (int rc = check(h)) return rc;
+    if (!cells) return fail(GOLHIP_EINVAL, "cells is null");
+    std::lock_guard<std::mutex> g(h->mu);
+    if (int rc = set_dev(h)) return rc;
+    const int64_t chunk = stage_rows(h);
+    if (int rc = ensure_stage(h, chunk * h->W)) return rc;
+    for (int64_t r = 0; r < h->rows; r += chunk) {
+        const int64_t n = std::min<int64_t>(chunk, h->rows - r);
+        HIP_OR_FAIL(hipMemcpyAsync(h->d_stage, cells + r * h->W, (size_t)(n * h->W), hipMemcpyHostToDevice, h->stream));
+        HIP_OR_FAIL(golk::launch_pack(h->d_stage, h->cur_rows() + r * h->Ww, h->W, h->Ww, (int)n, h->stream));
+    }
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    h->loaded = true;
+    h->turns = 0;
+    h->alive_turn = -1;
+    h->flips_valid = false;
+    return GOLHIP_OK;
+}
+
+int golhip_load_bits(golhip_t h, const uint32_t *words) {
+    if (int rc = check(h)) return rc;
+    if (!words) return fail(GOLHIP_EINVAL, "words is null");
+    std::lock_guard<std::mutex> g(h->mu);
+    if (int rc = set_dev(h)) return rc;
+    HIP_OR_FAIL(hipMemcpyAsync(h->cur_rows(), words, (size_t)h->local_words() * 4, hipMemcpyHostToDevice, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    h->loaded = true;
+    h->turns = 0;
+    h->alive_turn = -1;
+    h->flips_valid = false;
+    return GOLHIP_OK;
+}
+
+int golhip_fill_random(golhip_t h, uint64_t seed) {
+    if (int rc = check(h)) return rc;
+    std::lock_guard<std::mutex> g(h->mu);
+    if (int rc = set_dev(h)) return rc;
+    HIP_OR_FAIL(golk::launch_fill_random(h->cur_rows(), h->W, h->Ww, h->rows, h->row0, seed, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    h->loaded = true;
+    h->turns = 0;
+    h->alive_turn = -1;
+    h->flips_valid = false;
+    return GOLHIP_OK;
+}
+
+int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
+    if (int rc = check(h)) return rc;
+    if (nturns < 0) return fail(GOLHIP_EINVAL, "nturns %lld", (long long)nturns);
+    std::lock_guard<std::mutex> g(h->mu);
+    if (!h->loaded) return fail(GOLHIP_EINVAL, "no board loaded");
+    if (h->nranks == 1 && !h->torus()) return fail(GOLHIP_EINVAL, "strip handle needs golhip_comm_init or golhip_group_step");
+    if (int rc = set_dev(h)) return rc;
+    h->flips_valid = false;
+    int64_t left = nturns;
+    const int64_t tail = want_flips ? 1 : 0;
+    const bool halo = h->nranks > 1;
+    while (left > tail) {
+        const int d = next_depth(h, left - tail, halo);
+        if (halo)
+            if (int rc = exchange_rccl(h, d)) return rc;
+        if (int rc = launch_depth(h, d, left - d == 0, halo)) return rc;
+        left -= d;
+    }
+    if (want_flips && nturns > 0) {
+        if (halo)
+            if (int rc = exchange_rccl(h, 1)) return rc;
+        if (int rc = launch_depth(h, 1, true, halo)) return rc;
+        if (int rc = start_flips(h)) return rc;
+    }
+    return GOLHIP_OK;
+}
+
+int golhip_group_step(golhip_t *hs, int32_t n, int64_t nturns) {
+    if (!hs || n < 1 || nturns < 0) return fail(GOLHIP_EINVAL, "bad group");
+    for (int i = 0; i < n; ++i) {
+        if (int rc = check(hs[i])) return rc;
+        if (!hs[i]->loaded) return fail(GOLHIP_EINVAL, "strip %d has no board", i);
+        if (hs[i]->W != hs[0]->W || hs[i]->H != hs[0]->H || hs[i]->nranks != 1)
+            return fail(GOLHIP_EINVAL, "strip %d does not belong to the group", i);
+        const int expect_row0 = i == 0 ? 0 : hs[i - 1]->row0 + hs[i - 1]->rows;
+        if (hs[i]->row0 != expect_row0) return fail(GOLHIP_EINVAL, "strip %d starts at %d, expected %d", i, hs[i]->row0, expect_row0);
+    }
+    if (hs[n - 1]->row0 + hs[n - 1]->rows != hs[0]->H) return fail(GOLHIP_EINVAL, "strips do not cover the board");
+    std::vector<std::unique_lock<std::mutex>> locks;
+    for (int i = 0; i < n; ++i) locks.emplace_back(hs[i]->mu);
+    std::vector<hipEvent_t> ready(n, nullptr);
+    int rc = GOLHIP_OK;
+    for (int i = 0; i < n; ++i) {
+        HIP_RC(hipSetDevice(hs[i]->device));
+        HIP_RC(hipEventCreateWithFlags(&ready[i], hipEventDisableTiming));
+        hs[i]->flips_valid = false;
+    }
+    int64_t left = nturns;
+    while (left > 0 && rc == GOLHIP_OK) {
+        int d = GOLHIP_MAX_TB_DEPTH;
+        for (int i = 0; i < n; ++i) d = std::min(d, next_depth(hs[i], left, n > 1));
+        d = largest_depth(d);
+        if (n > 1) {
+            for (int i = 0; i < n && !rc; ++i) {
+                HIP_RC(hipSetDevice(hs[i]->device));
+                HIP_RC(hipEventRecord(ready[i], hs[i]->stream));
+            }
+            for (int i = 0; i < n && !rc; ++i) {
+                golhip *me = hs[i], *prev = hs[(i - 1 + n) % n], *next = hs[(i + 1) % n];
+                golhip_halo_plan_t p;
+                plan(me->rows, n, i, d, me->Ww, &p);
+                HIP_RC(hipSetDevice(me->device));
+                HIP_RC(hipStreamWaitEvent(me->stream, ready[(i - 1 + n) % n], 0));
+                HIP_RC(hipStreamWaitEvent(me->stream, ready[(i + 1) % n], 0));
+                const size_t bytes = (size_t)p.bytes;
+                // top halo <- prev's last d rows; bottom halo <- next's first d rows
+                uint32_t *mb = me->buf[me->cur];
+                const uint32_t *pb = prev->buf[prev->cur] + (int64_t)(kHalo + prev->rows - d) * prev->Ww;
+                const uint32_t *nb = next->buf[next->cur] + (int64_t)kHalo * next->Ww;
+                HIP_RC(hipMemcpyPeerAsync(mb + (int64_t)p.recv_top_row * me->Ww, me->device, pb, prev->device, bytes,
+                                          me->stream));
+                HIP_RC(hipMemcpyPeerAsync(mb + (int64_t)p.recv_bottom_row * me->Ww, me->device, nb, next->device,
+                                          bytes, me->stream));
+                me->halo_bytes += 2 * (int64_t)bytes;
+            }
+        }
+        for (int i = 0; i < n && !rc; ++i) {
+            HIP_RC(hipSetDevice(hs[i]->device));
+            if (!rc) rc = launch_depth(hs[i], d, left - d == 0, n > 1);
+        }
+        left -= d;
+    }
+    for (int i = 0; i < n; ++i) {
+        HIP_RC(hipSetDevice(hs[i]->device));
+        if (ready[i]) {
+            HIP_RC(hipStreamSynchronize(hs[i]->stream));
+            HIP_RC(hipEventDestroy(ready[i]));
+        }
+    }
+    return rc;
+}
+
+int golhip_sync(golhip_t h) {
+    if (int rc = check(h)) return rc;
+    std::lock_guard<std::mutex> g(h->mu);
+    if (int rc = set_dev(h)) return rc;
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    return GOLHIP_OK;
+}
+
+int golhip_turn(golhip_t h, int64_t *t) {
+    if (int rc = check(h)) return rc;
+    if (!t) return fail(GOLHIP_EINVAL, "null out");
+    *t = h->turns.load();
+    return GOLHIP_OK;
+}
+
+int golhip_alive_count(golhip_t h, uint64_t *count, int64_t *at_turn) {
+    if (int rc = check(h)) return rc;
+    if (!count) return fail(GOLHIP_EINVAL, "null out");
+    std::lock_guard<std::mutex> g(h->mu);
+    if (int rc = set_dev(h)) return rc;
+    if (h->alive_turn != h->turns) {
+        HIP_OR_FAIL(hipMemsetAsync(h->d_scalars, 0, sizeof(unsigned long long), h->stream));
+        HIP_OR_FAIL(golk::launch_popcount(h->cur_rows(), h->local_words(), h->d_scalars, h->stream));
+        h->alive_turn = h->turns;
+    }
+    HIP_OR_FAIL(hipMemcpyAsync(h->h_scalars, h->d_scalars, sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    *count = h->h_scalars[0];
+    if (at_turn) *at_turn = h->alive_turn;
+    return GOLHIP_OK;
+}
+
+int golhip_alive_count_global(golhip_t h, uint64_t *count, int64_t *at_turn) {
+    if (int rc = golhip_alive_count(h, count, at_turn)) return rc;
+    if (h->nranks == 1 || !h->comm) return GOLHIP_OK;
+    std::lock_guard<std::mutex> g(h->mu);
+    HIP_OR_FAIL(hipMemcpyAsync(h->d_scalars + 3, h->d_scalars, sizeof(unsigned long long), hipMemcpyDeviceToDevice,
+                               h->stream));
+    NCCL_OR_FAIL(ncclAllReduce(h->d_scalars + 3, h->d_scalars + 3, 1, ncclUint64, ncclSum, h->comm, h->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(h->h_scalars + 3, h->d_scalars + 3, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                               h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    *count = h->h_scalars[3];
+    return GOLHIP_OK;
+}
+
+int golhip_flips(golhip_t h, int32_t *xy, uint64_t cap, uint64_t *n) {
+    if (int rc = check(h)) return rc;
+    std::lock_guard<std::mutex> g(h->mu);
+    if (int rc = set_dev(h)) return rc;
+    if (!h->flips_valid || h->flips_turn != h->turns) {
+        if (n) *n = 0;
+        return fail(GOLHIP_EINVAL, "no flip list: step with want_flips first");
+    }
+    return finish_compact(h, h->cur_rows(), h->prev_rows(), xy, cap, n);
+}
+
+int golhip_alive_cells(golhip_t h, int32_t *xy, uint64_t cap, uint64_t *n) {
+    if (int rc = check(h)) return rc;
+    std::lock_guard<std::mutex> g(h->mu);
+    if (int rc = set_dev(h)) return rc;
+    const int64_t nw = h->local_words();
+    const int64_t nb = golk::compact_blocks(nw);
+    if (int rc = ensure_blk(h, nb)) return rc;
+    HIP_OR_FAIL(golk::launch_compact_count(h->cur_rows(), nullptr, nw, h->d_blk, h->stream));
+    HIP_OR_FAIL(golk::launch_compact_scan(h->d_blk, nb, h->d_scalars + 1, h->stream));
+    h->flips_valid = false;  // d_blk reused
+    return finish_compact(h, h->cur_rows(), nullptr, xy, cap, n);
+}
+
+int golhip_snapshot_bytes(golhip_t h, uint8_t *out) {
+    if (int rc = check(h)) return rc;
+    if (!out) return fail(GOLHIP_EINVAL, "out is null");
+    std::lock_guard<std::mutex> g(h->mu);
+    if (int rc = set_dev(h)) return rc;
+    const int64_t chunk = stage_rows(h);
+    if (int rc = ensure_stage(h, chunk * h->W)) return rc;
+    for (int64_t r = 0; r < h->rows; r += chunk) {
+        const int64_t n = std::min<int64_t>(chunk, h->rows - r);
+        HIP_OR_FAIL(golk::launch_unpack(h->cur_rows() + r * h->Ww, h->d_stage, h->W, h->Ww, (int)n, h->stream));
+        HIP_OR_FAIL(hipMemcpyAsync(out + r * h->W, h->d_stage, (size_t)(n * h->W), hipMemcpyDeviceToHost, h->stream));
+    }
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    return GOLHIP_OK;
+}
+
+int golhip_snapshot_bits(golhip_t h, uint32_t *out) {
+    if (int rc = check(h)) return rc;
+    if (!out) return fail(GOLHIP_EINVAL, "out is null");
+    std::lock_guard<std::mutex> g(h->mu);
+    if (int rc = set_dev(h)) return rc;
+    HIP_OR_FAIL(hipMemcpyAsync(out, h->cur_rows(), (size_t)h->local_words() * 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    return GOLHIP_OK;
+}
+
+int golhip_board_hash(golhip_t h, uint64_t *hash) {
+    if (int rc = check(h)) return rc;
+    if (!hash) return fail(GOLHIP_EINVAL, "null out");
+    std::lock_guard<std::mutex> g(h->mu);
+    if (int rc = set_dev(h)) return rc;
+    HIP_OR_FAIL(hipMemsetAsync(h->d_scalars + 2, 0, sizeof(unsigned long long), h->stream));
+    HIP_OR_FAIL(golk::launch_hash(h->cur_rows(), h->local_words(), (int64_t)h->row0 * h->Ww, h->d_scalars + 2, h->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(h->h_scalars + 2, h->d_scalars + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                               h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    *hash = h->h_scalars[2];
+    return GOLHIP_OK;
+}
+
+int golhip_perf(golhip_t h, golhip_perf_t *out) {
+    if (int rc = check(h)) return rc;
+    if (!out) return fail(GOLHIP_EINVAL, "null out");
+    std::lock_guard<std::mutex> g(h->mu);
+    if (int rc = set_dev(h)) return rc;
+    if (int rc = drain_events(h)) return rc;
+    memset(out, 0, sizeof *out);
+    out->turns = h->turns;
+    out->step_launches = h->step_launches;
+    out->step_turns = h->step_turns;
+    out->step_kernel_ms = h->step_ms;
+    out->cell_updates = (int64_t)h->W * h->rows * h->step_turns;
+    out->alg_bytes = out->cell_updates / 4;
+    out->halo_bytes = h->halo_bytes;
+    out->tb_depth = h->tb_depth;
+    out->rows_per_wave = h->rows_per_wave;
+    out->kernel_variant = h->W % 32 == 0 ? 1 : 0;
+    return GOLHIP_OK;
+}
+
+int golhip_perf_reset(golhip_t h) {
+    if (int rc = check(h)) return rc;
+    std::lock_guard<std::mutex> g(h->mu);
+    if (int rc = set_dev(h)) return rc;
+    if (int rc = drain_events(h)) return rc;
+    h->step_ms = 0;
+    h->step_launches = h->step_turns = h->halo_bytes = 0;
+    return GOLHIP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,160 @@
+/*
+ * golhip.h — C-ABI of libgolhip.so, the MI355X engine behind gol.Run.
+ *
+ * The reference's hot path is the per-turn loop of
+ *   gol/distributor.go:93-173  distributor(): serial calculateNextState (:350-379)
+ *                              or the worker pool worker/workerWorld (:304-347),
+ *                              both over checkNeighbour (:382-417);
+ * with its side channels
+ *   gol/distributor.go:212-220 initializeAliveCells  -> CellFlipped events
+ *   gol/distributor.go:420-432 calculateAliveCells   -> FinalTurnComplete.Alive,
+ *                                                       AliveCellsCount (:283-302)
+ *   gol/distributor.go:66-80   world fill from the io goroutine (ioInput)
+ *   gol/distributor.go:180-191 final PGM stream (ioOutput), also s/q (:229-261).
+ * The reference has no FFI of its own (pure Go); these entry points are what a
+ * cgo shim in gol/distributor.go binds in place of those functions
+ * (INTEGRATION.md shows the binding).  Plain pointers and sizes only.
+ *
+ * Board model: a width x height torus, rows are y (0..height-1), columns x.
+ * Byte boards are row-major height x width, alive <=> byte == 255 (the
+ * reference's test `world[x][y] == 255`, distributor.go:363, :411); byte
+ * outputs are 0 / 255.  Bit boards are row-major, ceil(width/32) uint32 words
+ * per row, cell (y, x) = bit x%32 of word x/32 (padding bits zero).
+ *
+ * Conventions: every function returns 0 (GOLHIP_OK) or a negative GOLHIP_E*
+ * code and sets a thread-local message for golhip_last_error().  Caller-owned
+ * buffers are never retained past the call (cgo pointer rules).  One handle is
+ * driven by one engine thread; golhip_turn and golhip_alive_count may be
+ * called concurrently from another thread (the reference's ticker, :283-302)
+ * and return a (turn, count) pair that belongs together.
+ */
+#ifndef GOLHIP_H
+#define GOLHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GOLHIP_OK 0
+#define GOLHIP_EINVAL (-1)  /* bad argument (size, pointer, state)            */
+#define GOLHIP_EHIP (-2)    /* HIP runtime error                              */
+#define GOLHIP_ENOMEM (-3)  /* device or host allocation failed               */
+#define GOLHIP_ERANGE (-4)  /* caller buffer too small (required size is set) */
+#define GOLHIP_ERCCL (-5)   /* RCCL error                                     */
+
+/* golhip_create flags */
+#define GOLHIP_FLAG_TIMING 0x1u /* time every step kernel with HIP events     */
+
+#define GOLHIP_UNIQUE_ID_BYTES 128 /* == sizeof(ncclUniqueId)                 */
+#define GOLHIP_MAX_TB_DEPTH 32     /* max turns fused in one step launch      */
+
+typedef struct golhip golhip;
+typedef golhip *golhip_t;
+
+typedef struct golhip_perf {
+    int64_t turns;            /* turns completed since the last load/fill     */
+    int64_t step_launches;    /* step-kernel launches since golhip_perf_reset */
+    int64_t step_turns;       /* turns run by those launches                  */
+    double step_kernel_ms;    /* summed device time of those launches (TIMING)*/
+    int64_t cell_updates;     /* width * local rows * step_turns              */
+    int64_t alg_bytes;        /* 0.25 B per cell-update (1 bit in + 1 bit out)*/
+    int64_t halo_bytes;       /* bytes sent to neighbour ranks                */
+    int32_t tb_depth;         /* turns fused per step launch                  */
+    int32_t rows_per_wave;    /* rows streamed by one wavefront per launch    */
+    int32_t kernel_variant;   /* 0 = generic (width % 32 != 0), 1 = bit-sliced*/
+    int32_t reserved;
+} golhip_perf_t;
+
+/* ---- library ---------------------------------------------------------- */
+const char *golhip_version(void);
+const char *golhip_last_error(void);
+int golhip_device_count(int32_t *n);
+
+/* ---- handles ---------------------------------------------------------- */
+/* Whole width x height torus on one device.  Replaces the world allocation
+ * of distributor.go:66-69. */
+int golhip_create(int32_t width, int32_t height, int32_t device, uint32_t flags, golhip_t *out);
+
+/* Row strip [row0, row0 + rows) of a width x height torus (multi-GPU row-strip
+ * decomposition, README halo-exchange extension).  Its halo rows come from
+ * the neighbouring strips through golhip_comm_init (one process per GPU, RCCL)
+ * or golhip_group_step (several strips driven by one process). */
+int golhip_create_strip(int32_t width, int32_t height, int32_t row0, int32_t rows, int32_t device,
+                        uint32_t flags, golhip_t *out);
+int golhip_destroy(golhip_t h);
+
+/* Run on a caller-provided hipStream_t (e.g. torch.cuda.current_stream()). */
+int golhip_set_stream(golhip_t h, void *hip_stream);
+void *golhip_stream(golhip_t h);
+
+/* Tuning: turns fused per launch (1..GOLHIP_MAX_TB_DEPTH) and rows streamed
+ * per wavefront.  Results never depend on them. */
+int golhip_set_tb_depth(golhip_t h, int32_t turns);
+int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
+
+/* ---- multi-GPU -------------------------------------------------------- */
+/* RCCL ring of strips: rank r's neighbours are r-1 (rows above) and r+1
+ * (rows below), mod nranks (toroidal wrap).  id comes from rank 0's
+ * golhip_comm_unique_id, broadcast by the caller. */
+int golhip_comm_unique_id(uint8_t id[GOLHIP_UNIQUE_ID_BYTES]);
+int golhip_comm_init(golhip_t h, const uint8_t id[GOLHIP_UNIQUE_ID_BYTES], int32_t nranks, int32_t rank);
+
+/* Steps n strips (ring order = array order) driven from one process; halos
+ * move with peer/device copies.  Same semantics as golhip_step on each. */
+int golhip_group_step(golhip_t *hs, int32_t n, int64_t nturns);
+
+/* Halo plan used by both transports (exposed for tests): rows this strip
+ * sends up/down and receives for a launch of `depth` turns. */
+typedef struct golhip_halo_plan {
+    int32_t prev_rank, next_rank;   /* ring neighbours                       */
+    int32_t send_up_row, recv_top_row;     /* physical buffer rows             */
+    int32_t send_down_row, recv_bottom_row;
+    int32_t rows;                   /* = depth                               */
+    int64_t bytes;                  /* per message                            */
+} golhip_halo_plan_t;
+int golhip_halo_plan(int32_t width, int32_t strip_rows, int32_t nranks, int32_t rank, int32_t depth,
+                     golhip_halo_plan_t *out);
+
+/* ---- board I/O -------------------------------------------------------- */
+/* Load this handle's rows (height x width bytes, or its strip's rows). */
+int golhip_load_bytes(golhip_t h, const uint8_t *cells);
+int golhip_load_bits(golhip_t h, const uint32_t *words);
+/* Synthetic board: cell (y, x) alive <=> (splitmix64(seed ^ (y*width + x)) & 3) == 0,
+ * global coordinates (strips of one board agree). */
+int golhip_fill_random(golhip_t h, uint64_t seed);
+
+/* ---- the turn loop ---------------------------------------------------- */
+/* Enqueue nturns turns (asynchronous).  want_flips != 0 keeps the flip list
+ * of the LAST turn for golhip_flips (initializeAliveCells, :212-220). */
+int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips);
+int golhip_sync(golhip_t h);
+int golhip_turn(golhip_t h, int64_t *turns_done);
+
+/* ---- side channels ---------------------------------------------------- */
+/* Alive cells of this handle's rows at turn *at_turn (len(calculateAliveCells)). */
+int golhip_alive_count(golhip_t h, uint64_t *count, int64_t *at_turn);
+/* Sum over the RCCL ring (equals golhip_alive_count without a comm). */
+int golhip_alive_count_global(golhip_t h, uint64_t *count, int64_t *at_turn);
+/* Cells that changed in the last stepped turn (want_flips), row-major,
+ * (x = col, y = row) pairs in global coordinates.  ERANGE sets *n. */
+int golhip_flips(golhip_t h, int32_t *xy, uint64_t cap, uint64_t *n);
+/* Alive cells, row-major (x = col, y = row) pairs — calculateAliveCells. */
+int golhip_alive_cells(golhip_t h, int32_t *xy, uint64_t cap, uint64_t *n);
+/* Board as 0/255 bytes / bit words (this handle's rows). */
+int golhip_snapshot_bytes(golhip_t h, uint8_t *out);
+int golhip_snapshot_bits(golhip_t h, uint32_t *out);
+/* Order-independent board digest: sum over words of
+ * splitmix64((global_word_index << 32) | word) mod 2^64 (strips add up). */
+int golhip_board_hash(golhip_t h, uint64_t *hash);
+
+/* ---- measurement ------------------------------------------------------ */
+int golhip_perf(golhip_t h, golhip_perf_t *out);
+int golhip_perf_reset(golhip_t h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GOLHIP_H */

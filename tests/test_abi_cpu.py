@@ -1,0 +1,64 @@
+"""CPU-side checks of the C-ABI boundary (no GPU needed).
+
+* libgolhip.so loads and exports every function include/golhip.h declares;
+* the library refuses to run without a HIP device (no silent CPU fallback);
+* the halo plan (shared by the RCCL ring and the in-process strip group) is
+  self-consistent: what rank r sends up lands in rank r-1's bottom halo, etc.
+"""
+import ctypes
+
+import pytest
+
+golhip = pytest.importorskip("golhip")
+
+
+def test_library_exports_every_header_symbol():
+    lib = golhip.load()
+    syms = golhip.header_symbols()
+    assert len(syms) >= 25
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_version_and_error_string():
+    lib = golhip.load()
+    assert b"gfx950" in lib.golhip_version()
+    rc = lib.golhip_create(0, 0, 0, 0, ctypes.byref(ctypes.c_void_p()))
+    assert rc == -1
+    assert b"bad board" in lib.golhip_last_error()
+
+
+def test_no_device_fails_loudly():
+    """On a host without a GPU the product path raises instead of falling back."""
+    try:
+        n = golhip.device_count()
+    except golhip.GolHipError as e:
+        assert e.code == -2
+        with pytest.raises(golhip.GolHipError):
+            golhip.Board(64, 64)
+        return
+    if n == 0:
+        with pytest.raises(golhip.GolHipError):
+            golhip.Board(64, 64)
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 3, 8])
+@pytest.mark.parametrize("depth", [1, 4, 32])
+def test_halo_plan_pairs_up(nranks, depth):
+    rows = 40
+    plans = [golhip.halo_plan(2048, rows, nranks, r, depth) for r in range(nranks)]
+    halo = 32
+    for r, p in enumerate(plans):
+        assert p["prev_rank"] == (r - 1) % nranks and p["next_rank"] == (r + 1) % nranks
+        assert p["rows"] == depth and p["bytes"] == depth * 2048 // 8
+        # my first `depth` rows go up, my last go down
+        assert p["send_up_row"] == halo and p["send_down_row"] == halo + rows - depth
+        # received rows sit directly above / below my rows
+        assert p["recv_top_row"] + depth == halo and p["recv_bottom_row"] == halo + rows
+
+
+def test_halo_plan_rejects_depth_above_strip():
+    with pytest.raises(golhip.GolHipError):
+        golhip.halo_plan(64, 3, 2, 0, 4)
+    with pytest.raises(golhip.GolHipError):
+        golhip.halo_plan(64, 64, 2, 0, 33)

@@ -1,0 +1,291 @@
+"""GPU parity: libgolhip.so (HIP, gfx950) against the oracle and the golden fixtures.
+
+Bar: bit-exact (integer / bit work).  Mirrors the reference's tests:
+  TestGol  (gol_test.go:15-47)  final alive set for 16/64/512 x turns {0,1,100}
+  TestPgm  (pgm_test.go:10-42)  output PGM equals check/images (here: SHA-256 of the bytes)
+  TestAlive(count_test.go:17-69) alive counts vs check/alive/*.csv (every turn 1..10000)
+  TestSdl  (sdl_test.go:93-128)  CellFlipped stream applied to a shadow board
+and adds what the GPU design needs: every fused depth / strip height, odd
+widths, multi-strip (row-strip decomposition) runs and full-size property
+checks (BASELINE configs) through the board digest.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from oracle.oracle import (COracle, alive_cells_np, fill_random_np, flips_np, pack_bits, pgm_bytes, run_np,
+                           step_np, unpack_bits)
+
+pytestmark = pytest.mark.gpu
+
+golhip = pytest.importorskip("golhip")
+
+CHECKS = [(16, 0), (16, 1), (16, 100), (64, 0), (64, 1), (64, 100), (512, 0), (512, 1), (512, 100)]
+DEPTHS = [1, 2, 4, 8, 16, 32]
+
+
+@pytest.fixture(scope="module")
+def coracle():
+    return COracle()
+
+
+def img(fixtures, n):
+    return unpack_bits(fixtures[f"image_{n}"], n)
+
+
+def run_gpu(board, turns, depth=16, rows_per_wave=512):
+    H, W = board.shape
+    with golhip.Board(W, H) as b:
+        b.set_tb_depth(depth)
+        b.set_rows_per_wave(rows_per_wave)
+        b.load_bytes(board)
+        b.step(turns)
+        out = b.snapshot_bytes()
+        cnt, at = b.alive_count()
+        assert at == turns
+        assert cnt == int((out == 255).sum())
+        return out
+
+
+# ---------------------------------------------------------------- TestGol / TestPgm
+@pytest.mark.parametrize("n,t", CHECKS)
+def test_gol_final_alive_cells(fixtures, n, t):
+    """FinalTurnComplete.Alive == golden alive set (gol_test.go:42, :58-86)."""
+    with golhip.Board(n, n) as b:
+        b.load_bytes(img(fixtures, n))
+        b.step(t)
+        got = b.alive_cells()
+    expected = alive_cells_np(unpack_bits(fixtures[f"check_{n}x{t}"], n))
+    assert np.array_equal(got, expected)
+
+
+@pytest.mark.parametrize("n,t", CHECKS)
+def test_pgm_output_bytes(fixtures, manifest, n, t):
+    """out/NxNxT.pgm byte-identical to check/images (io.go:52-81 writer format)."""
+    out = run_gpu(img(fixtures, n), t)
+    assert hashlib.sha256(pgm_bytes(out)).hexdigest() == manifest[f"check_{n}x{t}"]["sha256"]
+
+
+@pytest.mark.parametrize("n", [128, 256])
+@pytest.mark.parametrize("t", [1, 100, 1000])
+def test_unchecked_images_vs_oracle(fixtures, n, t):
+    """128x128 and 256x256 have no goldens in the reference: the oracle is the check."""
+    board = img(fixtures, n)
+    assert np.array_equal(run_gpu(board, t), run_np(board, t))
+
+
+# ---------------------------------------------------------------- TestAlive
+@pytest.mark.parametrize("n", [16, 64, 512])
+def test_alive_counts_every_turn(fixtures, n):
+    """check/alive/NxN.csv at every turn 1..10000, plus count_test's post-10000 rule."""
+    exp = fixtures[f"alive_{n}"]
+    with golhip.Board(n, n) as b:
+        b.load_bytes(img(fixtures, n))
+        assert b.alive_count() == (exp[0], 0)
+        for t in range(1, 10001):
+            b.step(1)
+            cnt, at = b.alive_count()
+            assert at == t and cnt == exp[t], (t, cnt, exp[t])
+        if n == 512:
+            for t in range(10001, 10005):
+                b.step(1)
+                cnt, _ = b.alive_count()
+                assert cnt == (5565 if t % 2 == 0 else 5567)
+
+
+@pytest.mark.parametrize("depth", DEPTHS)
+def test_alive_counts_fused_launches(fixtures, depth):
+    """Counts sampled at fused-launch boundaries (the ticker path) match the CSV."""
+    exp = fixtures["alive_512"]
+    with golhip.Board(512, 512) as b:
+        b.set_tb_depth(depth)
+        b.load_bytes(img(fixtures, 512))
+        t = 0
+        for chunk in [1, 3, 32, 64, 100, 1000, 2800]:
+            b.step(chunk)
+            t += chunk
+            assert b.alive_count() == (exp[t], t)
+
+
+# ---------------------------------------------------------------- TestSdl
+def test_sdl_flip_stream_512(fixtures):
+    """CellFlipped events applied to a shadow board reproduce every alive count
+    (sdl_test.go:58, :107-116); flips also equal the oracle's diff list."""
+    board = img(fixtures, 512)
+    exp = fixtures["alive_512"]
+    shadow = np.zeros((512, 512), dtype=np.uint8)
+    with golhip.Board(512, 512) as b:
+        b.load_bytes(board)
+        init = b.alive_cells()                      # initial CellFlipped (distributor.go:72-80)
+        shadow[init[:, 1], init[:, 0]] ^= 0xFF
+        prev = board
+        for t in range(1, 101):
+            b.step(1, want_flips=True)
+            fl = b.flips()
+            shadow[fl[:, 1], fl[:, 0]] ^= 0xFF
+            assert int((shadow == 255).sum()) == exp[t]
+            nxt = step_np(prev)
+            assert np.array_equal(fl, flips_np(prev, nxt))
+            prev = nxt
+        assert np.array_equal(shadow, b.snapshot_bytes())
+
+
+@pytest.mark.parametrize("n", [64, 256])
+def test_flips_match_oracle_each_turn(fixtures, n):
+    board = img(fixtures, n)
+    with golhip.Board(n, n) as b:
+        b.load_bytes(board)
+        for _ in range(20):
+            nxt = step_np(board)
+            b.step(1, want_flips=True)
+            assert np.array_equal(b.flips(), flips_np(board, nxt))
+            board = nxt
+
+
+def test_flips_after_multi_turn_step(fixtures):
+    """want_flips with n > 1: flips of the last turn only."""
+    board = img(fixtures, 512)
+    with golhip.Board(512, 512) as b:
+        b.load_bytes(board)
+        b.step(37, want_flips=True)
+        a = run_np(board, 36)
+        assert np.array_equal(b.flips(), flips_np(a, step_np(a)))
+
+
+# ---------------------------------------------------------------- kernel geometry sweeps
+@pytest.mark.parametrize("depth", DEPTHS)
+@pytest.mark.parametrize("rpw", [1, 2, 5, 37, 512])
+def test_depth_and_strip_height_invariance(fixtures, depth, rpw):
+    board = img(fixtures, 256)
+    assert np.array_equal(run_gpu(board, 70, depth, rpw), run_np(board, 70))
+
+
+@pytest.mark.parametrize("W,H", [(32, 1), (32, 3), (64, 2), (96, 7), (2016, 9), (1984, 33), (4000 - 4000 % 32, 40),
+                                 (8192, 5), (320, 1000), (6272, 70)])
+@pytest.mark.parametrize("depth", [1, 8, 32])
+def test_random_shapes(W, H, depth):
+    """Widths that are 1..many tiles (62 stored words/tile), heights below the depth."""
+    rng = np.random.default_rng(W * 7 + H)
+    board = np.where(rng.random((H, W)) < 0.3, 255, 0).astype(np.uint8)
+    assert np.array_equal(run_gpu(board, 45, depth, 16), run_np(board, 45))
+
+
+@pytest.mark.parametrize("W,H", [(16, 16), (1, 1), (3, 5), (17, 9), (48, 20), (100, 37), (33, 64)])
+def test_generic_width_kernel(W, H):
+    """Widths that are not a multiple of 32 take the generic kernel."""
+    rng = np.random.default_rng(W + 100 * H)
+    board = np.where(rng.random((H, W)) < 0.35, 255, 0).astype(np.uint8)
+    out = run_gpu(board, 23)
+    assert np.array_equal(out, run_np(board, 23))
+
+
+def test_non_binary_bytes_follow_reference_rule():
+    """alive <=> byte == 255 (distributor.go:363, :411): other values are dead."""
+    rng = np.random.default_rng(5)
+    board = rng.choice(np.array([0, 1, 128, 254, 255], dtype=np.uint8), size=(64, 128))
+    out = run_gpu(board, 3)
+    assert np.array_equal(out, run_np(board, 3))
+
+
+def test_zero_turns_and_empty_board():
+    z = np.zeros((64, 64), dtype=np.uint8)
+    assert np.array_equal(run_gpu(z, 0), z)
+    assert np.array_equal(run_gpu(z, 10), z)
+    with golhip.Board(64, 64) as b:
+        b.load_bytes(z)
+        assert len(b.alive_cells()) == 0
+        b.step(1, want_flips=True)
+        assert len(b.flips()) == 0
+
+
+# ---------------------------------------------------------------- synthetic boards, digest
+def test_fill_random_matches_oracle(coracle):
+    for (W, H, seed) in [(64, 32, 1), (100, 7, 0x5EED0001), (1024, 300, 0x5EED0005)]:
+        with golhip.Board(W, H) as b:
+            b.fill_random(seed)
+            assert np.array_equal(b.snapshot_bytes(), coracle.fill_random(W, H, seed))
+
+
+def test_board_hash_matches_host():
+    rng = np.random.default_rng(9)
+    board = np.where(rng.random((300, 640)) < 0.5, 255, 0).astype(np.uint8)
+    with golhip.Board(640, 300) as b:
+        b.load_bytes(board)
+        assert b.board_hash() == golhip.board_hash_np(pack_bits(board))
+
+
+def test_random_2048_vs_c_oracle(coracle):
+    board = coracle.fill_random(2048, 2048, 0x5EED0001)
+    with golhip.Board(2048, 2048) as b:
+        b.fill_random(0x5EED0001)
+        b.step(40)
+        got = b.snapshot_bytes()
+    assert np.array_equal(got, coracle.run(board, 40))
+
+
+# ---------------------------------------------------------------- row strips (multi-GPU decomposition)
+@pytest.mark.parametrize("splits", [[64], [32, 32], [10, 20, 34], [1, 1, 62], [16, 16, 16, 16]])
+@pytest.mark.parametrize("depth", [1, 4, 32])
+def test_group_strips_equal_single_board(fixtures, splits, depth):
+    """n strips of one torus, halos exchanged every launch, == the whole board."""
+    board = img(fixtures, 64)
+    strips, r = [], 0
+    for rows in splits:
+        s = golhip.Board(64, 64, row0=r, rows=rows)
+        s.set_tb_depth(depth)
+        s.load_bytes(board[r:r + rows])
+        strips.append(s)
+        r += rows
+    golhip.group_step(strips, 100)
+    got = np.concatenate([s.snapshot_bytes() for s in strips])
+    assert np.array_equal(got, unpack_bits(fixtures["check_64x100"], 64))
+    assert sum(s.alive_count()[0] for s in strips) == fixtures["alive_64"][100]
+    digest = sum(s.board_hash() for s in strips) % (1 << 64)
+    assert digest == golhip.board_hash_np(pack_bits(got))
+    for s in strips:
+        s.close()
+
+
+def test_group_strips_large_random_hash():
+    """Config-3 shape in miniature: 8 strips of a 8192^2 torus == one board."""
+    W = H = 8192
+    seed = 0x5EED0002
+    with golhip.Board(W, H) as one:
+        one.fill_random(seed)
+        one.step(64)
+        ref = one.board_hash()
+    strips = [golhip.Board(W, H, row0=i * H // 8, rows=H // 8) for i in range(8)]
+    for s in strips:
+        s.fill_random(seed)
+    golhip.group_step(strips, 64)
+    assert sum(s.board_hash() for s in strips) % (1 << 64) == ref
+    for s in strips:
+        s.close()
+
+
+# ---------------------------------------------------------------- full-size properties
+@pytest.mark.parametrize("N,turns", [(16384, 256), (65536, 32)])
+def test_full_size_depth_invariance(N, turns):
+    """BASELINE configs 2/3 at full size: fused depths 32 / 16 / 1 agree (digest + count)."""
+    res = []
+    for depth in (32, 16, 1):
+        with golhip.Board(N, N) as b:
+            b.set_tb_depth(depth)
+            b.fill_random(0x5EED0001 if N == 16384 else 0x5EED0002)
+            b.step(turns)
+            res.append((b.board_hash(), b.alive_count()))
+    assert res[0] == res[1] == res[2]
+
+
+def test_full_size_fill_sample_rows(coracle):
+    """Sampled rows of the 16384^2 synthetic board equal the host generator."""
+    N, seed = 16384, 0x5EED0001
+    with golhip.Board(N, N) as b:
+        b.fill_random(seed)
+        bits = b.snapshot_bits()
+    for r in (0, 1, 777, N - 1):
+        idx = np.arange(N, dtype=np.uint64) + np.uint64(r * N)
+        from oracle.oracle import splitmix64_np
+        row = np.where((splitmix64_np(np.uint64(seed) ^ idx) & np.uint64(3)) == 0, 255, 0).astype(np.uint8)
+        assert np.array_equal(unpack_bits(bits[r:r + 1], N)[0], row)
