@@ -88,32 +88,44 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 // per 32 cells.  HBM traffic per launch ~ 2 bits per cell (read + write) for
 // DEPTH turns.
 // ---------------------------------------------------------------------------
+// One stage (turn t) for the row entering with role R (R = input index % 3).
 template <int D, int R>
-__device__ __forceinline__ uint32_t push_row(uint32_t x, uint32_t (&h0)[3][D], uint32_t (&h1)[3][D],
-                                             uint32_t (&cc)[3][D]) {
+__device__ __forceinline__ void stage(int t, uint32_t &x, uint32_t (&h0)[3][D], uint32_t (&h1)[3][D],
+                                      uint32_t (&cc)[3][D]) {
     constexpr int N = R;            // slot of the row entering now
     constexpr int C = (R + 2) % 3;  // previous row (the one we emit)
     constexpr int P = (R + 1) % 3;  // the row before it
+    const uint32_t l = from_left_lane(x);
+    const uint32_t r = from_right_lane(x);
+    const uint32_t west = __builtin_amdgcn_alignbit(x, l, 31);  // bit k = cell k-1
+    const uint32_t east = __builtin_amdgcn_alignbit(r, x, 1);   // bit k = cell k+1
+    h0[N][t] = bop<kXor3>(west, x, east);
+    h1[N][t] = bop<kMaj>(west, x, east);
+    const uint32_t u0 = bop<kXor3>(h0[P][t], h0[C][t], h0[N][t]);
+    const uint32_t u1 = bop<kMaj>(h0[P][t], h0[C][t], h0[N][t]);
+    const uint32_t v0 = bop<kXor3>(h1[P][t], h1[C][t], h1[N][t]);
+    const uint32_t v1 = bop<kMaj>(h1[P][t], h1[C][t], h1[N][t]);
+    const uint32_t t1 = bop<kT1>(u1, v0, v1);
+    const uint32_t t2 = bop<kT2>(u1, v0, v1);
+    const uint32_t born = bop<kBorn>(cc[C][t], t2, u0);
+    const uint32_t nx = bop<kNext>(u0, t1, born);
+    cc[N][t] = x;
+    x = nx;
+}
+
+// A group of 3 consecutive input rows through all D stages.  Stage t of row
+// i+1 needs stage t of row i (its row sum), so the rows run skewed by one
+// stage: (row0, t), (row1, t-1), (row2, t-2) are independent and interleave,
+// which hides the VALU->DPP hazard of each stage's serial chain.
+template <int D>
+__device__ __forceinline__ void push_group(uint32_t &x0, uint32_t &x1, uint32_t &x2, uint32_t (&h0)[3][D],
+                                           uint32_t (&h1)[3][D], uint32_t (&cc)[3][D]) {
 #pragma unroll
-    for (int t = 0; t < D; ++t) {
-        const uint32_t l = from_left_lane(x);
-        const uint32_t r = from_right_lane(x);
-        const uint32_t west = __builtin_amdgcn_alignbit(x, l, 31);  // bit k = cell k-1
-        const uint32_t east = __builtin_amdgcn_alignbit(r, x, 1);   // bit k = cell k+1
-        h0[N][t] = bop<kXor3>(west, x, east);
-        h1[N][t] = bop<kMaj>(west, x, east);
-        const uint32_t u0 = bop<kXor3>(h0[P][t], h0[C][t], h0[N][t]);
-        const uint32_t u1 = bop<kMaj>(h0[P][t], h0[C][t], h0[N][t]);
-        const uint32_t v0 = bop<kXor3>(h1[P][t], h1[C][t], h1[N][t]);
-        const uint32_t v1 = bop<kMaj>(h1[P][t], h1[C][t], h1[N][t]);
-        const uint32_t t1 = bop<kT1>(u1, v0, v1);
-        const uint32_t t2 = bop<kT2>(u1, v0, v1);
-        const uint32_t born = bop<kBorn>(cc[C][t], t2, u0);
-        const uint32_t nx = bop<kNext>(u0, t1, born);
-        cc[N][t] = x;
-        x = nx;
+    for (int s = 0; s < D + 2; ++s) {
+        if (s < D) stage<D, 0>(s, x0, h0, h1, cc);
+        if (s >= 1 && s - 1 < D) stage<D, 1>(s - 1, x1, h0, h1, cc);
+        if (s >= 2 && s - 2 < D) stage<D, 2>(s - 2, x2, h0, h1, cc);
     }
-    return x;
 }
 
 template <int D>
@@ -134,8 +146,6 @@ __global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
     const bool keep = lane >= 1 && lane <= kTileValid && (t0 + lane - 1) < Ww;
 
     const int rows_here = min(S, a.rows_out - r0);
-    const int n_in = rows_here + 2 * D;
-    const int n_groups = (n_in + 2) / 3;
 
     // input row cursor (wave-uniform)
     int r = r0 - D + a.in.off;
@@ -152,8 +162,19 @@ __global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
         return v;
     };
 
-    uint32_t *__restrict__ dp = a.dst + (size_t)(a.dst_base + r0) * Ww + col;
+    // Output rows are stored unconditionally so the whole 3-row group is one
+    // basic block (the scheduler can then overlap stage t of row i+1 with
+    // stage t+1 of row i): pipeline-fill rows and halo lanes write to a dummy
+    // address in physical row 0, a halo row that is never an output.
+    uint32_t *const dst_row0 = a.dst + (size_t)(a.dst_base + r0) * Ww + col;
+    uint32_t *const dummy = a.dst + col;
     uint32_t cnt = 0;
+    auto emit = [&](uint32_t y, int out_idx) {
+        const bool ok = keep && (unsigned)out_idx < (unsigned)rows_here;
+        uint32_t *p = ok ? dst_row0 + (ptrdiff_t)out_idx * Ww : dummy;
+        *p = y;
+        cnt += ok ? (uint32_t)__builtin_popcount(y) : 0u;
+    };
 
     uint32_t h0[3][D], h1[3][D], cc[3][D];
 #pragma unroll
@@ -161,32 +182,32 @@ __global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
 #pragma unroll
         for (int t = 0; t < D; ++t) h0[s][t] = h1[s][t] = cc[s][t] = 0u;
 
-    uint32_t p0 = load_next(), p1 = load_next(), p2 = load_next();
-    int out_idx = -2 * D;  // output row of the group's first input row
-    for (int g = 0; g < n_groups; ++g) {
-        const uint32_t x0 = p0, x1 = p1, x2 = p2;
-        p0 = load_next();
-        p1 = load_next();
-        p2 = load_next();
-        uint32_t y;
-        y = push_row<D, 0>(x0, h0, h1, cc);
-        if (out_idx >= 0 && out_idx < rows_here) {
-            if (keep) { *dp = y; cnt += __builtin_popcount(y); }
-            dp += Ww;
-        }
-        ++out_idx;
-        y = push_row<D, 1>(x1, h0, h1, cc);
-        if (out_idx >= 0 && out_idx < rows_here) {
-            if (keep) { *dp = y; cnt += __builtin_popcount(y); }
-            dp += Ww;
-        }
-        ++out_idx;
-        y = push_row<D, 2>(x2, h0, h1, cc);
-        if (out_idx >= 0 && out_idx < rows_here) {
-            if (keep) { *dp = y; cnt += __builtin_popcount(y); }
-            dp += Ww;
-        }
-        ++out_idx;
+    // Prefetch: the next group's rows are issued at the top of the body and
+    // moved into place at the bottom, so their vmcnt wait lands a full group
+    // of compute after issue (the sched_barrier stops the scheduler from
+    // sinking the loads).
+    auto vmov = [](uint32_t v) {
+        uint32_t r;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
+        return r;
+    };
+    // the first group also goes through vmov, so no load is pending on the
+    // loop's entry edge either (else the header waits for it every iteration)
+    uint32_t x0 = vmov(load_next()), x1 = vmov(load_next()), x2 = vmov(load_next());
+    for (int oi = -2 * D; oi < rows_here; oi += 3) {
+        const uint32_t n0 = load_next(), n1 = load_next(), n2 = load_next();
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t y0 = x0, y1 = x1, y2 = x2;
+        push_group<D>(y0, y1, y2, h0, h1, cc);
+        emit(y0, oi);
+        emit(y1, oi + 1);
+        emit(y2, oi + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        // a real v_mov (not a coalescable copy): the register allocator would
+        // otherwise merge x and n and hoist the copy (and its wait) to the top
+        x0 = vmov(n0);
+        x1 = vmov(n1);
+        x2 = vmov(n2);
     }
     if (a.alive) {
         const uint32_t tot = wave_sum_u32(cnt);

@@ -1,0 +1,37 @@
+"""Tuning sweep (one process): GCUPS of the step kernel per (board, depth, rows_per_wave)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "game-of-life-distributed_amd"))
+import golhip  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--sizes", default="16384,65536")
+ap.add_argument("--depths", default="8,16,32")
+ap.add_argument("--rpw", default="32,64,128,256,512,1024")
+ap.add_argument("--turns", type=int, default=256)
+a = ap.parse_args()
+for N in map(int, a.sizes.split(",")):
+    b = golhip.Board(N, N, timing=True)
+    b.fill_random(0x5EED0001)
+    for d in map(int, a.depths.split(",")):
+        for s in map(int, a.rpw.split(",")):
+            b.set_tb_depth(d)
+            b.set_rows_per_wave(s)
+            b.step(2 * d)
+            b.sync()
+            b.perf_reset()
+            t0 = time.perf_counter()
+            b.step(a.turns)
+            b.sync()
+            dt = time.perf_counter() - t0
+            p = b.perf()
+            kern = p["step_kernel_ms"] / p["step_launches"]
+            rec = dict(N=N, depth=d, rpw=s, wall_gcups=N * N * a.turns / dt / 1e9,
+                       kernel_gcups=N * N * d / (kern * 1e-3) / 1e9, launch_ms=kern)
+            print(json.dumps(rec), flush=True)
+    b.close()
