@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--workload", type=int, default=16384, choices=sorted(WORKLOADS))
     ap.add_argument("--turns-per-step", type=int, default=None)
     ap.add_argument("--tb-depth", type=int, default=16)
-    ap.add_argument("--rows-per-wave", type=int, default=512)
+    ap.add_argument("--rows-per-wave", type=int, default=0, help="0 = automatic")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -182,7 +182,7 @@ def main():
             "rows_per_rank": rows,
             "turns_per_step": turns_per_step,
             "tb_depth": a.tb_depth,
-            "rows_per_wave": a.rows_per_wave,
+            "rows_per_wave": perf["rows_per_wave"],
             "parallelism": f"row-strips x{world} (RCCL halo ring)" if world > 1 else "single GPU torus",
         },
         "roofline": {

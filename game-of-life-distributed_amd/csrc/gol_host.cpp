@@ -1,0 +1,443 @@
+// gol_host.cpp — the reference's gol.Run host flow over libgolhip.so.
+//
+// Mirrors gol/distributor.go:30-209 (distributor), :223-280 (keyPress),
+// :283-302 (ticker) and gol/io.go:42-126 (PGM io).  The turn loop itself is
+// golhip_step; everything here is event sequencing and file I/O.
+#include "gol_host.h"
+
+#include <sys/stat.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <thread>
+
+#include "../../include/golhip.h"
+#include "../../include/golrun.h"
+
+namespace gol {
+
+std::string StateString(State s) {
+    switch (s) {
+        case State::Paused: return "Paused";
+        case State::Executing: return "Executing";
+        case State::Quitting: return "Quitting";
+    }
+    return "Incorrect State";
+}
+
+std::string Event::String() const {
+    switch (kind) {
+        case EventKind::AliveCellsCount: return "Alive Cells " + std::to_string(CellsCount);
+        case EventKind::ImageOutputComplete: return "File " + Filename + " output complete";
+        case EventKind::StateChange: return StateString(NewState);
+        default: return "";  // CellFlipped, TurnComplete, FinalTurnComplete (event.go:107-129)
+    }
+}
+
+// ---------------------------------------------------------------- PGM io
+// readPgmImage (io.go:90-126): whitespace-separated fields P5, W, H, 255;
+// the raster follows the single whitespace byte after maxval.
+std::vector<uint8_t> ReadPgm(const std::string &path, int width, int height) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw std::runtime_error("open " + path + ": no such file or directory");
+    std::vector<uint8_t> data((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    size_t pos = 0;
+    auto ws = [](uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f'; };
+    std::string fields[4];
+    for (auto &fld : fields) {
+        while (pos < data.size() && ws(data[pos])) ++pos;
+        while (pos < data.size() && !ws(data[pos])) fld.push_back((char)data[pos++]);
+    }
+    ++pos;
+    if (fields[0] != "P5") throw std::runtime_error("Not a pgm file");
+    if (std::atoi(fields[1].c_str()) != width) throw std::runtime_error("Incorrect width");
+    if (std::atoi(fields[2].c_str()) != height) throw std::runtime_error("Incorrect height");
+    if (std::atoi(fields[3].c_str()) != 255) throw std::runtime_error("Incorrect maxval/bit depth");
+    const size_t n = (size_t)width * height;
+    if (data.size() < pos + n) throw std::runtime_error("short raster in " + path);
+    return std::vector<uint8_t>(data.begin() + pos, data.begin() + pos + n);
+}
+
+// writePgmImage (io.go:42-87): "P5\n" W " " H "\n" "255\n" + raster, one bulk write.
+void WritePgm(const std::string &path, int width, int height, const uint8_t *raster) {
+    std::ofstream f(path, std::ios::binary | std::ios::trunc);
+    if (!f) throw std::runtime_error("create " + path + " failed");
+    f << "P5\n" << width << " " << height << "\n" << 255 << "\n";
+    f.write(reinterpret_cast<const char *>(raster), (std::streamsize)width * height);
+    f.flush();
+    if (!f) throw std::runtime_error("write " + path + " failed");
+}
+
+namespace {
+
+void check(int rc) {
+    if (rc != GOLHIP_OK) throw std::runtime_error(std::string("golhip: ") + golhip_last_error());
+}
+
+struct Board {
+    golhip_t h = nullptr;
+    Board(int w, int hgt, int dev) { check(golhip_create(w, hgt, dev, 0, &h)); }
+    ~Board() { golhip_destroy(h); }
+};
+
+std::vector<util::Cell> cells_of(golhip_t h, int (*fn)(golhip_t, int32_t *, uint64_t, uint64_t *), bool transpose) {
+    uint64_t n = 0;
+    int rc = fn(h, nullptr, 0, &n);
+    if (rc != GOLHIP_OK && rc != GOLHIP_ERANGE) check(rc);
+    std::vector<int32_t> xy(2 * std::max<uint64_t>(n, 1));
+    check(fn(h, xy.data(), n, &n));
+    std::vector<util::Cell> out(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        out[i].X = transpose ? xy[2 * i + 1] : xy[2 * i];
+        out[i].Y = transpose ? xy[2 * i] : xy[2 * i + 1];
+    }
+    return out;
+}
+
+}  // namespace
+
+void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOptions &opt) {
+    const int W = p.ImageWidth, H = p.ImageHeight;
+    if (W <= 0 || H <= 0 || p.Turns < 0) throw std::runtime_error("bad Params");
+    const std::string name = std::to_string(W) + "x" + std::to_string(H);
+    const bool quirks = opt.ref_quirks;
+
+    // distributor.go:39-41 -> io.readPgmImage
+    std::vector<uint8_t> raster = ReadPgm(opt.root + "/images/" + name + ".pgm", W, H);
+    std::printf("File %s input done!\n", name.c_str());
+    std::fflush(stdout);
+
+    Board board(W, H, opt.device);
+    check(golhip_load_bytes(board.h, raster.data()));
+
+    auto send = [&](Event e) {
+        if (events) events->send(std::move(e));
+    };
+    auto write_snapshot = [&](int turn, bool transposed) -> std::string {
+        std::vector<uint8_t> snap((size_t)W * H);
+        check(golhip_snapshot_bytes(board.h, snap.data()));
+        if (transposed) {  // the reference streams (*world)[x][y] for s/q (distributor.go:234-238)
+            std::vector<uint8_t> t((size_t)W * H);
+            for (int y = 0; y < H; ++y)
+                for (int x = 0; x < W; ++x) t[(size_t)x * H + y] = snap[(size_t)y * W + x];
+            snap.swap(t);
+        }
+        const std::string fname = name + "x" + std::to_string(turn);
+        mkdir((opt.root + "/out").c_str(), 0777);  // io.go:43 os.Mkdir("out")
+        WritePgm(opt.root + "/out/" + fname + ".pgm", W, H, snap.data());
+        std::printf("File %s output done!\n", fname.c_str());
+        std::fflush(stdout);
+        return fname;
+    };
+
+    // distributor.go:72-80: CellFlipped for every cell alive at load, turn 0.
+    if (opt.cell_events && events)
+        for (const util::Cell &c : cells_of(board.h, golhip_alive_cells, quirks)) {
+            Event e;
+            e.kind = EventKind::CellFlipped;
+            e.CompletedTurns = 0;
+            e.Cell = c;
+            send(e);
+        }
+
+    std::mutex mu;                 // the reference's `mu`: held by the turn loop and by pause
+    std::atomic<int> turn{0};      // completed turns
+    std::atomic<bool> finished{false}, quit{false};
+    std::mutex tick_mu;
+    std::condition_variable tick_cv;
+
+    // ticker (distributor.go:283-302): (turn, count) read as one pair from the engine.
+    std::exception_ptr helper_err;  // first exception raised on a helper thread
+    std::mutex err_mu;
+    auto guarded = [&](auto body) {
+        return [&, body] {
+            try {
+                body();
+            } catch (...) {
+                std::lock_guard<std::mutex> g(err_mu);
+                if (!helper_err) helper_err = std::current_exception();
+                quit = true;
+            }
+        };
+    };
+    std::thread ticker(guarded([&] {
+        const auto period = std::chrono::duration<double>(opt.ticker_seconds);
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(tick_mu);
+                if (tick_cv.wait_for(lk, period, [&] { return finished.load(); })) break;
+            }
+            uint64_t n = 0;
+            int64_t at = 0;
+            {
+                std::lock_guard<std::mutex> g(mu);  // blocked while paused, like the reference
+                check(golhip_alive_count(board.h, &n, &at));
+            }
+            Event e;
+            e.kind = EventKind::AliveCellsCount;
+            e.CompletedTurns = (int)at;
+            e.CellsCount = (int)n;
+            send(e);
+        }
+    }));
+
+    // keyPress (distributor.go:223-280); a nil channel simply never delivers.
+    std::thread keys;
+    if (keyPresses) keys = std::thread(guarded([&] {
+        char32_t k;
+        while (!finished.load()) {
+            int r = keyPresses->try_recv(k);
+            if (r < 0) break;
+            if (r == 0) {
+                std::this_thread::sleep_for(std::chrono::milliseconds(2));
+                continue;
+            }
+            if (k == U's' || k == U'q') {
+                std::string fname;
+                int t;
+                {
+                    std::lock_guard<std::mutex> g(mu);  // snapshot at a turn boundary
+                    t = turn.load();
+                    fname = write_snapshot(t, quirks);
+                }
+                Event e;
+                e.kind = EventKind::ImageOutputComplete;
+                e.CompletedTurns = t;
+                e.Filename = fname;
+                send(e);
+                if (k == U'q') {
+                    quit = true;
+                    break;
+                }
+            } else if (k == U'p') {
+                std::unique_lock<std::mutex> g(mu);
+                std::printf("%d\n", turn.load());
+                std::fflush(stdout);
+                if (!quirks) {
+                    Event e;
+                    e.kind = EventKind::StateChange;
+                    e.CompletedTurns = turn.load();
+                    e.NewState = State::Paused;
+                    send(e);
+                }
+                char32_t k2 = 0;
+                while (!finished.load()) {
+                    int r2 = keyPresses->try_recv(k2);
+                    if (r2 < 0) break;
+                    if (r2 == 1 && k2 == U'p') break;
+                    std::this_thread::sleep_for(std::chrono::milliseconds(2));
+                }
+                std::printf("Continuing\n");
+                std::fflush(stdout);
+                if (!quirks) {
+                    Event e;
+                    e.kind = EventKind::StateChange;
+                    e.CompletedTurns = turn.load();
+                    e.NewState = State::Executing;
+                    send(e);
+                }
+            }
+        }
+    }));
+
+    auto stop_helpers = [&] {
+        {
+            std::lock_guard<std::mutex> lk(tick_mu);
+            finished = true;
+        }
+        tick_cv.notify_all();
+        if (ticker.joinable()) ticker.join();
+        if (keys.joinable()) keys.join();
+        if (helper_err) std::rethrow_exception(helper_err);
+    };
+
+    try {
+        const bool per_turn = opt.cell_events || opt.turn_events;
+        int t = 0;
+        while (t < p.Turns && !quit.load()) {
+            // per-turn events need one turn per step; otherwise fuse up to
+            // 256 turns per call (bounded key/pause latency)
+            const int n = per_turn ? 1 : std::min(256, p.Turns - t);
+            std::vector<util::Cell> flips;
+            {
+                std::lock_guard<std::mutex> g(mu);
+                check(golhip_step(board.h, n, opt.cell_events ? 1 : 0));
+                if (opt.cell_events) flips = cells_of(board.h, golhip_flips, quirks);
+                else check(golhip_sync(board.h));
+                t += n;
+                turn = t;
+            }
+            for (const util::Cell &c : flips) {  // initializeAliveCells (:212-220)
+                Event e;
+                e.kind = EventKind::CellFlipped;
+                e.CompletedTurns = quirks ? t - 1 : t;
+                e.Cell = c;
+                send(e);
+            }
+            if (opt.turn_events) {  // :113 / :171 (the reference sends the 0-based turn)
+                Event e;
+                e.kind = EventKind::TurnComplete;
+                e.CompletedTurns = quirks ? t - 1 : t;
+                send(e);
+            }
+        }
+        stop_helpers();
+        if (quit.load()) {
+            // `q` (:244-261): snapshot already written; the reference os.Exit(0)s
+            // without FinalTurnComplete.  The mirror ends the run instead.
+            Event e;
+            e.kind = EventKind::StateChange;
+            e.CompletedTurns = turn.load();
+            e.NewState = State::Quitting;
+            send(e);
+            if (events) events->close();
+            return;
+        }
+        // distributor.go:180-206
+        std::vector<util::Cell> alive = cells_of(board.h, golhip_alive_cells, false);
+        const std::string fname = write_snapshot(p.Turns, false);
+        Event io;
+        io.kind = EventKind::ImageOutputComplete;
+        io.CompletedTurns = p.Turns;
+        io.Filename = fname;
+        send(io);
+        Event fin;
+        fin.kind = EventKind::FinalTurnComplete;
+        fin.CompletedTurns = p.Turns;
+        fin.Alive = std::move(alive);
+        send(fin);
+        Event q;
+        q.kind = EventKind::StateChange;
+        q.CompletedTurns = p.Turns;
+        q.NewState = State::Quitting;
+        send(q);
+        if (events) events->close();
+    } catch (...) {
+        stop_helpers();
+        if (events) events->close();
+        throw;
+    }
+}
+
+}  // namespace gol
+
+// ---------------------------------------------------------------------------
+// C-ABI of the host mirror (include/golrun.h): lets non-C++ callers (the
+// Python parity tests) drive gol::Run the way gol_test.go drives gol.Run.
+// ---------------------------------------------------------------------------
+struct golrun {
+    gol::Chan<gol::Event> events;
+    gol::Chan<char32_t> keys;
+    bool use_keys;
+    std::thread th;
+    std::string err;
+    std::atomic<bool> done{false};
+    gol::Event current;
+    golrun(size_t cap, bool k) : events(cap), keys(16), use_keys(k) {}
+};
+
+namespace {
+thread_local std::string g_run_err;
+int run_fail(const std::string &m) {
+    g_run_err = m;
+    return GOLHIP_EINVAL;
+}
+}  // namespace
+
+extern "C" {
+
+const char *golrun_last_error(void) { return g_run_err.c_str(); }
+
+int golrun_start(int32_t turns, int32_t threads, int32_t width, int32_t height, const char *root, int32_t device,
+                 uint32_t flags, int32_t events_cap, int32_t ticker_ms, golrun_t *out) {
+    if (!out || !root || events_cap < 0) return run_fail("bad arguments");
+    gol::Params p;
+    p.Turns = turns;
+    p.Threads = threads;
+    p.ImageWidth = width;
+    p.ImageHeight = height;
+    gol::RunOptions o;
+    o.root = root;
+    o.device = device;
+    o.ref_quirks = (flags & GOLRUN_FLAG_REF_QUIRKS) != 0;
+    o.cell_events = (flags & GOLRUN_FLAG_NO_CELL_EVENTS) == 0;
+    o.turn_events = (flags & GOLRUN_FLAG_NO_TURN_EVENTS) == 0;
+    if (ticker_ms > 0) o.ticker_seconds = ticker_ms / 1000.0;
+    golrun *r = new golrun((size_t)events_cap, (flags & GOLRUN_FLAG_KEYS) != 0);
+    r->th = std::thread([r, p, o] {
+        try {
+            gol::Run(p, &r->events, r->use_keys ? &r->keys : nullptr, o);
+        } catch (const std::exception &e) {
+            r->err = e.what();
+            r->events.close();
+        }
+        r->done = true;
+    });
+    *out = r;
+    return GOLHIP_OK;
+}
+
+int golrun_next_event(golrun_t r, golrun_event_t *ev, int32_t timeout_ms) {
+    if (!r || !ev) return run_fail("bad arguments");
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms < 0 ? 0 : timeout_ms);
+    for (;;) {
+        int got = r->events.try_recv(r->current);
+        if (got == 1) break;
+        if (got < 0) return 0;  // closed and drained: the `range events` loop ends
+        if (timeout_ms >= 0 && std::chrono::steady_clock::now() >= t_end) return 2;
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    const gol::Event &e = r->current;
+    memset(ev, 0, sizeof *ev);
+    ev->kind = (int32_t)e.kind;
+    ev->completed_turns = e.CompletedTurns;
+    ev->cells_count = e.CellsCount;
+    ev->new_state = (int32_t)e.NewState;
+    ev->cell_x = e.Cell.X;
+    ev->cell_y = e.Cell.Y;
+    ev->alive_len = (int64_t)e.Alive.size();
+    std::snprintf(ev->filename, sizeof ev->filename, "%s", e.Filename.c_str());
+    std::snprintf(ev->text, sizeof ev->text, "%s", e.String().c_str());
+    return 1;
+}
+
+int golrun_event_cells(golrun_t r, int32_t *xy, uint64_t cap) {
+    if (!r) return run_fail("bad arguments");
+    const auto &a = r->current.Alive;
+    if (cap < a.size() || (!xy && !a.empty())) return run_fail("buffer too small");
+    for (size_t i = 0; i < a.size(); ++i) {
+        xy[2 * i] = a[i].X;
+        xy[2 * i + 1] = a[i].Y;
+    }
+    return GOLHIP_OK;
+}
+
+int golrun_send_key(golrun_t r, uint32_t key) {
+    if (!r || !r->use_keys) return run_fail("run has no key channel");
+    return r->keys.send((char32_t)key) ? GOLHIP_OK : run_fail("key channel closed");
+}
+
+int golrun_wait(golrun_t r, char *err, uint64_t err_cap) {
+    if (!r) return run_fail("bad arguments");
+    // drain whatever the caller left unread so the run can finish
+    gol::Event tmp;
+    while (!r->done.load()) {
+        if (r->events.try_recv(tmp) == 0) std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    if (r->th.joinable()) r->th.join();
+    if (err && err_cap) std::snprintf(err, err_cap, "%s", r->err.c_str());
+    return r->err.empty() ? GOLHIP_OK : GOLHIP_EINVAL;
+}
+
+int golrun_destroy(golrun_t r) {
+    if (!r) return GOLHIP_OK;
+    golrun_wait(r, nullptr, 0);
+    delete r;
+    return GOLHIP_OK;
+}
+
+}  // extern "C"

@@ -215,6 +215,41 @@ __global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
     }
 }
 
+int tb_blocks_per_cu(int depth) {
+    int b = 0;
+    hipError_t e = hipErrorInvalidValue;
+    switch (depth) {
+        case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<1>, 256, 0); break;
+        case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<2>, 256, 0); break;
+        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<4>, 256, 0); break;
+        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<8>, 256, 0); break;
+        case 16: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<16>, 256, 0); break;
+        case 32: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<32>, 256, 0); break;
+        default: break;
+    }
+    return (e == hipSuccess && b > 0) ? b : 1;
+}
+
+int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots) {
+    // Each wave streams S + 2*depth rows; waves run in ceil(waves / slots)
+    // rounds.  Minimise rounds * (S + 2*depth) (fill overhead vs tail).
+    const int tiles_x = (Ww + kTileValid - 1) / kTileValid;
+    int best_s = rows;
+    double best = 1e300;
+    for (int strips = 1; strips <= rows; ++strips) {
+        const int S = (rows + strips - 1) / strips;
+        const long long waves = (long long)tiles_x * ((rows + S - 1) / S);
+        const long long rounds = (waves + wave_slots - 1) / wave_slots;
+        const double cost = (double)rounds * (S + 2 * depth);
+        if (cost < best * 0.999) {
+            best = cost;
+            best_s = S;
+        }
+        if (S <= 2) break;
+    }
+    return best_s;
+}
+
 int tb_waves(const StepArgs &a, int depth) {
     (void)depth;
     const int tiles_x = (a.Ww + kTileValid - 1) / kTileValid;

@@ -81,7 +81,9 @@ struct golhip {
     int64_t phys_rows = 0;
 
     int tb_depth = 16;
-    int rows_per_wave = 512;
+    int rows_per_wave = 0;      // 0 = automatic (per depth, from occupancy)
+    int cu_count = 0;
+    int auto_rpw[6] = {0, 0, 0, 0, 0, 0};  // cache per depth index
     bool loaded = false;
     std::atomic<int64_t> turns{0};
 
@@ -209,6 +211,24 @@ golk::StepArgs step_args(golhip_t h, unsigned long long *alive, bool halo) {
     return a;
 }
 
+int depth_index(int d) {
+    int i = 0;
+    while ((1 << i) < d) ++i;
+    return i;
+}
+
+// Rows per wave for a launch of `depth` turns: the user's value, or the
+// automatic choice (wave slots = CUs x resident waves per CU).
+int rows_per_wave_for(golhip_t h, int depth) {
+    if (h->rows_per_wave > 0) return h->rows_per_wave;
+    int &c = h->auto_rpw[depth_index(depth)];
+    if (c == 0) {
+        const int slots = h->cu_count * golk::tb_blocks_per_cu(depth) * 4;
+        c = golk::auto_rows_per_wave(h->Ww, h->rows, depth, std::max(slots, 1));
+    }
+    return c;
+}
+
 hipEvent_t take_event(golhip_t h) {
     if (!h->ev_pool.empty()) {
         hipEvent_t e = h->ev_pool.back();
@@ -271,6 +291,7 @@ int launch_depth(golhip_t h, int depth, bool count, bool halo) {
         HIP_OR_FAIL(hipMemsetAsync(alive, 0, sizeof(unsigned long long), h->stream));
     }
     golk::StepArgs a = step_args(h, alive, halo);
+    a.rows_per_wave = rows_per_wave_for(h, depth);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->flags & GOLHIP_FLAG_TIMING) {
         e0 = take_event(h);
@@ -352,6 +373,11 @@ int create_common(int32_t width, int32_t height, int32_t row0, int32_t rows, int
     h->device = device;
     h->flags = flags;
     h->phys_rows = (int64_t)rows + 2 * kHalo;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess) h->cu_count = prop.multiProcessorCount;
+        if (h->cu_count <= 0) h->cu_count = 256;
+    }
     const size_t bytes = (size_t)h->phys_rows * h->Ww * sizeof(uint32_t);
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e == hipSuccess) h->own_stream = true;
@@ -446,7 +472,7 @@ int golhip_set_tb_depth(golhip_t h, int32_t t) {
 
 int golhip_set_rows_per_wave(golhip_t h, int32_t r) {
     if (int rc = check(h)) return rc;
-    if (r < 1) return fail(GOLHIP_EINVAL, "rows per wave %d", r);
+    if (r < 0) return fail(GOLHIP_EINVAL, "rows per wave %d", r);
     std::lock_guard<std::mutex> g(h->mu);
     h->rows_per_wave = r;
     return GOLHIP_OK;
@@ -749,7 +775,7 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     out->alg_bytes = out->cell_updates / 4;
     out->halo_bytes = h->halo_bytes;
     out->tb_depth = h->tb_depth;
-    out->rows_per_wave = h->rows_per_wave;
+    out->rows_per_wave = rows_per_wave_for(h, next_depth(h, h->tb_depth, h->nranks > 1));
     out->kernel_variant = h->W % 32 == 0 ? 1 : 0;
     return GOLHIP_OK;
 }

@@ -289,3 +289,130 @@ def board_hash_np(words: np.ndarray, row0: int = 0) -> int:
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         z = z ^ (z >> np.uint64(31))
         return int(z.sum(dtype=np.uint64))
+
+
+# --------------------------------------------------------------------------
+# host mirror of gol.Run (libgolhost.so, include/golrun.h)
+# --------------------------------------------------------------------------
+HOST_LIB_PATH = os.path.join(HERE, "libgolhost.so")
+FLAG_KEYS, FLAG_REF_QUIRKS, FLAG_NO_CELL_EVENTS, FLAG_NO_TURN_EVENTS = 0x1, 0x2, 0x4, 0x8
+ALIVE_CELLS_COUNT, IMAGE_OUTPUT_COMPLETE, STATE_CHANGE, CELL_FLIPPED, TURN_COMPLETE, FINAL_TURN_COMPLETE = range(6)
+PAUSED, EXECUTING, QUITTING = range(3)
+EVENT_NAMES = ["AliveCellsCount", "ImageOutputComplete", "StateChange", "CellFlipped", "TurnComplete",
+               "FinalTurnComplete"]
+
+
+class RunEvent(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int32), ("completed_turns", ctypes.c_int32), ("cells_count", ctypes.c_int32),
+        ("new_state", ctypes.c_int32), ("cell_x", ctypes.c_int32), ("cell_y", ctypes.c_int32),
+        ("alive_len", ctypes.c_int64), ("filename", ctypes.c_char * 256), ("text", ctypes.c_char * 288),
+    ]
+
+
+_host = None
+
+
+def load_host(path: str = HOST_LIB_PATH) -> ctypes.CDLL:
+    global _host
+    if _host is not None:
+        return _host
+    load()
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"{path} not built")
+    lib = ctypes.CDLL(path)
+    P = ctypes.POINTER
+    i32, u32, u64 = ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64
+    sig = {
+        "golrun_last_error": ([], ctypes.c_char_p),
+        "golrun_start": ([i32, i32, i32, i32, ctypes.c_char_p, i32, u32, i32, i32, P(ctypes.c_void_p)], ctypes.c_int),
+        "golrun_next_event": ([ctypes.c_void_p, P(RunEvent), i32], ctypes.c_int),
+        "golrun_event_cells": ([ctypes.c_void_p, ctypes.c_void_p, u64], ctypes.c_int),
+        "golrun_send_key": ([ctypes.c_void_p, u32], ctypes.c_int),
+        "golrun_wait": ([ctypes.c_void_p, ctypes.c_char_p, u64], ctypes.c_int),
+        "golrun_destroy": ([ctypes.c_void_p], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _host = lib
+    return lib
+
+
+class Run:
+    """`go gol.Run(p, events, keyPresses)`; iterate it like `for event := range events`.
+
+    Events are dicts: {"type": "TurnComplete", "CompletedTurns": 3, ...}."""
+
+    def __init__(self, turns: int, threads: int, width: int, height: int, root: str, *, device: int = 0,
+                 keys: bool = False, quirks: bool = False, cell_events: bool = True, turn_events: bool = True,
+                 events_cap: int = 0, ticker_ms: int = 0):
+        lib = load_host()
+        flags = (FLAG_KEYS if keys else 0) | (FLAG_REF_QUIRKS if quirks else 0) | \
+            (0 if cell_events else FLAG_NO_CELL_EVENTS) | (0 if turn_events else FLAG_NO_TURN_EVENTS)
+        h = ctypes.c_void_p()
+        rc = lib.golrun_start(turns, threads, width, height, root.encode(), device, flags, events_cap, ticker_ms,
+                              ctypes.byref(h))
+        if rc != 0:
+            raise GolHipError(rc, lib.golrun_last_error().decode())
+        self._h = h
+        self._ev = RunEvent()
+
+    def next(self, timeout_ms: int = -1):
+        """Next event dict, None once closed, "timeout" on timeout."""
+        lib = load_host()
+        rc = lib.golrun_next_event(self._h, ctypes.byref(self._ev), timeout_ms)
+        if rc == 0:
+            return None
+        if rc == 2:
+            return "timeout"
+        if rc != 1:
+            raise GolHipError(rc, lib.golrun_last_error().decode())
+        e = self._ev
+        ev = {"type": EVENT_NAMES[e.kind], "CompletedTurns": e.completed_turns, "String": e.text.decode()}
+        if e.kind == ALIVE_CELLS_COUNT:
+            ev["CellsCount"] = e.cells_count
+        elif e.kind == IMAGE_OUTPUT_COMPLETE:
+            ev["Filename"] = e.filename.decode()
+        elif e.kind == STATE_CHANGE:
+            ev["NewState"] = e.new_state
+        elif e.kind == CELL_FLIPPED:
+            ev["Cell"] = (e.cell_x, e.cell_y)
+        elif e.kind == FINAL_TURN_COMPLETE:
+            xy = np.zeros((max(e.alive_len, 1), 2), dtype=np.int32)
+            rc = lib.golrun_event_cells(self._h, _ptr(xy), e.alive_len)
+            if rc != 0:
+                raise GolHipError(rc, lib.golrun_last_error().decode())
+            ev["Alive"] = xy[: e.alive_len]
+        return ev
+
+    def __iter__(self):
+        while True:
+            ev = self.next()
+            if ev is None:
+                return
+            yield ev
+
+    def send_key(self, key: str) -> None:
+        lib = load_host()
+        rc = lib.golrun_send_key(self._h, ord(key))
+        if rc != 0:
+            raise GolHipError(rc, lib.golrun_last_error().decode())
+
+    def wait(self) -> str:
+        """Join the run; returns the panic message ('' if the run ended normally)."""
+        buf = ctypes.create_string_buffer(1024)
+        load_host().golrun_wait(self._h, buf, 1024)
+        return buf.value.decode()
+
+    def close(self) -> None:
+        if self._h:
+            load_host().golrun_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

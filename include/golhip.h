@@ -63,7 +63,7 @@ typedef struct golhip_perf {
     int64_t alg_bytes;        /* 0.25 B per cell-update (1 bit in + 1 bit out)*/
     int64_t halo_bytes;       /* bytes sent to neighbour ranks                */
     int32_t tb_depth;         /* turns fused per step launch                  */
-    int32_t rows_per_wave;    /* rows streamed by one wavefront per launch    */
+    int32_t rows_per_wave;    /* rows streamed per wavefront (full-depth launch)*/
     int32_t kernel_variant;   /* 0 = generic (width % 32 != 0), 1 = bit-sliced*/
     int32_t reserved;
 } golhip_perf_t;
@@ -91,7 +91,8 @@ int golhip_set_stream(golhip_t h, void *hip_stream);
 void *golhip_stream(golhip_t h);
 
 /* Tuning: turns fused per launch (1..GOLHIP_MAX_TB_DEPTH) and rows streamed
- * per wavefront.  Results never depend on them. */
+ * per wavefront (0 = automatic, the default: sized from the CU count and the
+ * kernel's occupancy).  Results never depend on them. */
 int golhip_set_tb_depth(golhip_t h, int32_t turns);
 int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
 

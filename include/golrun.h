@@ -1,0 +1,71 @@
+/*
+ * golrun.h — C-ABI of libgolhost.so, the host-side mirror of the reference's
+ * gol.Run (gol/gol.go:12) built on libgolhip.so.
+ *
+ * golrun_start is `go gol.Run(p, events, keyPresses)` (gol_test.go:34,
+ * count_test.go:26): it starts the run on its own thread; golrun_next_event is
+ * one receive of `for event := range events` (it returns 0 once the channel is
+ * closed and drained); golrun_send_key is `keyPresses <- k`.
+ * Event kinds, fields and String() text follow gol/event.go:19-131.
+ */
+#ifndef GOLRUN_H
+#define GOLRUN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* golrun_start flags */
+#define GOLRUN_FLAG_KEYS 0x1u            /* create a keyPresses channel (else nil)          */
+#define GOLRUN_FLAG_REF_QUIRKS 0x2u      /* reference quirks: 0-based TurnComplete, transposed
+                                            CellFlipped and s/q snapshots (DESIGN.md "Quirks") */
+#define GOLRUN_FLAG_NO_CELL_EVENTS 0x4u  /* no per-cell CellFlipped (fused turns, fast)     */
+#define GOLRUN_FLAG_NO_TURN_EVENTS 0x8u  /* no per-turn TurnComplete                        */
+
+/* event kinds (gol/event.go) */
+#define GOLRUN_ALIVE_CELLS_COUNT 0
+#define GOLRUN_IMAGE_OUTPUT_COMPLETE 1
+#define GOLRUN_STATE_CHANGE 2
+#define GOLRUN_CELL_FLIPPED 3
+#define GOLRUN_TURN_COMPLETE 4
+#define GOLRUN_FINAL_TURN_COMPLETE 5
+/* State (event.go:33-38) */
+#define GOLRUN_PAUSED 0
+#define GOLRUN_EXECUTING 1
+#define GOLRUN_QUITTING 2
+
+typedef struct golrun golrun;
+typedef golrun *golrun_t;
+
+typedef struct golrun_event {
+    int32_t kind;
+    int32_t completed_turns;   /* GetCompletedTurns()                      */
+    int32_t cells_count;       /* AliveCellsCount.CellsCount               */
+    int32_t new_state;         /* StateChange.NewState                     */
+    int32_t cell_x, cell_y;    /* CellFlipped.Cell                         */
+    int64_t alive_len;         /* len(FinalTurnComplete.Alive)             */
+    char filename[256];        /* ImageOutputComplete.Filename             */
+    char text[288];            /* String()                                 */
+} golrun_event_t;
+
+const char *golrun_last_error(void);
+/* root: directory with images/<W>x<H>.pgm; output goes to root/out/.
+ * events_cap: 0 = unbuffered (as in the tests), 1000 as in main.go:53.
+ * ticker_ms: AliveCellsCount period (<= 0: 2000 as distributor.go:285). */
+int golrun_start(int32_t turns, int32_t threads, int32_t width, int32_t height, const char *root, int32_t device,
+                 uint32_t flags, int32_t events_cap, int32_t ticker_ms, golrun_t *out);
+/* 1 = event received, 0 = channel closed and drained, 2 = timeout (timeout_ms >= 0). */
+int golrun_next_event(golrun_t r, golrun_event_t *ev, int32_t timeout_ms);
+/* Alive list of the last FinalTurnComplete received (alive_len pairs X, Y). */
+int golrun_event_cells(golrun_t r, int32_t *xy, uint64_t cap);
+int golrun_send_key(golrun_t r, uint32_t key);
+/* Drains unread events, joins the run; 0 or the panic message in err. */
+int golrun_wait(golrun_t r, char *err, uint64_t err_cap);
+int golrun_destroy(golrun_t r);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GOLRUN_H */

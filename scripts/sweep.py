@@ -12,7 +12,7 @@ import golhip  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--sizes", default="16384,65536")
 ap.add_argument("--depths", default="8,16,32")
-ap.add_argument("--rpw", default="32,64,128,256,512,1024")
+ap.add_argument("--rpw", default="0,32,64,128,256,512,1024")
 ap.add_argument("--turns", type=int, default=256)
 a = ap.parse_args()
 for N in map(int, a.sizes.split(",")):

@@ -34,7 +34,7 @@ def img(fixtures, n):
     return unpack_bits(fixtures[f"image_{n}"], n)
 
 
-def run_gpu(board, turns, depth=16, rows_per_wave=512):
+def run_gpu(board, turns, depth=16, rows_per_wave=0):
     H, W = board.shape
     with golhip.Board(W, H) as b:
         b.set_tb_depth(depth)

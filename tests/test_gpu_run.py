@@ -1,0 +1,175 @@
+"""gol.Run through the host mirror (libgolhost.so over libgolhip.so): the
+reference's own tests, restated.
+
+  TestGol  gol_test.go:15-47    FinalTurnComplete.Alive == check/images alive set
+  TestPgm  pgm_test.go:10-42    out/WxHxT.pgm == check/images (byte-identical here)
+  TestAlive count_test.go:17-69 AliveCellsCount events vs check/alive/512x512.csv, then 'q'
+  TestSdl  sdl_test.go:93-128   CellFlipped stream on a shadow board == alive counts per turn
+plus the event order of distributor.go:30-209 and the s / p keys.
+"""
+import hashlib
+import os
+import time
+
+import numpy as np
+import pytest
+
+from oracle.oracle import alive_cells_np, pgm_bytes, read_pgm, run_np, unpack_bits
+
+pytestmark = pytest.mark.gpu
+golhip = pytest.importorskip("golhip")
+
+
+@pytest.fixture()
+def root(tmp_path, fixtures):
+    img = tmp_path / "images"
+    img.mkdir()
+    for n in (16, 64, 128, 256, 512):
+        (img / f"{n}x{n}.pgm").write_bytes(pgm_bytes(unpack_bits(fixtures[f"image_{n}"], n)))
+    return tmp_path
+
+
+def multiset(cells):
+    return sorted(map(tuple, np.asarray(cells).reshape(-1, 2).tolist()))
+
+
+@pytest.mark.parametrize("n", [16, 64, 512])
+@pytest.mark.parametrize("turns", [0, 1, 100])
+@pytest.mark.parametrize("threads", [1, 2, 8, 16])
+def test_gol(root, fixtures, n, turns, threads):
+    r = golhip.Run(turns, threads, n, n, str(root))
+    cells = None
+    for ev in r:
+        if ev["type"] == "FinalTurnComplete":
+            cells = ev["Alive"]
+    assert r.wait() == ""
+    r.close()
+    expected = alive_cells_np(unpack_bits(fixtures[f"check_{n}x{turns}"], n))
+    assert multiset(cells) == multiset(expected)
+
+
+@pytest.mark.parametrize("n", [16, 64, 512])
+@pytest.mark.parametrize("turns", [0, 1, 100])
+def test_pgm(root, manifest, n, turns):
+    r = golhip.Run(turns, 8, n, n, str(root))
+    for _ in r:
+        pass
+    assert r.wait() == ""
+    r.close()
+    data = (root / "out" / f"{n}x{n}x{turns}.pgm").read_bytes()
+    assert hashlib.sha256(data).hexdigest() == manifest[f"check_{n}x{turns}"]["sha256"]
+
+
+def test_event_order(root, fixtures):
+    """distributor.go: initial CellFlipped (turn 0) -> per turn CellFlipped* then
+    TurnComplete -> ImageOutputComplete -> FinalTurnComplete -> StateChange(Quitting) -> close."""
+    r = golhip.Run(5, 4, 64, 64, str(root))
+    evs = list(r)
+    assert r.wait() == ""
+    kinds = [e["type"] for e in evs if e["type"] != "AliveCellsCount"]
+    n0 = int(fixtures["alive_64"][0])
+    assert kinds[:n0] == ["CellFlipped"] * n0
+    tc = [i for i, k in enumerate(kinds) if k == "TurnComplete"]
+    assert len(tc) == 5
+    assert [evs_i["CompletedTurns"] for evs_i in [e for e in evs if e["type"] == "TurnComplete"]] == [1, 2, 3, 4, 5]
+    assert kinds[-3:] == ["ImageOutputComplete", "FinalTurnComplete", "StateChange"]
+    tail = [e for e in evs if e["type"] != "AliveCellsCount"][-3:]
+    assert tail[0]["Filename"] == "64x64x5" and tail[0]["String"] == "File 64x64x5 output complete"
+    assert tail[2]["NewState"] == golhip.QUITTING and tail[2]["String"] == "Quitting"
+    assert all(k in ("CellFlipped", "TurnComplete") for k in kinds[n0:tc[-1] + 1])
+
+
+def test_sdl(root, fixtures):
+    """sdl_test.go:58, :107-116: shadow board from CellFlipped, count per TurnComplete."""
+    alive = fixtures["alive_512"]
+    board = np.zeros((512, 512), dtype=np.uint8)
+    r = golhip.Run(100, 8, 512, 512, str(root))
+    turn_num, final = 0, False
+    for ev in r:
+        if ev["type"] == "CellFlipped":
+            x, y = ev["Cell"]
+            board[y, x] = ~board[y, x]
+        elif ev["type"] == "TurnComplete":
+            turn_num += 1
+            assert int((board == 255).sum()) == alive[turn_num], turn_num
+        elif ev["type"] == "FinalTurnComplete":
+            final = True
+    assert r.wait() == "" and final and turn_num == 100
+
+
+def test_alive(root, fixtures):
+    """count_test.go:17-69 with a 0.2 s ticker: every AliveCellsCount matches the
+    CSV (or the post-10000 period-2 rule); then 'q' ends the run."""
+    alive = fixtures["alive_512"]
+    r = golhip.Run(100000000, 8, 512, 512, str(root), keys=True, cell_events=False, turn_events=False,
+                   ticker_ms=200)
+    seen = 0
+    t0 = time.time()
+    while seen < 5:
+        ev = r.next(timeout_ms=5000)
+        assert ev not in (None, "timeout"), "no AliveCellsCount events received in 5 seconds"
+        if ev["type"] == "AliveCellsCount":
+            t = ev["CompletedTurns"]
+            exp = alive[t] if t <= 10000 else (5565 if t % 2 == 0 else 5567)
+            assert ev["CellsCount"] == exp, (t, ev["CellsCount"], exp)
+            assert ev["String"] == f"Alive Cells {exp}"
+            seen += 1
+    assert time.time() - t0 < 30
+    r.send_key("q")
+    rest = list(r)
+    assert r.wait() == ""
+    out = [e for e in rest if e["type"] == "ImageOutputComplete"]
+    assert len(out) == 1
+    t = out[0]["CompletedTurns"]
+    snap = read_pgm(str(root / "out" / f"{out[0]['Filename']}.pgm"), 512, 512)
+    assert int((snap == 255).sum()) == (alive[t] if t <= 10000 else (5565 if t % 2 == 0 else 5567))
+    assert rest[-1]["type"] == "StateChange" and rest[-1]["NewState"] == golhip.QUITTING
+    assert not any(e["type"] == "FinalTurnComplete" for e in rest)
+
+
+def test_snapshot_key_s(root, fixtures):
+    """'s' writes out/WxHx<turn>.pgm at a turn boundary (the mirror is untorn)."""
+    board0 = unpack_bits(fixtures["image_64"], 64)
+    r = golhip.Run(3000, 4, 64, 64, str(root), keys=True)
+    got = None
+    sent = False
+    for ev in r:
+        if ev["type"] == "TurnComplete" and ev["CompletedTurns"] == 10 and not sent:
+            r.send_key("s")
+            sent = True
+        if ev["type"] == "ImageOutputComplete" and got is None:
+            got = ev
+    assert r.wait() == ""
+    t = got["CompletedTurns"]
+    snap = read_pgm(str(root / "out" / f"64x64x{t}.pgm"), 64, 64)
+    assert np.array_equal(snap, run_np(board0, t))
+
+
+def test_pause_key_p(root):
+    r = golhip.Run(100000, 4, 64, 64, str(root), keys=True, cell_events=False)
+    r.send_key("p")
+    states = []
+    for ev in r:
+        if ev["type"] == "StateChange":
+            states.append(ev["NewState"])
+            if ev["NewState"] == golhip.PAUSED:
+                paused_at = ev["CompletedTurns"]
+                time.sleep(0.3)
+                r.send_key("p")
+            elif ev["NewState"] == golhip.EXECUTING:
+                assert ev["CompletedTurns"] == paused_at   # nothing ran while paused
+                r.send_key("q")
+    assert r.wait() == ""
+    assert states[:2] == [golhip.PAUSED, golhip.EXECUTING] and states[-1] == golhip.QUITTING
+
+
+def test_ref_quirks_mode(root, fixtures):
+    """GOLRUN_FLAG_REF_QUIRKS: 0-based TurnComplete and transposed CellFlipped."""
+    r = golhip.Run(2, 4, 64, 64, str(root), quirks=True)
+    evs = [e for e in r if e["type"] in ("TurnComplete", "CellFlipped")]
+    assert r.wait() == ""
+    assert [e["CompletedTurns"] for e in evs if e["type"] == "TurnComplete"] == [0, 1]
+    b0 = unpack_bits(fixtures["image_64"], 64)
+    first = [e["Cell"] for e in evs if e["type"] == "CellFlipped" and e["CompletedTurns"] == 0]
+    rows, cols = np.nonzero(b0 == 255)
+    assert first[: len(rows)] == list(zip(rows.tolist(), cols.tolist()))   # Cell{X: row, Y: col}

@@ -1,0 +1,47 @@
+"""Host mirror of gol.Run (libgolhost.so) — behaviour that needs no GPU:
+the io goroutine's panics (io.go:95-117) surface as the run's error, and a
+host without a HIP device fails loudly instead of computing on the CPU."""
+import os
+
+import numpy as np
+import pytest
+
+golhip = pytest.importorskip("golhip")
+
+
+def run_err(tmp_path, data, W=64, H=64):
+    img = tmp_path / "images"
+    img.mkdir(exist_ok=True)
+    if data is not None:
+        (img / f"{W}x{H}.pgm").write_bytes(data)
+    r = golhip.Run(10, 4, W, H, str(tmp_path))
+    evs = list(r)
+    err = r.wait()
+    r.close()
+    return evs, err
+
+
+def test_missing_image(tmp_path):
+    evs, err = run_err(tmp_path, None)
+    assert evs == [] and "no such file" in err
+
+
+@pytest.mark.parametrize("data,msg", [
+    (b"P2\n64 64\n255\n" + bytes(4096), "Not a pgm file"),
+    (b"P5\n32 64\n255\n" + bytes(4096), "Incorrect width"),
+    (b"P5\n64 32\n255\n" + bytes(4096), "Incorrect height"),
+    (b"P5\n64 64\n15\n" + bytes(4096), "Incorrect maxval/bit depth"),
+])
+def test_pgm_panics(tmp_path, data, msg):
+    evs, err = run_err(tmp_path, data)
+    assert evs == [] and msg in err
+
+
+def test_no_device_fails_loudly(tmp_path):
+    try:
+        if golhip.device_count() > 0:
+            pytest.skip("a GPU is present")
+    except golhip.GolHipError:
+        pass
+    evs, err = run_err(tmp_path, b"P5\n64 64\n255\n" + bytes(4096))
+    assert evs == [] and "golhip" in err
