@@ -117,14 +117,17 @@ __device__ __forceinline__ void stage(int t, uint32_t &x, uint32_t (&h0)[3][D], 
 // i+1 needs stage t of row i (its row sum), so the rows run skewed by one
 // stage: (row0, t), (row1, t-1), (row2, t-2) are independent and interleave,
 // which hides the VALU->DPP hazard of each stage's serial chain.
-template <int D>
+// FILL: the pipeline is still filling (input index i0 of row0 < 2(D-1)).
+// Stage t only receives real rows from input index 2t on, so earlier
+// stage-rows are skipped (their outputs would be garbage nobody stores).
+template <int D, bool FILL>
 __device__ __forceinline__ void push_group(uint32_t &x0, uint32_t &x1, uint32_t &x2, uint32_t (&h0)[3][D],
-                                           uint32_t (&h1)[3][D], uint32_t (&cc)[3][D]) {
+                                           uint32_t (&h1)[3][D], uint32_t (&cc)[3][D], int i0) {
 #pragma unroll
     for (int s = 0; s < D + 2; ++s) {
-        if (s < D) stage<D, 0>(s, x0, h0, h1, cc);
-        if (s >= 1 && s - 1 < D) stage<D, 1>(s - 1, x1, h0, h1, cc);
-        if (s >= 2 && s - 2 < D) stage<D, 2>(s - 2, x2, h0, h1, cc);
+        if (s < D && (!FILL || i0 >= 2 * s)) stage<D, 0>(s, x0, h0, h1, cc);
+        if (s >= 1 && s - 1 < D && (!FILL || i0 + 1 >= 2 * (s - 1))) stage<D, 1>(s - 1, x1, h0, h1, cc);
+        if (s >= 2 && s - 2 < D && (!FILL || i0 + 2 >= 2 * (s - 2))) stage<D, 2>(s - 2, x2, h0, h1, cc);
     }
 }
 
@@ -194,11 +197,31 @@ __global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
     // the first group also goes through vmov, so no load is pending on the
     // loop's entry edge either (else the header waits for it every iteration)
     uint32_t x0 = vmov(load_next()), x1 = vmov(load_next()), x2 = vmov(load_next());
-    for (int oi = -2 * D; oi < rows_here; oi += 3) {
+    int oi = -2 * D;  // output row of the group's first input row (input index oi + 2D)
+    // Pipeline fill: the groups before the first output row, fully unrolled
+    // so every "stage t needs input index >= 2t" test folds at compile time
+    // (a runtime test would keep two versions of the stage registers live).
+    // Depth 32 fills without skipping to bound the code size.
+    constexpr int kFillGroups = (2 * D - 2 + 2) / 3;
+    if constexpr (D <= 16) {
+#pragma unroll
+        for (int g = 0; g < kFillGroups; ++g) {
+            const uint32_t n0 = load_next(), n1 = load_next(), n2 = load_next();
+            __builtin_amdgcn_sched_barrier(0);
+            uint32_t y0 = x0, y1 = x1, y2 = x2;
+            push_group<D, true>(y0, y1, y2, h0, h1, cc, 3 * g);
+            __builtin_amdgcn_sched_barrier(0);
+            x0 = vmov(n0);
+            x1 = vmov(n1);
+            x2 = vmov(n2);
+        }
+        oi += 3 * kFillGroups;
+    }
+    for (; oi < rows_here; oi += 3) {
         const uint32_t n0 = load_next(), n1 = load_next(), n2 = load_next();
         __builtin_amdgcn_sched_barrier(0);
         uint32_t y0 = x0, y1 = x1, y2 = x2;
-        push_group<D>(y0, y1, y2, h0, h1, cc);
+        push_group<D, false>(y0, y1, y2, h0, h1, cc, 0);
         emit(y0, oi);
         emit(y1, oi + 1);
         emit(y2, oi + 2);
