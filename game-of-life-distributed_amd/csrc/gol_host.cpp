@@ -145,7 +145,15 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
         }
 
     std::mutex mu;                 // the reference's `mu`: held by the turn loop and by pause
+    std::atomic<int> waiters{0};   // helpers queued for `mu` (std::mutex is not fair)
     std::atomic<int> turn{0};      // completed turns
+    // helpers take `mu` through this, so the turn loop can step aside for them
+    auto lock_mu = [&]() {
+        ++waiters;
+        std::unique_lock<std::mutex> g(mu);
+        --waiters;
+        return g;
+    };
     std::atomic<bool> finished{false}, quit{false};
     std::mutex tick_mu;
     std::condition_variable tick_cv;
@@ -174,7 +182,7 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
             uint64_t n = 0;
             int64_t at = 0;
             {
-                std::lock_guard<std::mutex> g(mu);  // blocked while paused, like the reference
+                auto g = lock_mu();  // blocked while paused, like the reference
                 check(golhip_alive_count(board.h, &n, &at));
             }
             Event e;
@@ -200,7 +208,7 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
                 std::string fname;
                 int t;
                 {
-                    std::lock_guard<std::mutex> g(mu);  // snapshot at a turn boundary
+                    auto g = lock_mu();  // snapshot at a turn boundary
                     t = turn.load();
                     fname = write_snapshot(t, quirks);
                 }
@@ -214,7 +222,7 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
                     break;
                 }
             } else if (k == U'p') {
-                std::unique_lock<std::mutex> g(mu);
+                auto g = lock_mu();
                 std::printf("%d\n", turn.load());
                 std::fflush(stdout);
                 if (!quirks) {
@@ -271,6 +279,8 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
                 t += n;
                 turn = t;
             }
+            // let a queued ticker / key handler take `mu` before the next turn
+            while (waiters.load() > 0) std::this_thread::sleep_for(std::chrono::microseconds(20));
             for (const util::Cell &c : flips) {  // initializeAliveCells (:212-220)
                 Event e;
                 e.kind = EventKind::CellFlipped;

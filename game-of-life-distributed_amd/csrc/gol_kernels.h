@@ -36,14 +36,15 @@ struct StepArgs {
 };
 
 // Bit-sliced temporal-blocked step: `depth` in {1,2,4,8,16,32}; requires W % 32 == 0.
-hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s);
+// fill_skip: skip the pipeline-fill stage-rows that only see padding.
+hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s, bool fill_skip = true);
 // One turn for any width (W % 32 != 0 boards such as 16x16).
 hipError_t launch_step_generic(const StepArgs &a, hipStream_t s);
 int tb_waves(const StepArgs &a, int depth);
 // Resident 256-thread blocks per CU of the depth-`depth` step kernel.
 int tb_blocks_per_cu(int depth);
 // Rows per wavefront minimising (rounds of waves) x (rows streamed per wave).
-int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots);
+int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_skip);
 
 hipError_t launch_pack(const uint8_t *bytes, uint32_t *words, int W, int Ww, int rows, hipStream_t s);
 hipError_t launch_unpack(const uint32_t *words, uint8_t *bytes, int W, int Ww, int rows, hipStream_t s);

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <type_traits>
 
 namespace golk {
 
@@ -113,25 +114,24 @@ __device__ __forceinline__ void stage(int t, uint32_t &x, uint32_t (&h0)[3][D], 
     x = nx;
 }
 
-// A group of 3 consecutive input rows through all D stages.  Stage t of row
-// i+1 needs stage t of row i (its row sum), so the rows run skewed by one
-// stage: (row0, t), (row1, t-1), (row2, t-2) are independent and interleave,
-// which hides the VALU->DPP hazard of each stage's serial chain.
-// FILL: the pipeline is still filling (input index i0 of row0 < 2(D-1)).
-// Stage t only receives real rows from input index 2t on, so earlier
-// stage-rows are skipped (their outputs would be garbage nobody stores).
-template <int D, bool FILL>
+// A group of 3 consecutive input rows through the first A of the D stages.
+// Stage t of row i+1 needs stage t of row i (its row sum), so the rows run
+// skewed by one stage: (row0, t), (row1, t-1), (row2, t-2) are independent and
+// interleave, which hides the VALU->DPP hazard of each stage's serial chain.
+// A < D is used while the pipeline fills: stage t only sees real rows from
+// input index 2t on, so later stages would only compute garbage.
+template <int D, int A>
 __device__ __forceinline__ void push_group(uint32_t &x0, uint32_t &x1, uint32_t &x2, uint32_t (&h0)[3][D],
-                                           uint32_t (&h1)[3][D], uint32_t (&cc)[3][D], int i0) {
+                                           uint32_t (&h1)[3][D], uint32_t (&cc)[3][D]) {
 #pragma unroll
-    for (int s = 0; s < D + 2; ++s) {
-        if (s < D && (!FILL || i0 >= 2 * s)) stage<D, 0>(s, x0, h0, h1, cc);
-        if (s >= 1 && s - 1 < D && (!FILL || i0 + 1 >= 2 * (s - 1))) stage<D, 1>(s - 1, x1, h0, h1, cc);
-        if (s >= 2 && s - 2 < D && (!FILL || i0 + 2 >= 2 * (s - 2))) stage<D, 2>(s - 2, x2, h0, h1, cc);
+    for (int s = 0; s < A + 2; ++s) {
+        if (s < A) stage<D, 0>(s, x0, h0, h1, cc);
+        if (s >= 1 && s - 1 < A) stage<D, 1>(s - 1, x1, h0, h1, cc);
+        if (s >= 2 && s - 2 < A) stage<D, 2>(s - 2, x2, h0, h1, cc);
     }
 }
 
-template <int D>
+template <int D, bool SKIP>
 __global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -198,30 +198,34 @@ __global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
     // loop's entry edge either (else the header waits for it every iteration)
     uint32_t x0 = vmov(load_next()), x1 = vmov(load_next()), x2 = vmov(load_next());
     int oi = -2 * D;  // output row of the group's first input row (input index oi + 2D)
-    // Pipeline fill: the groups before the first output row, fully unrolled
-    // so every "stage t needs input index >= 2t" test folds at compile time
-    // (a runtime test would keep two versions of the stage registers live).
-    // Depth 32 fills without skipping to bound the code size.
-    constexpr int kFillGroups = (2 * D - 2 + 2) / 3;
-    if constexpr (D <= 16) {
-#pragma unroll
-        for (int g = 0; g < kFillGroups; ++g) {
-            const uint32_t n0 = load_next(), n1 = load_next(), n2 = load_next();
-            __builtin_amdgcn_sched_barrier(0);
-            uint32_t y0 = x0, y1 = x1, y2 = x2;
-            push_group<D, true>(y0, y1, y2, h0, h1, cc, 3 * g);
-            __builtin_amdgcn_sched_barrier(0);
-            x0 = vmov(n0);
-            x1 = vmov(n1);
-            x2 = vmov(n2);
+    // Pipeline fill in three steps: while the group's last input index
+    // i = oi + 2D + 2 satisfies i/2 + 1 <= A, stages >= A cannot see real rows
+    // yet, so a body with only the first A = D/4, D/2, 3D/4 stages runs.
+    // Runtime loops keep the code small (a fully unrolled triangular fill
+    // thrashes the instruction cache beside the main loop).
+    auto fill = [&](auto a_tag) {
+        constexpr int A = decltype(a_tag)::value;
+        if constexpr (SKIP && A >= 1 && A < D) {
+            for (; (oi + 2 * D + 2) / 2 + 1 <= A; oi += 3) {
+                const uint32_t n0 = load_next(), n1 = load_next(), n2 = load_next();
+                __builtin_amdgcn_sched_barrier(0);
+                uint32_t y0 = x0, y1 = x1, y2 = x2;
+                push_group<D, A>(y0, y1, y2, h0, h1, cc);
+                __builtin_amdgcn_sched_barrier(0);
+                x0 = vmov(n0);
+                x1 = vmov(n1);
+                x2 = vmov(n2);
+            }
         }
-        oi += 3 * kFillGroups;
-    }
+    };
+    fill(std::integral_constant<int, D / 4>());
+    fill(std::integral_constant<int, D / 2>());
+    fill(std::integral_constant<int, 3 * D / 4>());
     for (; oi < rows_here; oi += 3) {
         const uint32_t n0 = load_next(), n1 = load_next(), n2 = load_next();
         __builtin_amdgcn_sched_barrier(0);
         uint32_t y0 = x0, y1 = x1, y2 = x2;
-        push_group<D, false>(y0, y1, y2, h0, h1, cc, 0);
+        push_group<D, D>(y0, y1, y2, h0, h1, cc);
         emit(y0, oi);
         emit(y1, oi + 1);
         emit(y2, oi + 2);
@@ -242,20 +246,21 @@ int tb_blocks_per_cu(int depth) {
     int b = 0;
     hipError_t e = hipErrorInvalidValue;
     switch (depth) {
-        case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<1>, 256, 0); break;
-        case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<2>, 256, 0); break;
-        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<4>, 256, 0); break;
-        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<8>, 256, 0); break;
-        case 16: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<16>, 256, 0); break;
-        case 32: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<32>, 256, 0); break;
+        case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<1, true>, 256, 0); break;
+        case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<2, true>, 256, 0); break;
+        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<4, true>, 256, 0); break;
+        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<8, true>, 256, 0); break;
+        case 16: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<16, true>, 256, 0); break;
+        case 32: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<32, true>, 256, 0); break;
         default: break;
     }
     return (e == hipSuccess && b > 0) ? b : 1;
 }
 
-int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots) {
-    // Each wave streams S + 2*depth rows; waves run in ceil(waves / slots)
-    // rounds.  Minimise rounds * (S + 2*depth) (fill overhead vs tail).
+int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_skip) {
+    // Each wave streams S + 2*depth rows (~S + 1.25*depth row-equivalents of
+    // work when the fill skips dead stages); waves run in ceil(waves / slots)
+    // rounds.  Minimise rounds * work (fill overhead vs tail).
     const int tiles_x = (Ww + kTileValid - 1) / kTileValid;
     int best_s = rows;
     double best = 1e300;
@@ -263,7 +268,7 @@ int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots) {
         const int S = (rows + strips - 1) / strips;
         const long long waves = (long long)tiles_x * ((rows + S - 1) / S);
         const long long rounds = (waves + wave_slots - 1) / wave_slots;
-        const double cost = (double)rounds * (S + 2 * depth);
+        const double cost = (double)rounds * (S + (fill_skip ? 2 * depth - 0.75 * depth : 2 * depth));
         if (cost < best * 0.999) {
             best = cost;
             best_s = S;
@@ -280,19 +285,24 @@ int tb_waves(const StepArgs &a, int depth) {
     return tiles_x * strips;
 }
 
-hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s) {
+template <bool SKIP>
+static hipError_t launch_tb(const StepArgs &a, int depth, hipStream_t s) {
     const int waves = tb_waves(a, depth);
     const dim3 grid((waves + 3) / 4), block(256);
     switch (depth) {
-        case 1: hipLaunchKernelGGL(gol_tb_kernel<1>, grid, block, 0, s, a); break;
-        case 2: hipLaunchKernelGGL(gol_tb_kernel<2>, grid, block, 0, s, a); break;
-        case 4: hipLaunchKernelGGL(gol_tb_kernel<4>, grid, block, 0, s, a); break;
-        case 8: hipLaunchKernelGGL(gol_tb_kernel<8>, grid, block, 0, s, a); break;
-        case 16: hipLaunchKernelGGL(gol_tb_kernel<16>, grid, block, 0, s, a); break;
-        case 32: hipLaunchKernelGGL(gol_tb_kernel<32>, grid, block, 0, s, a); break;
+        case 1: hipLaunchKernelGGL((gol_tb_kernel<1, SKIP>), grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((gol_tb_kernel<2, SKIP>), grid, block, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((gol_tb_kernel<4, SKIP>), grid, block, 0, s, a); break;
+        case 8: hipLaunchKernelGGL((gol_tb_kernel<8, SKIP>), grid, block, 0, s, a); break;
+        case 16: hipLaunchKernelGGL((gol_tb_kernel<16, SKIP>), grid, block, 0, s, a); break;
+        case 32: hipLaunchKernelGGL((gol_tb_kernel<32, SKIP>), grid, block, 0, s, a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s, bool fill_skip) {
+    return fill_skip ? launch_tb<true>(a, depth, s) : launch_tb<false>(a, depth, s);
 }
 
 // ---------------------------------------------------------------------------

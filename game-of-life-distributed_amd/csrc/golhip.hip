@@ -83,6 +83,7 @@ struct golhip {
     int tb_depth = 16;
     int rows_per_wave = 0;      // 0 = automatic (per depth, from occupancy)
     int cu_count = 0;
+    bool fill_skip = true;      // option "fill_skip"
     int auto_rpw[6] = {0, 0, 0, 0, 0, 0};  // cache per depth index
     bool loaded = false;
     std::atomic<int64_t> turns{0};
@@ -224,7 +225,7 @@ int rows_per_wave_for(golhip_t h, int depth) {
     int &c = h->auto_rpw[depth_index(depth)];
     if (c == 0) {
         const int slots = h->cu_count * golk::tb_blocks_per_cu(depth) * 4;
-        c = golk::auto_rows_per_wave(h->Ww, h->rows, depth, std::max(slots, 1));
+        c = golk::auto_rows_per_wave(h->Ww, h->rows, depth, std::max(slots, 1), h->fill_skip);
     }
     return c;
 }
@@ -301,7 +302,7 @@ int launch_depth(golhip_t h, int depth, bool count, bool halo) {
     }
     hipError_t e;
     if (h->W % 32 == 0)
-        e = golk::launch_step_tb(a, depth, h->stream);
+        e = golk::launch_step_tb(a, depth, h->stream, h->fill_skip);
     else
         e = golk::launch_step_generic(a, h->stream);
     if (e != hipSuccess) return fail(GOLHIP_EHIP, "step launch: %s", hipGetErrorString(e));
@@ -476,6 +477,18 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t r) {
     std::lock_guard<std::mutex> g(h->mu);
     h->rows_per_wave = r;
     return GOLHIP_OK;
+}
+
+int golhip_set_option(golhip_t h, const char *key, int64_t value) {
+    if (int rc = check(h)) return rc;
+    if (!key) return fail(GOLHIP_EINVAL, "null option");
+    std::lock_guard<std::mutex> g(h->mu);
+    if (!strcmp(key, "fill_skip")) {
+        h->fill_skip = value != 0;
+        for (int &c : h->auto_rpw) c = 0;
+        return GOLHIP_OK;
+    }
+    return fail(GOLHIP_EINVAL, "unknown option %s", key);
 }
 
 int golhip_comm_unique_id(uint8_t id[GOLHIP_UNIQUE_ID_BYTES]) {

@@ -89,6 +89,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "golhip_stream": ([H], ctypes.c_void_p),
         "golhip_set_tb_depth": ([H, i32], ctypes.c_int),
         "golhip_set_rows_per_wave": ([H, i32], ctypes.c_int),
+        "golhip_set_option": ([H, ctypes.c_char_p, i64], ctypes.c_int),
         "golhip_comm_unique_id": ([ctypes.c_char_p], ctypes.c_int),
         "golhip_comm_init": ([H, ctypes.c_char_p, i32, i32], ctypes.c_int),
         "golhip_group_step": ([P(H), i32, i64], ctypes.c_int),
@@ -190,6 +191,9 @@ class Board:
 
     def set_rows_per_wave(self, rows: int) -> None:
         _check(load().golhip_set_rows_per_wave(self._h, rows))
+
+    def set_option(self, key: str, value: int) -> None:
+        _check(load().golhip_set_option(self._h, key.encode(), value))
 
     def set_stream(self, stream_ptr: int) -> None:
         _check(load().golhip_set_stream(self._h, ctypes.c_void_p(stream_ptr)))

@@ -95,6 +95,9 @@ void *golhip_stream(golhip_t h);
  * kernel's occupancy).  Results never depend on them. */
 int golhip_set_tb_depth(golhip_t h, int32_t turns);
 int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
+/* Named engine options (kernel variants for A/B measurement); results never
+ * depend on them.  "fill_skip" (default 1): skip pipeline-fill stage-rows. */
+int golhip_set_option(golhip_t h, const char *key, int64_t value);
 
 /* ---- multi-GPU -------------------------------------------------------- */
 /* RCCL ring of strips: rank r's neighbours are r-1 (rows above) and r+1

@@ -1,4 +1,6 @@
-"""Tuning sweep (one process): GCUPS of the step kernel per (board, depth, rows_per_wave)."""
+"""Tuning sweep (one process, one device): GCUPS of the step kernel per
+(board, depth, rows_per_wave, engine options).  Variants are interleaved over
+--repeats rounds so device clock drift hits them alike; the best round is kept."""
 import argparse
 import json
 import os
@@ -13,25 +15,38 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--sizes", default="16384,65536")
 ap.add_argument("--depths", default="8,16,32")
 ap.add_argument("--rpw", default="0,32,64,128,256,512,1024")
+ap.add_argument("--variants", default="", help="semicolon-separated option sets, e.g. 'fill_skip=0;fill_skip=1'")
 ap.add_argument("--turns", type=int, default=256)
+ap.add_argument("--repeats", type=int, default=1)
 a = ap.parse_args()
+variants = [v for v in a.variants.split(";") if v] or [""]
 for N in map(int, a.sizes.split(",")):
     b = golhip.Board(N, N, timing=True)
     b.fill_random(0x5EED0001)
     for d in map(int, a.depths.split(",")):
         for s in map(int, a.rpw.split(",")):
-            b.set_tb_depth(d)
-            b.set_rows_per_wave(s)
-            b.step(2 * d)
-            b.sync()
-            b.perf_reset()
-            t0 = time.perf_counter()
-            b.step(a.turns)
-            b.sync()
-            dt = time.perf_counter() - t0
-            p = b.perf()
-            kern = p["step_kernel_ms"] / p["step_launches"]
-            rec = dict(N=N, depth=d, rpw=s, wall_gcups=N * N * a.turns / dt / 1e9,
-                       kernel_gcups=N * N * d / (kern * 1e-3) / 1e9, launch_ms=kern)
-            print(json.dumps(rec), flush=True)
+            best = {}
+            for _ in range(a.repeats):
+                for v in variants:
+                    opts = dict(kv.split("=") for kv in v.split(",") if kv)
+                    for k, val in opts.items():
+                        b.set_option(k, int(val))
+                    b.set_tb_depth(d)
+                    b.set_rows_per_wave(s)
+                    b.step(2 * d)
+                    b.sync()
+                    b.perf_reset()
+                    t0 = time.perf_counter()
+                    b.step(a.turns)
+                    b.sync()
+                    dt = time.perf_counter() - t0
+                    p = b.perf()
+                    kern = p["step_kernel_ms"] / p["step_launches"]
+                    rec = dict(N=N, depth=d, rpw=s, variant=v, rpw_used=p["rows_per_wave"],
+                               wall_gcups=N * N * a.turns / dt / 1e9,
+                               kernel_gcups=N * N * d / (kern * 1e-3) / 1e9, launch_ms=kern)
+                    if rec["wall_gcups"] > best.get(v, {"wall_gcups": 0})["wall_gcups"]:
+                        best[v] = rec
+            for v in variants:
+                print(json.dumps(best[v]), flush=True)
     b.close()

@@ -34,9 +34,11 @@ def img(fixtures, n):
     return unpack_bits(fixtures[f"image_{n}"], n)
 
 
-def run_gpu(board, turns, depth=16, rows_per_wave=0):
+def run_gpu(board, turns, depth=16, rows_per_wave=0, **options):
     H, W = board.shape
     with golhip.Board(W, H) as b:
+        for k, v in options.items():
+            b.set_option(k, v)
         b.set_tb_depth(depth)
         b.set_rows_per_wave(rows_per_wave)
         b.load_bytes(board)
@@ -155,10 +157,11 @@ def test_flips_after_multi_turn_step(fixtures):
 
 # ---------------------------------------------------------------- kernel geometry sweeps
 @pytest.mark.parametrize("depth", DEPTHS)
-@pytest.mark.parametrize("rpw", [1, 2, 5, 37, 512])
-def test_depth_and_strip_height_invariance(fixtures, depth, rpw):
+@pytest.mark.parametrize("rpw", [0, 1, 2, 5, 37, 512])
+@pytest.mark.parametrize("fill_skip", [0, 1])
+def test_depth_and_strip_height_invariance(fixtures, depth, rpw, fill_skip):
     board = img(fixtures, 256)
-    assert np.array_equal(run_gpu(board, 70, depth, rpw), run_np(board, 70))
+    assert np.array_equal(run_gpu(board, 70, depth, rpw, fill_skip=fill_skip), run_np(board, 70))
 
 
 @pytest.mark.parametrize("W,H", [(32, 1), (32, 3), (64, 2), (96, 7), (2016, 9), (1984, 33), (4000 - 4000 % 32, 40),
