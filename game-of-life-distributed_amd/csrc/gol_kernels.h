@@ -46,6 +46,26 @@ int tb_blocks_per_cu(int depth);
 // Rows per wavefront minimising (rounds of waves) x (rows streamed per wave).
 int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_skip);
 
+// Persistent multi-super-step step kernel (torus mode); see gol_kernels.hip K1p.
+struct PersistArgs {
+    StepArgs base;            // rows_out, in-map, dst_base, W/Ww, alive (last super-step)
+    uint32_t *buf0, *buf1;    // the two physical boards
+    int first;                // buffer holding generation 0 (0 -> buf0)
+    int J;                    // super-steps of `depth` turns
+    int S;                    // rows per wavefront
+    int wg_tx, wg_sy;         // workgroup block of (tiles, strips)
+    int cols, wg_y;           // workgroup grid
+    int tiles_x;
+    unsigned *progress;       // per workgroup, zeroed before launch
+    unsigned *error;          // set on a spin timeout
+    long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
+};
+int persist_waves_for(int depth);
+int persist_blocks_per_cu(int depth);
+// Workgroup shape / band height for `cus` resident workgroups; false if none fits.
+bool plan_persist(int Ww, int rows, int depth, int cus, PersistArgs *p);
+hipError_t launch_persist(const PersistArgs &p, int depth, hipStream_t s);
+
 hipError_t launch_pack(const uint8_t *bytes, uint32_t *words, int W, int Ww, int rows, hipStream_t s);
 hipError_t launch_unpack(const uint32_t *words, uint8_t *bytes, int W, int Ww, int rows, hipStream_t s);
 hipError_t launch_fill_random(uint32_t *words, int W, int Ww, int rows, int64_t row0, uint64_t seed,

@@ -131,24 +131,16 @@ __device__ __forceinline__ void push_group(uint32_t &x0, uint32_t &x1, uint32_t 
     }
 }
 
+// One wavefront streams output rows [r0, r0 + rows_here) of the tile whose
+// first stored word is t0, D turns ahead; returns the popcount of its stored
+// output words.  Shared by the per-launch and the persistent kernel.
 template <int D, bool SKIP>
-__global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
+__device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int rows_here, int t0) {
     const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     const int Ww = a.Ww;
-    const int tiles_x = (Ww + kTileValid - 1) / kTileValid;
-    const int S = a.rows_per_wave;
-    const int strip = wave / tiles_x;
-    const int tile = wave - strip * tiles_x;
-    const int r0 = strip * S;
-    if (r0 >= a.rows_out) return;  // wave-uniform
-
-    const int t0 = tile * kTileValid;
     int col = (t0 + lane - 1) % Ww;
     if (col < 0) col += Ww;
     const bool keep = lane >= 1 && lane <= kTileValid && (t0 + lane - 1) < Ww;
-
-    const int rows_here = min(S, a.rows_out - r0);
 
     // input row cursor (wave-uniform)
     int r = r0 - D + a.in.off;
@@ -236,10 +228,167 @@ __global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
         x1 = vmov(n1);
         x2 = vmov(n2);
     }
+    return cnt;
+}
+
+template <int D, bool SKIP>
+__global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
+    const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int tiles_x = (a.Ww + kTileValid - 1) / kTileValid;
+    const int S = a.rows_per_wave;
+    const int strip = wave / tiles_x;
+    const int tile = wave - strip * tiles_x;
+    const int r0 = strip * S;
+    if (r0 >= a.rows_out) return;  // wave-uniform
+    const uint32_t cnt = stream_band<D, SKIP>(a, r0, min(S, a.rows_out - r0), tile * kTileValid);
     if (a.alive) {
         const uint32_t tot = wave_sum_u32(cnt);
-        if (lane == 0) atomicAdd(a.alive, (unsigned long long)tot);
+        if ((threadIdx.x & 63) == 0) atomicAdd(a.alive, (unsigned long long)tot);
     }
+}
+
+// ---------------------------------------------------------------------------
+// K1p: persistent multi-super-step kernel (torus mode, one device).
+//
+// One workgroup of NW wavefronts per CU stays resident for J super-steps of
+// D turns.  Workgroup (wy, wx) owns a wg_tx x wg_sy block of (tile, strip)
+// units; super-step j reads generation jD from buf[(first + j) & 1] and
+// writes generation (j+1)D to the other buffer.  Its inputs are the outputs
+// of its 3 x 3 workgroup neighbourhood at super-step j-1, and the buffer it
+// overwrites was last read by that same neighbourhood during j-1, so the one
+// wait "all 9 neighbours finished j-1" covers both hazards.  Hand-off per
+// MI355X guide Guideline 16: stores -> vmcnt(0) -> barrier -> lane 0
+// release fence -> vmcnt(0) -> relaxed agent store of the progress counter;
+// consumer: relaxed agent polls -> lane 0 acquire fence -> vmcnt(0) ->
+// barrier -> loads.  Every spin is bounded: on timeout the kernel sets
+// *error and all workgroups drain out.
+// ---------------------------------------------------------------------------
+template <int D>
+constexpr int persist_waves() { return D <= 16 ? 16 : 8; }
+
+template <int D>
+__global__ __launch_bounds__(persist_waves<D>() * 64) void gol_persist_kernel(PersistArgs p) {
+    constexpr int NW = persist_waves<D>();
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = blockIdx.x;
+    const int wx = b % p.cols, wy = b / p.cols;
+    const int tile = wx * p.wg_tx + w % p.wg_tx;
+    const int strip = wy * p.wg_sy + w / p.wg_tx;
+    const int r0 = strip * p.S;
+    const int rows_here = (tile < p.tiles_x && r0 < p.base.rows_out) ? min(p.S, p.base.rows_out - r0) : 0;
+    (void)NW;
+
+    // neighbour workgroup polled by lane k < 9
+    int nb = b;
+    if (lane < 9) {
+        const int ny = (wy + lane / 3 - 1 + p.wg_y) % p.wg_y;
+        const int nx = (wx + lane % 3 - 1 + p.cols) % p.cols;
+        nb = ny * p.cols + nx;
+    }
+    __shared__ int s_abort;
+    if (threadIdx.x == 0) s_abort = 0;
+    __syncthreads();
+
+    uint32_t cnt = 0;
+    for (int j = 0; j < p.J; ++j) {
+        if (j > 0) {
+            if (w == 0) {
+                const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
+                for (;;) {
+                    const unsigned v = __hip_atomic_load(&p.progress[nb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (__all(v >= (unsigned)j)) break;
+                    const unsigned err = __hip_atomic_load(p.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (err || (long long)__builtin_amdgcn_s_memrealtime() - t_start > p.timeout_ticks) {
+                        if (lane == 0) {
+                            atomicOr(p.error, 1u);
+                            s_abort = 1;
+                        }
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if (lane == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();
+            if (s_abort) return;  // uniform over the workgroup
+        }
+        StepArgs a = p.base;
+        const bool odd = ((p.first + j) & 1) != 0;
+        a.src = odd ? p.buf1 : p.buf0;
+        a.dst = odd ? p.buf0 : p.buf1;
+        cnt = rows_here > 0 ? stream_band<D, true>(a, r0, rows_here, tile * kTileValid) : 0u;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&p.progress[b], (unsigned)(j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (p.base.alive) {
+        const uint32_t tot = wave_sum_u32(cnt);
+        if (lane == 0 && tot) atomicAdd(p.base.alive, (unsigned long long)tot);
+    }
+}
+
+int persist_waves_for(int depth) { return depth <= 16 ? 16 : 8; }
+
+int persist_blocks_per_cu(int depth) {
+    int b = 0;
+    hipError_t e = hipErrorInvalidValue;
+    switch (depth) {
+        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_persist_kernel<4>, 64 * persist_waves<4>(), 0); break;
+        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_persist_kernel<8>, 64 * persist_waves<8>(), 0); break;
+        case 16: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_persist_kernel<16>, 64 * persist_waves<16>(), 0); break;
+        case 32: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_persist_kernel<32>, 64 * persist_waves<32>(), 0); break;
+        default: break;
+    }
+    return e == hipSuccess ? b : 0;
+}
+
+bool plan_persist(int Ww, int rows, int depth, int cus, PersistArgs *p) {
+    const int NW = persist_waves_for(depth);
+    const int tiles_x = (Ww + kTileValid - 1) / kTileValid;
+    bool found = false;
+    long best_s = 0;
+    for (int wg_tx = 1; wg_tx <= NW; wg_tx *= 2) {
+        const int wg_sy = NW / wg_tx;
+        const int cols = (tiles_x + wg_tx - 1) / wg_tx;
+        // as many workgroup rows as CUs allow, but bands of >= depth rows
+        const int wg_y = std::min(cus / cols, rows / (wg_sy * depth));
+        if (wg_y < 1) continue;
+        const int strips = wg_y * wg_sy;
+        const int S = (rows + strips - 1) / strips;
+        if (S < depth) continue;                         // halo rows from the adjacent strip only
+        // every workgroup row must hold >= depth real rows (its neighbours' halos)
+        const int last_rows = rows - (wg_y - 1) * wg_sy * S;
+        if (last_rows < depth) continue;
+        if (!found || S < best_s) {
+            found = true;
+            best_s = S;
+            p->wg_tx = wg_tx;
+            p->wg_sy = wg_sy;
+            p->cols = cols;
+            p->wg_y = wg_y;
+            p->S = S;
+            p->tiles_x = tiles_x;
+        }
+    }
+    return found;
+}
+
+hipError_t launch_persist(const PersistArgs &p, int depth, hipStream_t s) {
+    const dim3 grid(p.cols * p.wg_y), block(64 * persist_waves_for(depth));
+    switch (depth) {
+        case 4: hipLaunchKernelGGL(gol_persist_kernel<4>, grid, block, 0, s, p); break;
+        case 8: hipLaunchKernelGGL(gol_persist_kernel<8>, grid, block, 0, s, p); break;
+        case 16: hipLaunchKernelGGL(gol_persist_kernel<16>, grid, block, 0, s, p); break;
+        case 32: hipLaunchKernelGGL(gol_persist_kernel<32>, grid, block, 0, s, p); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 int tb_blocks_per_cu(int depth) {

@@ -84,6 +84,12 @@ struct golhip {
     int rows_per_wave = 0;      // 0 = automatic (per depth, from occupancy)
     int cu_count = 0;
     bool fill_skip = true;      // option "fill_skip"
+    bool persistent = true;     // option "persistent": K1p for long torus runs
+    int persist_depth = 0;      // option "persist_depth" (0: tb_depth)
+    unsigned *d_sync = nullptr; // persistent kernel: [0] error, [1..] progress per workgroup
+    unsigned *h_err = nullptr;  // pinned copy of the error word
+    bool persist_pending = false;
+    int64_t persist_launches = 0;
     int auto_rpw[6] = {0, 0, 0, 0, 0, 0};  // cache per depth index
     bool loaded = false;
     std::atomic<int64_t> turns{0};
@@ -322,6 +328,85 @@ int launch_depth(golhip_t h, int depth, bool count, bool halo) {
     return GOLHIP_OK;
 }
 
+// After any stream sync: a persistent launch that timed out leaves the board
+// undefined, so it is reported (loudly) and the persistent path is disabled.
+int check_persist(golhip_t h) {
+    if (!h->persist_pending) return GOLHIP_OK;
+    h->persist_pending = false;
+    if (*h->h_err) {
+        *h->h_err = 0;
+        h->persistent = false;
+        return fail(GOLHIP_EHIP, "persistent step kernel timed out waiting for a neighbour workgroup "
+                                 "(not all workgroups resident?); board state is undefined, persistent mode disabled");
+    }
+    return GOLHIP_OK;
+}
+
+int sync_stream(golhip_t h) {
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    return check_persist(h);
+}
+
+// J super-steps of `depth` turns in one resident launch; returns the turns
+// run (0 if the persistent path does not apply).
+int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
+    *rc = GOLHIP_OK;
+    if (!h->persistent || h->W % 32 != 0 || !h->torus()) return 0;
+    const int depth = largest_depth(h->persist_depth > 0 ? h->persist_depth : h->tb_depth);
+    if (depth < 4) return 0;
+    const int64_t J = left / depth;
+    if (J < 2) return 0;
+    if (golk::persist_blocks_per_cu(depth) < 1) return 0;
+    golk::PersistArgs p{};
+    if (!golk::plan_persist(h->Ww, h->rows, depth, h->cu_count, &p)) return 0;
+    if (!h->d_sync) {
+        if (hipMalloc(&h->d_sync, (size_t)(h->cu_count + 2) * sizeof(unsigned)) != hipSuccess ||
+            hipHostMalloc(&h->h_err, sizeof(unsigned), hipHostMallocDefault) != hipSuccess) {
+            *rc = fail(GOLHIP_ENOMEM, "persistent sync words");
+            return 0;
+        }
+        *h->h_err = 0;
+    }
+    const bool count = count_last && J * depth == left;
+    if (count) {
+        hipError_t e = hipMemsetAsync(h->d_scalars, 0, sizeof(unsigned long long), h->stream);
+        if (e != hipSuccess) { *rc = fail(GOLHIP_EHIP, "memset: %s", hipGetErrorString(e)); return 0; }
+    }
+    hipError_t e = hipMemsetAsync(h->d_sync, 0, (size_t)(h->cu_count + 2) * sizeof(unsigned), h->stream);
+    p.base = step_args(h, count ? h->d_scalars : nullptr, false);
+    p.buf0 = h->buf[0];
+    p.buf1 = h->buf[1];
+    p.first = h->cur;
+    p.J = (int)J;
+    p.error = h->d_sync;
+    p.progress = h->d_sync + 1;
+    p.timeout_ticks = 100000000ll;  // 1 s at the 100 MHz s_memrealtime clock
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (e == hipSuccess && (h->flags & GOLHIP_FLAG_TIMING)) {
+        e0 = take_event(h);
+        e1 = take_event(h);
+        if (e0 && e1) e = hipEventRecord(e0, h->stream);
+    }
+    if (e == hipSuccess) e = golk::launch_persist(p, depth, h->stream);
+    if (e == hipSuccess && e1) {
+        e = hipEventRecord(e1, h->stream);
+        h->ev_pending.emplace_back(e0, e1);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(h->h_err, h->d_sync, sizeof(unsigned), hipMemcpyDeviceToHost, h->stream);
+    if (e != hipSuccess) {
+        *rc = fail(GOLHIP_EHIP, "persistent launch: %s", hipGetErrorString(e));
+        return 0;
+    }
+    h->persist_pending = true;
+    if (J & 1) h->cur ^= 1;
+    h->turns += J * depth;
+    h->step_launches++;
+    h->step_turns += J * depth;
+    h->persist_launches++;
+    if (count) h->alive_turn = h->turns;
+    return J * depth;
+}
+
 int start_flips(golhip_t h) {
     const int64_t nw = h->local_words();
     const int64_t nb = golk::compact_blocks(nw);
@@ -338,7 +423,7 @@ int start_flips(golhip_t h) {
 int finish_compact(golhip_t h, const uint32_t *a, const uint32_t *b, int32_t *xy, uint64_t cap, uint64_t *n) {
     HIP_OR_FAIL(hipMemcpyAsync(h->h_scalars + 1, h->d_scalars + 1, sizeof(unsigned long long), hipMemcpyDeviceToHost,
                                h->stream));
-    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (int rc_ = sync_stream(h)) return rc_;
     const uint64_t total = h->h_scalars[1];
     if (n) *n = total;
     if (total > cap || (!xy && total > 0))
@@ -349,7 +434,7 @@ int finish_compact(golhip_t h, const uint32_t *a, const uint32_t *b, int32_t *xy
     if (rc) return rc;
     HIP_OR_FAIL(golk::launch_compact_scatter(a, b, h->local_words(), h->Ww, h->row0, h->d_blk, h->d_xy, h->stream));
     HIP_OR_FAIL(hipMemcpyAsync(xy, h->d_xy, total * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, h->stream));
-    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (int rc_ = sync_stream(h)) return rc_;
     return GOLHIP_OK;
 }
 
@@ -445,6 +530,8 @@ int golhip_destroy(golhip_t h) {
     HIP_RC(hipFree(h->d_blk));
     HIP_RC(hipFree(h->d_xy));
     HIP_RC(hipFree(h->d_stage));
+    HIP_RC(hipFree(h->d_sync));
+    if (h->h_err) HIP_RC(hipHostFree(h->h_err));
     if (h->own_stream && h->stream) HIP_RC(hipStreamDestroy(h->stream));
     delete h;
     return rc;
@@ -454,7 +541,7 @@ int golhip_set_stream(golhip_t h, void *s) {
     if (int rc = check(h)) return rc;
     std::lock_guard<std::mutex> g(h->mu);
     if (int rc = set_dev(h)) return rc;
-    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (int rc_ = sync_stream(h)) return rc_;
     if (h->own_stream) HIP_OR_FAIL(hipStreamDestroy(h->stream));
     h->own_stream = false;
     h->stream = (hipStream_t)s;
@@ -483,6 +570,15 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     if (int rc = check(h)) return rc;
     if (!key) return fail(GOLHIP_EINVAL, "null option");
     std::lock_guard<std::mutex> g(h->mu);
+    if (!strcmp(key, "persistent")) {
+        h->persistent = value != 0;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "persist_depth")) {
+        if (value < 0 || value > GOLHIP_MAX_TB_DEPTH) return fail(GOLHIP_EINVAL, "persist_depth %lld", (long long)value);
+        h->persist_depth = (int)value;
+        return GOLHIP_OK;
+    }
     if (!strcmp(key, "fill_skip")) {
         h->fill_skip = value != 0;
         for (int &c : h->auto_rpw) c = 0;
@@ -536,7 +632,7 @@ int golhip_load_bytes(golhip_t h, const uint8_t *cells) {
         HIP_OR_FAIL(hipMemcpyAsync(h->d_stage, cells + r * h->W, (size_t)(n * h->W), hipMemcpyHostToDevice, h->stream));
         HIP_OR_FAIL(golk::launch_pack(h->d_stage, h->cur_rows() + r * h->Ww, h->W, h->Ww, (int)n, h->stream));
     }
-    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (int rc_ = sync_stream(h)) return rc_;
     h->loaded = true;
     h->turns = 0;
     h->alive_turn = -1;
@@ -550,7 +646,7 @@ int golhip_load_bits(golhip_t h, const uint32_t *words) {
     std::lock_guard<std::mutex> g(h->mu);
     if (int rc = set_dev(h)) return rc;
     HIP_OR_FAIL(hipMemcpyAsync(h->cur_rows(), words, (size_t)h->local_words() * 4, hipMemcpyHostToDevice, h->stream));
-    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (int rc_ = sync_stream(h)) return rc_;
     h->loaded = true;
     h->turns = 0;
     h->alive_turn = -1;
@@ -563,7 +659,7 @@ int golhip_fill_random(golhip_t h, uint64_t seed) {
     std::lock_guard<std::mutex> g(h->mu);
     if (int rc = set_dev(h)) return rc;
     HIP_OR_FAIL(golk::launch_fill_random(h->cur_rows(), h->W, h->Ww, h->rows, h->row0, seed, h->stream));
-    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (int rc_ = sync_stream(h)) return rc_;
     h->loaded = true;
     h->turns = 0;
     h->alive_turn = -1;
@@ -582,6 +678,11 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     int64_t left = nturns;
     const int64_t tail = want_flips ? 1 : 0;
     const bool halo = h->nranks > 1;
+    if (!halo) {
+        int rc = GOLHIP_OK;
+        left -= try_persist(h, left - tail, tail == 0, &rc);
+        if (rc) return rc;
+    }
     while (left > tail) {
         const int d = next_depth(h, left - tail, halo);
         if (halo)
@@ -667,7 +768,7 @@ int golhip_sync(golhip_t h) {
     if (int rc = check(h)) return rc;
     std::lock_guard<std::mutex> g(h->mu);
     if (int rc = set_dev(h)) return rc;
-    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (int rc_ = sync_stream(h)) return rc_;
     return GOLHIP_OK;
 }
 
@@ -689,7 +790,7 @@ int golhip_alive_count(golhip_t h, uint64_t *count, int64_t *at_turn) {
         h->alive_turn = h->turns;
     }
     HIP_OR_FAIL(hipMemcpyAsync(h->h_scalars, h->d_scalars, sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
-    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (int rc_ = sync_stream(h)) return rc_;
     *count = h->h_scalars[0];
     if (at_turn) *at_turn = h->alive_turn;
     return GOLHIP_OK;
@@ -704,7 +805,7 @@ int golhip_alive_count_global(golhip_t h, uint64_t *count, int64_t *at_turn) {
     NCCL_OR_FAIL(ncclAllReduce(h->d_scalars + 3, h->d_scalars + 3, 1, ncclUint64, ncclSum, h->comm, h->stream));
     HIP_OR_FAIL(hipMemcpyAsync(h->h_scalars + 3, h->d_scalars + 3, sizeof(unsigned long long), hipMemcpyDeviceToHost,
                                h->stream));
-    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (int rc_ = sync_stream(h)) return rc_;
     *count = h->h_scalars[3];
     return GOLHIP_OK;
 }
@@ -745,7 +846,7 @@ int golhip_snapshot_bytes(golhip_t h, uint8_t *out) {
         HIP_OR_FAIL(golk::launch_unpack(h->cur_rows() + r * h->Ww, h->d_stage, h->W, h->Ww, (int)n, h->stream));
         HIP_OR_FAIL(hipMemcpyAsync(out + r * h->W, h->d_stage, (size_t)(n * h->W), hipMemcpyDeviceToHost, h->stream));
     }
-    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (int rc_ = sync_stream(h)) return rc_;
     return GOLHIP_OK;
 }
 
@@ -755,7 +856,7 @@ int golhip_snapshot_bits(golhip_t h, uint32_t *out) {
     std::lock_guard<std::mutex> g(h->mu);
     if (int rc = set_dev(h)) return rc;
     HIP_OR_FAIL(hipMemcpyAsync(out, h->cur_rows(), (size_t)h->local_words() * 4, hipMemcpyDeviceToHost, h->stream));
-    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (int rc_ = sync_stream(h)) return rc_;
     return GOLHIP_OK;
 }
 
@@ -768,7 +869,7 @@ int golhip_board_hash(golhip_t h, uint64_t *hash) {
     HIP_OR_FAIL(golk::launch_hash(h->cur_rows(), h->local_words(), (int64_t)h->row0 * h->Ww, h->d_scalars + 2, h->stream));
     HIP_OR_FAIL(hipMemcpyAsync(h->h_scalars + 2, h->d_scalars + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost,
                                h->stream));
-    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (int rc_ = sync_stream(h)) return rc_;
     *hash = h->h_scalars[2];
     return GOLHIP_OK;
 }
@@ -778,6 +879,7 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     if (!out) return fail(GOLHIP_EINVAL, "null out");
     std::lock_guard<std::mutex> g(h->mu);
     if (int rc = set_dev(h)) return rc;
+    if (int rc = sync_stream(h)) return rc;
     if (int rc = drain_events(h)) return rc;
     memset(out, 0, sizeof *out);
     out->turns = h->turns;

@@ -292,3 +292,33 @@ def test_full_size_fill_sample_rows(coracle):
         from oracle.oracle import splitmix64_np
         row = np.where((splitmix64_np(np.uint64(seed) ^ idx) & np.uint64(3)) == 0, 255, 0).astype(np.uint8)
         assert np.array_equal(unpack_bits(bits[r:r + 1], N)[0], row)
+
+
+# ---------------------------------------------------------------- persistent kernel (K1p)
+@pytest.mark.parametrize("N,depth", [(1024, 4), (2048, 8), (2048, 16), (4096, 32), (3968, 16)])
+def test_persistent_matches_oracle(coracle, N, depth):
+    """Resident multi-super-step kernel vs the C oracle (and vs the per-launch path)."""
+    board = coracle.fill_random(N, N // 2, 0x5EED0007)
+    want = coracle.run(board, 3 * depth + 5)
+    outs = {}
+    for persistent in (1, 0):
+        with golhip.Board(N, N // 2) as b:
+            b.set_option("persistent", persistent)
+            b.set_tb_depth(depth)
+            b.load_bytes(board)
+            b.step(3 * depth + 5)
+            outs[persistent] = b.snapshot_bytes()
+            assert b.alive_count() == (int((want == 255).sum()), 3 * depth + 5)
+    assert np.array_equal(outs[1], want) and np.array_equal(outs[0], want)
+
+
+@pytest.mark.parametrize("N,turns", [(16384, 512), (65536, 64)])
+def test_persistent_full_size_matches_per_launch(N, turns):
+    res = []
+    for persistent in (1, 0):
+        with golhip.Board(N, N) as b:
+            b.set_option("persistent", persistent)
+            b.fill_random(0x5EED0001)
+            b.step(turns)
+            res.append((b.board_hash(), b.alive_count()))
+    assert res[0] == res[1]
