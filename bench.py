@@ -103,7 +103,7 @@ def main():
         W = H = N
         rows = H // world
     row0 = rank * rows
-    turns_per_step = a.turns_per_step or (1000 if N <= 16384 else (100 if N <= 65536 else 10))
+    turns_per_step = a.turns_per_step or (1000 if N <= 16384 else 100)
 
     import torch
     torch.cuda.set_device(local)
@@ -149,15 +149,21 @@ def main():
     total_updates = W * H * turns_per_step * a.steps if wl["scaling"] == "weak" or world == 1 \
         else W * H * turns_per_step * a.steps
     gcups = total_updates / dt / 1e9
-    # dominant kernel: the fused step launch, timed with HIP events on the engine stream
-    launches = max(1, perf["step_launches"])
-    avg_ms = perf["step_kernel_ms"] / launches
-    alg_bytes_per_launch = W * rows * (perf["step_turns"] / launches) * ALG_BYTES_PER_UPDATE
+    # dominant kernel (by device time): the persistent or the per-launch step
+    # kernel, each timed with HIP events on the engine stream around every launch
+    if perf["persist_kernel_ms"] >= perf["step_kernel_ms"]:
+        kname, launches, kms, kturns = "gol_persist_kernel", perf["persist_launches"], perf["persist_kernel_ms"], \
+            perf["persist_turns"]
+    else:
+        kname, launches, kms, kturns = "gol_tb_kernel", perf["step_launches"], perf["step_kernel_ms"], perf["step_turns"]
+    launches = max(1, launches)
+    avg_ms = kms / launches
+    alg_bytes_per_launch = W * rows * (kturns / launches) * ALG_BYTES_PER_UPDATE
     achieved = alg_bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else None
     traffic = None
     try:
         with open(a.pmc) as f:
-            rec = json.load(f).get(f"{N}x{a.tb_depth}")
+            rec = json.load(f).get(f"{N}:{kname}")
         if rec:
             traffic = rec["hbm_bytes_per_launch"]
     except (OSError, ValueError):
@@ -192,13 +198,15 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
             "traffic": traffic,
-            "kernel": f"gol_tb_kernel<{perf['tb_depth']}>",
+            "kernel": f"{kname}<{perf['tb_depth']}>",
             "avg_launch_ms": round(avg_ms, 5),
-            "launches": perf["step_launches"],
+            "launches": launches,
+            "turns_per_launch": kturns / launches,
             "alg_bytes_per_launch": alg_bytes_per_launch,
-            "note": "achieved = 0.25 B/cell-update x updates per launch / avg launch time; "
-                    "one launch fuses tb_depth turns, so frac > 1 means temporal blocking beat "
-                    "the single-pass HBM roofline",
+            "note": "achieved = 0.25 B/cell-update (SURVEY 8d) x cell-updates per launch / avg launch time; "
+                    "a launch fuses many turns, so frac > 1 means temporal blocking beat the single-pass "
+                    "HBM roofline (the kernel is VALU-bound, see DESIGN.md 5); traffic = measured HBM bytes "
+                    "per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE) from profiles/pmc_traffic.json",
         },
         "final_alive": alive,
         "final_turn": at_turn,

@@ -113,9 +113,14 @@ struct golhip {
 
     // measurement
     std::vector<hipEvent_t> ev_pool;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
-    double step_ms = 0;
+    struct Timed {
+        hipEvent_t e0, e1;
+        bool persistent;
+    };
+    std::vector<Timed> ev_pending;
+    double step_ms = 0, persist_ms = 0;
     int64_t step_launches = 0, step_turns = 0, halo_bytes = 0;
+    int64_t persist_turns = 0;
 
     std::mutex mu;
 
@@ -249,12 +254,12 @@ hipEvent_t take_event(golhip_t h) {
 
 int drain_events(golhip_t h) {
     for (auto &p : h->ev_pending) {
-        HIP_OR_FAIL(hipEventSynchronize(p.second));
+        HIP_OR_FAIL(hipEventSynchronize(p.e1));
         float ms = 0;
-        HIP_OR_FAIL(hipEventElapsedTime(&ms, p.first, p.second));
-        h->step_ms += ms;
-        h->ev_pool.push_back(p.first);
-        h->ev_pool.push_back(p.second);
+        HIP_OR_FAIL(hipEventElapsedTime(&ms, p.e0, p.e1));
+        (p.persistent ? h->persist_ms : h->step_ms) += ms;
+        h->ev_pool.push_back(p.e0);
+        h->ev_pool.push_back(p.e1);
     }
     h->ev_pending.clear();
     return GOLHIP_OK;
@@ -314,7 +319,7 @@ int launch_depth(golhip_t h, int depth, bool count, bool halo) {
     if (e != hipSuccess) return fail(GOLHIP_EHIP, "step launch: %s", hipGetErrorString(e));
     if (e1) {
         HIP_OR_FAIL(hipEventRecord(e1, h->stream));
-        h->ev_pending.emplace_back(e0, e1);
+        h->ev_pending.push_back({e0, e1, false});
         if (h->ev_pending.size() >= 4096) {
             int rc = drain_events(h);
             if (rc) return rc;
@@ -390,7 +395,7 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     if (e == hipSuccess) e = golk::launch_persist(p, depth, h->stream);
     if (e == hipSuccess && e1) {
         e = hipEventRecord(e1, h->stream);
-        h->ev_pending.emplace_back(e0, e1);
+        h->ev_pending.push_back({e0, e1, true});
     }
     if (e == hipSuccess) e = hipMemcpyAsync(h->h_err, h->d_sync, sizeof(unsigned), hipMemcpyDeviceToHost, h->stream);
     if (e != hipSuccess) {
@@ -400,8 +405,7 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     h->persist_pending = true;
     if (J & 1) h->cur ^= 1;
     h->turns += J * depth;
-    h->step_launches++;
-    h->step_turns += J * depth;
+    h->persist_turns += J * depth;
     h->persist_launches++;
     if (count) h->alive_turn = h->turns;
     return J * depth;
@@ -517,8 +521,8 @@ int golhip_destroy(golhip_t h) {
     HIP_RC(hipSetDevice(h->device));
     if (h->stream) HIP_RC(hipStreamSynchronize(h->stream));
     for (auto &p : h->ev_pending) {
-        HIP_RC(hipEventDestroy(p.first));
-        HIP_RC(hipEventDestroy(p.second));
+        HIP_RC(hipEventDestroy(p.e0));
+        HIP_RC(hipEventDestroy(p.e1));
     }
     for (auto e : h->ev_pool) HIP_RC(hipEventDestroy(e));
     if (h->comm && ncclCommDestroy(h->comm) != ncclSuccess && rc == GOLHIP_OK)
@@ -886,7 +890,10 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     out->step_launches = h->step_launches;
     out->step_turns = h->step_turns;
     out->step_kernel_ms = h->step_ms;
-    out->cell_updates = (int64_t)h->W * h->rows * h->step_turns;
+    out->persist_launches = h->persist_launches;
+    out->persist_turns = h->persist_turns;
+    out->persist_kernel_ms = h->persist_ms;
+    out->cell_updates = (int64_t)h->W * h->rows * (h->step_turns + h->persist_turns);
     out->alg_bytes = out->cell_updates / 4;
     out->halo_bytes = h->halo_bytes;
     out->tb_depth = h->tb_depth;
@@ -900,8 +907,9 @@ int golhip_perf_reset(golhip_t h) {
     std::lock_guard<std::mutex> g(h->mu);
     if (int rc = set_dev(h)) return rc;
     if (int rc = drain_events(h)) return rc;
-    h->step_ms = 0;
+    h->step_ms = h->persist_ms = 0;
     h->step_launches = h->step_turns = h->halo_bytes = 0;
+    h->persist_launches = h->persist_turns = 0;
     return GOLHIP_OK;
 }
 

@@ -35,6 +35,9 @@ class Perf(ctypes.Structure):
         ("step_launches", ctypes.c_int64),
         ("step_turns", ctypes.c_int64),
         ("step_kernel_ms", ctypes.c_double),
+        ("persist_launches", ctypes.c_int64),
+        ("persist_turns", ctypes.c_int64),
+        ("persist_kernel_ms", ctypes.c_double),
         ("cell_updates", ctypes.c_int64),
         ("alg_bytes", ctypes.c_int64),
         ("halo_bytes", ctypes.c_int64),

@@ -56,10 +56,13 @@ typedef golhip *golhip_t;
 
 typedef struct golhip_perf {
     int64_t turns;            /* turns completed since the last load/fill     */
-    int64_t step_launches;    /* step-kernel launches since golhip_perf_reset */
+    int64_t step_launches;    /* per-launch step kernels (gol_tb_kernel) since golhip_perf_reset */
     int64_t step_turns;       /* turns run by those launches                  */
-    double step_kernel_ms;    /* summed device time of those launches (TIMING)*/
-    int64_t cell_updates;     /* width * local rows * step_turns              */
+    double step_kernel_ms;    /* their summed device time (GOLHIP_FLAG_TIMING)*/
+    int64_t persist_launches; /* persistent step kernels (gol_persist_kernel) */
+    int64_t persist_turns;    /* turns run by those                           */
+    double persist_kernel_ms; /* their summed device time (GOLHIP_FLAG_TIMING)*/
+    int64_t cell_updates;     /* width * local rows * all stepped turns       */
     int64_t alg_bytes;        /* 0.25 B per cell-update (1 bit in + 1 bit out)*/
     int64_t halo_bytes;       /* bytes sent to neighbour ranks                */
     int32_t tb_depth;         /* turns fused per step launch                  */

@@ -1,0 +1,58 @@
+"""BASELINE configs[4]: 5120 x 5120 board with the full event stream.
+
+Prints one JSON object with:
+  events_off      fused turns (no per-turn side channels), GCUPS
+  events_on       one turn per step + the turn's CellFlipped list copied to the
+                  host (golhip_flips, row-major) + AliveCellsCount every 2 s:
+                  turns/s, flips/s, GCUPS
+  snapshot_s      one 's' snapshot (golhip_snapshot_bytes + PGM write), ms
+The synthetic board is the counter-hash generator with seed 0x5EED0005.
+"""
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "game-of-life-distributed_amd")]
+import golhip  # noqa: E402
+from oracle.oracle import pgm_bytes  # noqa: E402  (PGM header format only)
+
+N = 5120
+SEED = 0x5EED0005
+out = {"workload": "configs[4]: 5120^2 random 25%, seed 0x5EED0005", "board": [N, N]}
+
+with golhip.Board(N, N, timing=True) as b:
+    b.fill_random(SEED)
+    b.step(64)
+    b.sync()
+    t0 = time.perf_counter()
+    b.step(2000)
+    b.sync()
+    dt = time.perf_counter() - t0
+    out["events_off"] = {"turns": 2000, "seconds": dt, "gcups": N * N * 2000 / dt / 1e9}
+
+    turns, flips_total = 200, 0
+    last_tick = time.perf_counter()
+    ticks = 0
+    t0 = time.perf_counter()
+    for _ in range(turns):
+        b.step(1, want_flips=True)
+        flips_total += len(b.flips())
+        if time.perf_counter() - last_tick >= 2.0:
+            b.alive_count()
+            ticks += 1
+            last_tick = time.perf_counter()
+    dt = time.perf_counter() - t0
+    out["events_on"] = {"turns": turns, "seconds": dt, "turns_per_s": turns / dt, "flips": flips_total,
+                        "flips_per_s": flips_total / dt, "gcups": N * N * turns / dt / 1e9, "ticks": ticks}
+
+    t0 = time.perf_counter()
+    snap = b.snapshot_bytes()
+    with tempfile.NamedTemporaryFile(suffix=".pgm") as f:
+        f.write(pgm_bytes(snap))
+        f.flush()
+    out["snapshot_s_ms"] = (time.perf_counter() - t0) * 1e3
+
+print(json.dumps(out))

@@ -14,12 +14,13 @@ import sys
 src = sys.argv[1]
 dst = sys.argv[2]
 out = json.load(open(dst)) if os.path.exists(dst) else {}
-for size in (16384, 65536, 262144):
+KERNELS = ("gol_persist_kernel", "gol_tb_kernel")
+for size, kname in [(s, k) for s in (16384, 65536, 262144) for k in KERNELS]:
     vals = {}
     durs = []
     for path in glob.glob(os.path.join(src, f"pmc_{size}_*", "*counter_collection.csv")):
         for row in csv.DictReader(open(path)):
-            if "gol_tb_kernel<16>" not in row["Kernel_Name"]:
+            if kname + "<" not in row["Kernel_Name"]:
                 continue
             vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
             durs.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
@@ -29,8 +30,9 @@ for size in (16384, 65536, 262144):
     w = statistics.mean(vals["WRITE_SIZE"]) * 1024
     rec = {"fetch_size_bytes_raw": f, "fetch_bytes_corrected": 2 * f, "write_bytes": w,
            "hbm_bytes_per_launch": 2 * f + w, "board_bytes": size * size / 8, "launches": len(vals["FETCH_SIZE"]),
-           "note": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes, gol_tb_kernel<16>, "
-                   "scripts/prof_step.py; Infinity-Cache hits are counted (board <= 256 MiB is cache-resident)"}
+           "kernel": kname,
+           "note": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes, scripts/prof_step.py; "
+                   "Infinity-Cache hits are counted (a board <= 256 MiB is cache-resident)"}
     if "SQ_INSTS_VALU" in vals:
         dur = statistics.median(durs)
         g = statistics.mean(vals["GRBM_GUI_ACTIVE"])
@@ -41,6 +43,6 @@ for size in (16384, 65536, 262144):
             "valu_active_frac": statistics.mean(vals["SQ_ACTIVE_INST_VALU"]) / max(1.0, statistics.mean(vals["SQ_WAVE_CYCLES"])),
             "clock_ghz_est": g / 8 / dur / 1e9 if dur > 0 else None,
         })
-    out[f"{size}x16"] = rec
+    out[f"{size}:{kname}"] = rec
 json.dump(out, open(dst, "w"), indent=1)
 print(json.dumps(out, indent=1))

@@ -12,15 +12,19 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--size", type=int, default=16384)
 ap.add_argument("--depth", type=int, default=16)
 ap.add_argument("--launches", type=int, default=20)
+ap.add_argument("--persistent", type=int, default=1)
 a = ap.parse_args()
 with golhip.Board(a.size, a.size, timing=True) as b:
     b.set_tb_depth(a.depth)
+    b.set_option("persistent", a.persistent)
     b.fill_random(0x5EED0001 if a.size == 16384 else 0x5EED0002)
     b.step(2 * a.depth)
     b.sync()
     b.perf_reset()
-    b.step(a.launches * a.depth)
+    # persistent: `launches` separate step calls of 4 super-steps each;
+    # per-launch: `launches` launches of `depth` turns
+    for _ in range(a.launches):
+        b.step(4 * a.depth if a.persistent else a.depth)
     b.sync()
     p = b.perf()
-    print({"size": a.size, "depth": a.depth, "launches": p["step_launches"],
-           "avg_launch_ms": p["step_kernel_ms"] / max(1, p["step_launches"]), "rows_per_wave": p["rows_per_wave"]})
+    print(p)

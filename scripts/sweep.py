@@ -41,10 +41,11 @@ for N in map(int, a.sizes.split(",")):
                     b.sync()
                     dt = time.perf_counter() - t0
                     p = b.perf()
-                    kern = p["step_kernel_ms"] / p["step_launches"]
+                    kms = p["step_kernel_ms"] + p["persist_kernel_ms"]
+                    kern = kms / max(1, p["step_launches"] + p["persist_launches"])
                     rec = dict(N=N, depth=d, rpw=s, variant=v, rpw_used=p["rows_per_wave"],
                                wall_gcups=N * N * a.turns / dt / 1e9,
-                               kernel_gcups=N * N * d / (kern * 1e-3) / 1e9, launch_ms=kern)
+                               kernel_gcups=N * N * a.turns / (kms * 1e-3) / 1e9, launch_ms=kern)
                     if rec["wall_gcups"] > best.get(v, {"wall_gcups": 0})["wall_gcups"]:
                         best[v] = rec
             for v in variants:
