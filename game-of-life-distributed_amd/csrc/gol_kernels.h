@@ -11,7 +11,7 @@ namespace golk {
 // exchange (strip mode) and unused in torus mode.
 constexpr int kHalo = 32;        // == GOLHIP_MAX_TB_DEPTH
 constexpr int kWave = 64;
-constexpr int kTileValid = 62;   // words per wavefront tile that are stored (lanes 1..62)
+constexpr int kTileValid = 62;   // lanes per wavefront tile that are stored (lanes 1..62)
 
 // How a step kernel finds input row i (logical, may be outside 0..rows-1).
 //   torus mode : phys = base + mod(i, wrap)                 (whole board on one device)
@@ -35,16 +35,19 @@ struct StepArgs {
     unsigned long long *alive;  // nullable: += popcount of the output
 };
 
-// Bit-sliced temporal-blocked step: `depth` in {1,2,4,8,16,32}; requires W % 32 == 0.
-// fill_skip: skip the pipeline-fill stage-rows that only see padding.
-hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s, bool fill_skip = true);
+// Bit-sliced temporal-blocked step: `depth` in {1,2,4,8,16,32}; requires W % 32 == 0
+// (wpl = 2: W % 64 == 0 and depth <= 16).  fill_skip: skip the pipeline-fill
+// stage-rows that only see padding.  wpl: words per lane (1 or 2).
+hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s, bool fill_skip, int wpl);
+int max_depth_for(int wpl);
+int tb_tiles(int Ww, int wpl);
 // One turn for any width (W % 32 != 0 boards such as 16x16).
 hipError_t launch_step_generic(const StepArgs &a, hipStream_t s);
-int tb_waves(const StepArgs &a, int depth);
+int tb_waves(const StepArgs &a, int wpl);
 // Resident 256-thread blocks per CU of the depth-`depth` step kernel.
-int tb_blocks_per_cu(int depth);
+int tb_blocks_per_cu(int depth, int wpl);
 // Rows per wavefront minimising (rounds of waves) x (rows streamed per wave).
-int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_skip);
+int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_skip, int wpl);
 
 // Persistent multi-super-step step kernel (torus mode); see gol_kernels.hip K1p.
 struct PersistArgs {
@@ -60,11 +63,11 @@ struct PersistArgs {
     unsigned *error;          // set on a spin timeout
     long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
 };
-int persist_waves_for(int depth);
-int persist_blocks_per_cu(int depth);
+int persist_waves_for(int depth, int wpl);
+int persist_blocks_per_cu(int depth, int wpl);
 // Workgroup shape / band height for `cus` resident workgroups; false if none fits.
-bool plan_persist(int Ww, int rows, int depth, int cus, PersistArgs *p);
-hipError_t launch_persist(const PersistArgs &p, int depth, hipStream_t s);
+bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, PersistArgs *p);
+hipError_t launch_persist(const PersistArgs &p, int depth, int wpl, hipStream_t s);
 
 hipError_t launch_pack(const uint8_t *bytes, uint32_t *words, int W, int Ww, int rows, hipStream_t s);
 hipError_t launch_unpack(const uint32_t *words, uint8_t *bytes, int W, int Ww, int rows, hipStream_t s);

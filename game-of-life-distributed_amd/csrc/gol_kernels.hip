@@ -76,42 +76,58 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 // ---------------------------------------------------------------------------
 // K1: temporal-blocked bit-sliced step.
 //
-// One wavefront = one tile of 64 consecutive words of a row band (lane j
-// holds word t0 + j - 1); it streams the band's rows top to bottom through a
-// DEPTH-stage register pipeline.  Stage t turns generation t-1 row i into
-// generation t row i-1, so after 2*DEPTH rows of fill every input row yields
-// one row DEPTH generations ahead.  Horizontal neighbours come from the
-// adjacent lanes (DPP); lanes 0 and 63 are the halo: their error front moves
-// one cell per turn, so with DEPTH <= 32 lanes 1..62 are exact and stored.
-// Vertically a wave reads DEPTH extra rows above and below its band.
-// Per stage and row: 2 DPP + 2 alignbit + 2 bitop3 (3-cell row sum, shared by
-// the three output rows that use it) + 8 bitop3 (column sum + rule) = 14 VALU
-// per 32 cells.  HBM traffic per launch ~ 2 bits per cell (read + write) for
-// DEPTH turns.
+// One wavefront = one tile of 64 lanes x WPL consecutive words of a row band
+// (lane j holds words t0 + WPL*(j-1) ...); it streams the band's rows top to
+// bottom through a D-stage register pipeline.  Stage t turns generation t-1
+// row i into generation t row i-1, so after 2D rows of fill every input row
+// yields one row D generations ahead.  Horizontal neighbours: the lane's own
+// words plus one edge word from each adjacent lane (DPP); lanes 0 and 63 are
+// the halo: their error front moves one cell per turn, so with D <= 32 lanes
+// 1..62 are exact and stored.  Vertically a wave reads D extra rows above and
+// below its band.
+// Per stage, row and word: 2/WPL DPP + 2 alignbit + 2 bitop3 (3-cell row sum,
+// shared by the three output rows that use it) + 8 bitop3 (column sum + rule).
+// DPP and alignbit issue at half rate on gfx950, bitop3 at full rate, so
+// WPL = 2 cuts a word-turn from ~18 to ~16 full-rate slots.
+// HBM traffic per launch ~ 2 bits per cell (read + write) for D turns.
 // ---------------------------------------------------------------------------
+template <int WPL>
+struct Lanes {
+    uint32_t w[WPL];
+};
+
 // One stage (turn t) for the row entering with role R (R = input index % 3).
-template <int D, int R>
-__device__ __forceinline__ void stage(int t, uint32_t &x, uint32_t (&h0)[3][D], uint32_t (&h1)[3][D],
-                                      uint32_t (&cc)[3][D]) {
+template <int D, int R, int WPL>
+__device__ __forceinline__ void stage(int t, Lanes<WPL> &x, uint32_t (&h0)[3][D][WPL], uint32_t (&h1)[3][D][WPL],
+                                      uint32_t (&cc)[3][D][WPL]) {
     constexpr int N = R;            // slot of the row entering now
     constexpr int C = (R + 2) % 3;  // previous row (the one we emit)
     constexpr int P = (R + 1) % 3;  // the row before it
-    const uint32_t l = from_left_lane(x);
-    const uint32_t r = from_right_lane(x);
-    const uint32_t west = __builtin_amdgcn_alignbit(x, l, 31);  // bit k = cell k-1
-    const uint32_t east = __builtin_amdgcn_alignbit(r, x, 1);   // bit k = cell k+1
-    h0[N][t] = bop<kXor3>(west, x, east);
-    h1[N][t] = bop<kMaj>(west, x, east);
-    const uint32_t u0 = bop<kXor3>(h0[P][t], h0[C][t], h0[N][t]);
-    const uint32_t u1 = bop<kMaj>(h0[P][t], h0[C][t], h0[N][t]);
-    const uint32_t v0 = bop<kXor3>(h1[P][t], h1[C][t], h1[N][t]);
-    const uint32_t v1 = bop<kMaj>(h1[P][t], h1[C][t], h1[N][t]);
-    const uint32_t t1 = bop<kT1>(u1, v0, v1);
-    const uint32_t t2 = bop<kT2>(u1, v0, v1);
-    const uint32_t born = bop<kBorn>(cc[C][t], t2, u0);
-    const uint32_t nx = bop<kNext>(u0, t1, born);
-    cc[N][t] = x;
-    x = nx;
+    const uint32_t l = from_left_lane(x.w[WPL - 1]);  // left lane's last word
+    const uint32_t r = from_right_lane(x.w[0]);       // right lane's first word
+    uint32_t nx[WPL];
+#pragma unroll
+    for (int k = 0; k < WPL; ++k) {
+        const uint32_t lo = k == 0 ? l : x.w[k - 1];
+        const uint32_t hi = k == WPL - 1 ? r : x.w[k + 1];
+        const uint32_t west = __builtin_amdgcn_alignbit(x.w[k], lo, 31);  // bit b = cell b-1
+        const uint32_t east = __builtin_amdgcn_alignbit(hi, x.w[k], 1);   // bit b = cell b+1
+        h0[N][t][k] = bop<kXor3>(west, x.w[k], east);
+        h1[N][t][k] = bop<kMaj>(west, x.w[k], east);
+        const uint32_t u0 = bop<kXor3>(h0[P][t][k], h0[C][t][k], h0[N][t][k]);
+        const uint32_t u1 = bop<kMaj>(h0[P][t][k], h0[C][t][k], h0[N][t][k]);
+        const uint32_t v0 = bop<kXor3>(h1[P][t][k], h1[C][t][k], h1[N][t][k]);
+        const uint32_t v1 = bop<kMaj>(h1[P][t][k], h1[C][t][k], h1[N][t][k]);
+        const uint32_t t1 = bop<kT1>(u1, v0, v1);
+        const uint32_t t2 = bop<kT2>(u1, v0, v1);
+        const uint32_t born = bop<kBorn>(cc[C][t][k], t2, u0);
+        nx[k] = bop<kNext>(u0, t1, born);
+    }
+#pragma unroll
+    for (int k = 0; k < WPL; ++k) {
+        cc[N][t][k] = x.w[k];
+        x.w[k] = nx[k];
+    }
 }
 
 // A group of 3 consecutive input rows through the first A of the D stages.
@@ -120,27 +136,36 @@ __device__ __forceinline__ void stage(int t, uint32_t &x, uint32_t (&h0)[3][D], 
 // interleave, which hides the VALU->DPP hazard of each stage's serial chain.
 // A < D is used while the pipeline fills: stage t only sees real rows from
 // input index 2t on, so later stages would only compute garbage.
-template <int D, int A>
-__device__ __forceinline__ void push_group(uint32_t &x0, uint32_t &x1, uint32_t &x2, uint32_t (&h0)[3][D],
-                                           uint32_t (&h1)[3][D], uint32_t (&cc)[3][D]) {
+template <int D, int A, int WPL>
+__device__ __forceinline__ void push_group(Lanes<WPL> &x0, Lanes<WPL> &x1, Lanes<WPL> &x2,
+                                           uint32_t (&h0)[3][D][WPL], uint32_t (&h1)[3][D][WPL],
+                                           uint32_t (&cc)[3][D][WPL]) {
 #pragma unroll
     for (int s = 0; s < A + 2; ++s) {
-        if (s < A) stage<D, 0>(s, x0, h0, h1, cc);
-        if (s >= 1 && s - 1 < A) stage<D, 1>(s - 1, x1, h0, h1, cc);
-        if (s >= 2 && s - 2 < A) stage<D, 2>(s - 2, x2, h0, h1, cc);
+        if (s < A) stage<D, 0, WPL>(s, x0, h0, h1, cc);
+        if (s >= 1 && s - 1 < A) stage<D, 1, WPL>(s - 1, x1, h0, h1, cc);
+        if (s >= 2 && s - 2 < A) stage<D, 2, WPL>(s - 2, x2, h0, h1, cc);
     }
+}
+
+template <int WPL>
+__device__ __forceinline__ Lanes<WPL> vmov(const Lanes<WPL> &v) {
+    Lanes<WPL> r;
+#pragma unroll
+    for (int k = 0; k < WPL; ++k) asm volatile("v_mov_b32 %0, %1" : "=v"(r.w[k]) : "v"(v.w[k]));
+    return r;
 }
 
 // One wavefront streams output rows [r0, r0 + rows_here) of the tile whose
 // first stored word is t0, D turns ahead; returns the popcount of its stored
 // output words.  Shared by the per-launch and the persistent kernel.
-template <int D, bool SKIP>
+template <int D, bool SKIP, int WPL>
 __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int rows_here, int t0) {
     const int lane = threadIdx.x & 63;
     const int Ww = a.Ww;
-    int col = (t0 + lane - 1) % Ww;
+    int col = (t0 + WPL * (lane - 1)) % Ww;  // WPL = 2 needs Ww even: a pair never wraps
     if (col < 0) col += Ww;
-    const bool keep = lane >= 1 && lane <= kTileValid && (t0 + lane - 1) < Ww;
+    const bool keep = lane >= 1 && lane <= kTileValid && (t0 + WPL * (lane - 1)) < Ww;
 
     // input row cursor (wave-uniform)
     int r = r0 - D + a.in.off;
@@ -150,9 +175,16 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
         if (r < 0) r += a.in.wrap;
     }
     const uint32_t *__restrict__ src = a.src + col;
-    auto load_next = [&]() -> uint32_t {
+    auto load_next = [&]() -> Lanes<WPL> {
         const int pr = a.in.base + min(r, a.in.rmax);
-        const uint32_t v = src[(size_t)pr * Ww];
+        Lanes<WPL> v;
+        if constexpr (WPL == 1) {
+            v.w[0] = src[(size_t)pr * Ww];
+        } else {
+            const uint2 q = *reinterpret_cast<const uint2 *>(src + (size_t)pr * Ww);
+            v.w[0] = q.x;
+            v.w[1] = q.y;
+        }
         r = (r + 1 == wrap) ? 0 : r + 1;
         return v;
     };
@@ -164,31 +196,35 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
     uint32_t *const dst_row0 = a.dst + (size_t)(a.dst_base + r0) * Ww + col;
     uint32_t *const dummy = a.dst + col;
     uint32_t cnt = 0;
-    auto emit = [&](uint32_t y, int out_idx) {
+    auto emit = [&](const Lanes<WPL> &y, int out_idx) {
         const bool ok = keep && (unsigned)out_idx < (unsigned)rows_here;
         uint32_t *p = ok ? dst_row0 + (ptrdiff_t)out_idx * Ww : dummy;
-        *p = y;
-        cnt += ok ? (uint32_t)__builtin_popcount(y) : 0u;
+        uint32_t pc = 0;
+        if constexpr (WPL == 1) {
+            *p = y.w[0];
+            pc = __builtin_popcount(y.w[0]);
+        } else {
+            *reinterpret_cast<uint2 *>(p) = make_uint2(y.w[0], y.w[1]);
+            pc = __builtin_popcount(y.w[0]) + __builtin_popcount(y.w[1]);
+        }
+        cnt += ok ? pc : 0u;
     };
 
-    uint32_t h0[3][D], h1[3][D], cc[3][D];
+    uint32_t h0[3][D][WPL], h1[3][D][WPL], cc[3][D][WPL];
 #pragma unroll
     for (int s = 0; s < 3; ++s)
 #pragma unroll
-        for (int t = 0; t < D; ++t) h0[s][t] = h1[s][t] = cc[s][t] = 0u;
+        for (int t = 0; t < D; ++t)
+#pragma unroll
+            for (int k = 0; k < WPL; ++k) h0[s][t][k] = h1[s][t][k] = cc[s][t][k] = 0u;
 
     // Prefetch: the next group's rows are issued at the top of the body and
-    // moved into place at the bottom, so their vmcnt wait lands a full group
-    // of compute after issue (the sched_barrier stops the scheduler from
-    // sinking the loads).
-    auto vmov = [](uint32_t v) {
-        uint32_t r;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
-        return r;
-    };
-    // the first group also goes through vmov, so no load is pending on the
-    // loop's entry edge either (else the header waits for it every iteration)
-    uint32_t x0 = vmov(load_next()), x1 = vmov(load_next()), x2 = vmov(load_next());
+    // moved into place at the bottom (an inline-asm v_mov: a plain copy lets
+    // the register allocator merge the registers and hoist the copy, and its
+    // vmcnt wait, to the loop top), so the wait lands a full group of compute
+    // after issue.  The first group also goes through vmov, so no load is
+    // pending on the loop's entry edge either.
+    Lanes<WPL> x0 = vmov(load_next()), x1 = vmov(load_next()), x2 = vmov(load_next());
     int oi = -2 * D;  // output row of the group's first input row (input index oi + 2D)
     // Pipeline fill in three steps: while the group's last input index
     // i = oi + 2D + 2 satisfies i/2 + 1 <= A, stages >= A cannot see real rows
@@ -199,10 +235,10 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
         constexpr int A = decltype(a_tag)::value;
         if constexpr (SKIP && A >= 1 && A < D) {
             for (; (oi + 2 * D + 2) / 2 + 1 <= A; oi += 3) {
-                const uint32_t n0 = load_next(), n1 = load_next(), n2 = load_next();
+                const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
                 __builtin_amdgcn_sched_barrier(0);
-                uint32_t y0 = x0, y1 = x1, y2 = x2;
-                push_group<D, A>(y0, y1, y2, h0, h1, cc);
+                Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
+                push_group<D, A, WPL>(y0, y1, y2, h0, h1, cc);
                 __builtin_amdgcn_sched_barrier(0);
                 x0 = vmov(n0);
                 x1 = vmov(n1);
@@ -214,16 +250,14 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
     fill(std::integral_constant<int, D / 2>());
     fill(std::integral_constant<int, 3 * D / 4>());
     for (; oi < rows_here; oi += 3) {
-        const uint32_t n0 = load_next(), n1 = load_next(), n2 = load_next();
+        const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
         __builtin_amdgcn_sched_barrier(0);
-        uint32_t y0 = x0, y1 = x1, y2 = x2;
-        push_group<D, D>(y0, y1, y2, h0, h1, cc);
+        Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
+        push_group<D, D, WPL>(y0, y1, y2, h0, h1, cc);
         emit(y0, oi);
         emit(y1, oi + 1);
         emit(y2, oi + 2);
         __builtin_amdgcn_sched_barrier(0);
-        // a real v_mov (not a coalescable copy): the register allocator would
-        // otherwise merge x and n and hoist the copy (and its wait) to the top
         x0 = vmov(n0);
         x1 = vmov(n1);
         x2 = vmov(n2);
@@ -231,16 +265,18 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
     return cnt;
 }
 
-template <int D, bool SKIP>
+__host__ __device__ constexpr int tile_words(int wpl) { return kTileValid * wpl; }
+
+template <int D, bool SKIP, int WPL>
 __global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-    const int tiles_x = (a.Ww + kTileValid - 1) / kTileValid;
+    const int tiles_x = (a.Ww + tile_words(WPL) - 1) / tile_words(WPL);
     const int S = a.rows_per_wave;
     const int strip = wave / tiles_x;
     const int tile = wave - strip * tiles_x;
     const int r0 = strip * S;
     if (r0 >= a.rows_out) return;  // wave-uniform
-    const uint32_t cnt = stream_band<D, SKIP>(a, r0, min(S, a.rows_out - r0), tile * kTileValid);
+    const uint32_t cnt = stream_band<D, SKIP, WPL>(a, r0, min(S, a.rows_out - r0), tile * tile_words(WPL));
     if (a.alive) {
         const uint32_t tot = wave_sum_u32(cnt);
         if ((threadIdx.x & 63) == 0) atomicAdd(a.alive, (unsigned long long)tot);
@@ -263,12 +299,10 @@ __global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
 // barrier -> loads.  Every spin is bounded: on timeout the kernel sets
 // *error and all workgroups drain out.
 // ---------------------------------------------------------------------------
-template <int D>
-constexpr int persist_waves() { return D <= 16 ? 16 : 8; }
+__host__ __device__ constexpr int persist_waves(int depth, int wpl) { return depth * wpl <= 16 ? 16 : 8; }
 
-template <int D>
-__global__ __launch_bounds__(persist_waves<D>() * 64) void gol_persist_kernel(PersistArgs p) {
-    constexpr int NW = persist_waves<D>();
+template <int D, int WPL>
+__global__ __launch_bounds__(persist_waves(D, WPL) * 64) void gol_persist_kernel(PersistArgs p) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int b = blockIdx.x;
@@ -277,7 +311,6 @@ __global__ __launch_bounds__(persist_waves<D>() * 64) void gol_persist_kernel(Pe
     const int strip = wy * p.wg_sy + w / p.wg_tx;
     const int r0 = strip * p.S;
     const int rows_here = (tile < p.tiles_x && r0 < p.base.rows_out) ? min(p.S, p.base.rows_out - r0) : 0;
-    (void)NW;
 
     // neighbour workgroup polled by lane k < 9
     int nb = b;
@@ -318,7 +351,7 @@ __global__ __launch_bounds__(persist_waves<D>() * 64) void gol_persist_kernel(Pe
         const bool odd = ((p.first + j) & 1) != 0;
         a.src = odd ? p.buf1 : p.buf0;
         a.dst = odd ? p.buf0 : p.buf1;
-        cnt = rows_here > 0 ? stream_band<D, true>(a, r0, rows_here, tile * kTileValid) : 0u;
+        cnt = rows_here > 0 ? stream_band<D, true, WPL>(a, r0, rows_here, tile * tile_words(WPL)) : 0u;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -333,24 +366,91 @@ __global__ __launch_bounds__(persist_waves<D>() * 64) void gol_persist_kernel(Pe
     }
 }
 
-int persist_waves_for(int depth) { return depth <= 16 ? 16 : 8; }
+// ---- host-side dispatch over (depth, fill skip, words per lane) ----------
+// WPL = 2 is instantiated up to depth 16 (depth 32 would exceed 256 VGPRs).
+template <typename F>
+static hipError_t dispatch(int depth, bool skip, int wpl, F &&f) {
+#define GOL_CASE(D, SK, WP) \
+    if (depth == D && skip == SK && wpl == WP) return f(gol_tb_kernel<D, SK, WP>);
+    GOL_CASE(1, true, 1) GOL_CASE(2, true, 1) GOL_CASE(4, true, 1) GOL_CASE(8, true, 1) GOL_CASE(16, true, 1)
+    GOL_CASE(32, true, 1) GOL_CASE(1, false, 1) GOL_CASE(2, false, 1) GOL_CASE(4, false, 1) GOL_CASE(8, false, 1)
+    GOL_CASE(16, false, 1) GOL_CASE(32, false, 1)
+    GOL_CASE(1, true, 2) GOL_CASE(2, true, 2) GOL_CASE(4, true, 2) GOL_CASE(8, true, 2) GOL_CASE(16, true, 2)
+    GOL_CASE(1, false, 2) GOL_CASE(2, false, 2) GOL_CASE(4, false, 2) GOL_CASE(8, false, 2) GOL_CASE(16, false, 2)
+#undef GOL_CASE
+    return hipErrorInvalidValue;
+}
 
-int persist_blocks_per_cu(int depth) {
+int max_depth_for(int wpl) { return wpl == 2 ? 16 : 32; }
+
+int tb_tiles(int Ww, int wpl) { return (Ww + tile_words(wpl) - 1) / tile_words(wpl); }
+
+int tb_waves(const StepArgs &a, int wpl) {
+    const int strips = (a.rows_out + a.rows_per_wave - 1) / a.rows_per_wave;
+    return tb_tiles(a.Ww, wpl) * strips;
+}
+
+hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s, bool fill_skip, int wpl) {
+    const int waves = tb_waves(a, wpl);
+    const dim3 grid((waves + 3) / 4), block(256);
+    return dispatch(depth, fill_skip, wpl, [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, block, 0, s, a);
+        return hipGetLastError();
+    });
+}
+
+int tb_blocks_per_cu(int depth, int wpl) {
     int b = 0;
-    hipError_t e = hipErrorInvalidValue;
-    switch (depth) {
-        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_persist_kernel<4>, 64 * persist_waves<4>(), 0); break;
-        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_persist_kernel<8>, 64 * persist_waves<8>(), 0); break;
-        case 16: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_persist_kernel<16>, 64 * persist_waves<16>(), 0); break;
-        case 32: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_persist_kernel<32>, 64 * persist_waves<32>(), 0); break;
-        default: break;
+    hipError_t e = dispatch(depth, true, wpl, [&](auto kern) {
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 256, 0);
+    });
+    return (e == hipSuccess && b > 0) ? b : 1;
+}
+
+int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_skip, int wpl) {
+    // Each wave streams S + 2*depth rows (~S + 1.25*depth row-equivalents of
+    // work when the fill skips dead stages); waves run in ceil(waves / slots)
+    // rounds.  Minimise rounds * work (fill overhead vs tail).
+    const int tiles_x = tb_tiles(Ww, wpl);
+    int best_s = rows;
+    double best = 1e300;
+    for (int strips = 1; strips <= rows; ++strips) {
+        const int S = (rows + strips - 1) / strips;
+        const long long waves = (long long)tiles_x * ((rows + S - 1) / S);
+        const long long rounds = (waves + wave_slots - 1) / wave_slots;
+        const double cost = (double)rounds * (S + (fill_skip ? 2 * depth - 0.75 * depth : 2 * depth));
+        if (cost < best * 0.999) {
+            best = cost;
+            best_s = S;
+        }
+        if (S <= 2) break;
     }
+    return best_s;
+}
+
+template <typename F>
+static hipError_t dispatch_persist(int depth, int wpl, F &&f) {
+#define GOL_PCASE(D, WP) \
+    if (depth == D && wpl == WP) return f(gol_persist_kernel<D, WP>, persist_waves(D, WP));
+    GOL_PCASE(4, 1) GOL_PCASE(8, 1) GOL_PCASE(16, 1) GOL_PCASE(32, 1) GOL_PCASE(4, 2) GOL_PCASE(8, 2)
+    GOL_PCASE(16, 2)
+#undef GOL_PCASE
+    return hipErrorInvalidValue;
+}
+
+int persist_waves_for(int depth, int wpl) { return persist_waves(depth, wpl); }
+
+int persist_blocks_per_cu(int depth, int wpl) {
+    int b = 0;
+    hipError_t e = dispatch_persist(depth, wpl, [&](auto kern, int nw) {
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 64 * nw, 0);
+    });
     return e == hipSuccess ? b : 0;
 }
 
-bool plan_persist(int Ww, int rows, int depth, int cus, PersistArgs *p) {
-    const int NW = persist_waves_for(depth);
-    const int tiles_x = (Ww + kTileValid - 1) / kTileValid;
+bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, PersistArgs *p) {
+    const int NW = persist_waves(depth, wpl);
+    const int tiles_x = tb_tiles(Ww, wpl);
     bool found = false;
     long best_s = 0;
     for (int wg_tx = 1; wg_tx <= NW; wg_tx *= 2) {
@@ -379,79 +479,11 @@ bool plan_persist(int Ww, int rows, int depth, int cus, PersistArgs *p) {
     return found;
 }
 
-hipError_t launch_persist(const PersistArgs &p, int depth, hipStream_t s) {
-    const dim3 grid(p.cols * p.wg_y), block(64 * persist_waves_for(depth));
-    switch (depth) {
-        case 4: hipLaunchKernelGGL(gol_persist_kernel<4>, grid, block, 0, s, p); break;
-        case 8: hipLaunchKernelGGL(gol_persist_kernel<8>, grid, block, 0, s, p); break;
-        case 16: hipLaunchKernelGGL(gol_persist_kernel<16>, grid, block, 0, s, p); break;
-        case 32: hipLaunchKernelGGL(gol_persist_kernel<32>, grid, block, 0, s, p); break;
-        default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-int tb_blocks_per_cu(int depth) {
-    int b = 0;
-    hipError_t e = hipErrorInvalidValue;
-    switch (depth) {
-        case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<1, true>, 256, 0); break;
-        case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<2, true>, 256, 0); break;
-        case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<4, true>, 256, 0); break;
-        case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<8, true>, 256, 0); break;
-        case 16: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<16, true>, 256, 0); break;
-        case 32: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_tb_kernel<32, true>, 256, 0); break;
-        default: break;
-    }
-    return (e == hipSuccess && b > 0) ? b : 1;
-}
-
-int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_skip) {
-    // Each wave streams S + 2*depth rows (~S + 1.25*depth row-equivalents of
-    // work when the fill skips dead stages); waves run in ceil(waves / slots)
-    // rounds.  Minimise rounds * work (fill overhead vs tail).
-    const int tiles_x = (Ww + kTileValid - 1) / kTileValid;
-    int best_s = rows;
-    double best = 1e300;
-    for (int strips = 1; strips <= rows; ++strips) {
-        const int S = (rows + strips - 1) / strips;
-        const long long waves = (long long)tiles_x * ((rows + S - 1) / S);
-        const long long rounds = (waves + wave_slots - 1) / wave_slots;
-        const double cost = (double)rounds * (S + (fill_skip ? 2 * depth - 0.75 * depth : 2 * depth));
-        if (cost < best * 0.999) {
-            best = cost;
-            best_s = S;
-        }
-        if (S <= 2) break;
-    }
-    return best_s;
-}
-
-int tb_waves(const StepArgs &a, int depth) {
-    (void)depth;
-    const int tiles_x = (a.Ww + kTileValid - 1) / kTileValid;
-    const int strips = (a.rows_out + a.rows_per_wave - 1) / a.rows_per_wave;
-    return tiles_x * strips;
-}
-
-template <bool SKIP>
-static hipError_t launch_tb(const StepArgs &a, int depth, hipStream_t s) {
-    const int waves = tb_waves(a, depth);
-    const dim3 grid((waves + 3) / 4), block(256);
-    switch (depth) {
-        case 1: hipLaunchKernelGGL((gol_tb_kernel<1, SKIP>), grid, block, 0, s, a); break;
-        case 2: hipLaunchKernelGGL((gol_tb_kernel<2, SKIP>), grid, block, 0, s, a); break;
-        case 4: hipLaunchKernelGGL((gol_tb_kernel<4, SKIP>), grid, block, 0, s, a); break;
-        case 8: hipLaunchKernelGGL((gol_tb_kernel<8, SKIP>), grid, block, 0, s, a); break;
-        case 16: hipLaunchKernelGGL((gol_tb_kernel<16, SKIP>), grid, block, 0, s, a); break;
-        case 32: hipLaunchKernelGGL((gol_tb_kernel<32, SKIP>), grid, block, 0, s, a); break;
-        default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s, bool fill_skip) {
-    return fill_skip ? launch_tb<true>(a, depth, s) : launch_tb<false>(a, depth, s);
+hipError_t launch_persist(const PersistArgs &p, int depth, int wpl, hipStream_t s) {
+    return dispatch_persist(depth, wpl, [&](auto kern, int nw) {
+        hipLaunchKernelGGL(kern, dim3(p.cols * p.wg_y), dim3(64 * nw), 0, s, p);
+        return hipGetLastError();
+    });
 }
 
 // ---------------------------------------------------------------------------

@@ -85,6 +85,7 @@ struct golhip {
     int cu_count = 0;
     bool fill_skip = true;      // option "fill_skip"
     bool persistent = true;     // option "persistent": K1p for long torus runs
+    int wpl_opt = 0;            // option "wpl": words per lane (0 = auto, 1, 2)
     int persist_depth = 0;      // option "persist_depth" (0: tb_depth)
     unsigned *d_sync = nullptr; // persistent kernel: [0] error, [1..] progress per workgroup
     unsigned *h_err = nullptr;  // pinned copy of the error word
@@ -188,11 +189,21 @@ int largest_depth(int64_t want) {
     return 1;
 }
 
+// Words per lane of the step kernels: 2 halves the DPP work per word but
+// quantises tiles at 124 words instead of 62; auto picks the variant that
+// computes fewer words (ties -> 2).
+int wpl_for(golhip_t h) {
+    if (h->W % 64 != 0) return 1;
+    if (h->wpl_opt == 1 || h->wpl_opt == 2) return h->wpl_opt;
+    const long w1 = (long)golk::tb_tiles(h->Ww, 1) * 64, w2 = (long)golk::tb_tiles(h->Ww, 2) * 128;
+    return w2 <= w1 ? 2 : 1;
+}
+
 // How many turns the next launch fuses.  In halo mode the `depth` halo rows
 // must all come from one neighbour strip, so depth <= strip rows.
 int next_depth(golhip_t h, int64_t remaining, bool halo) {
     if (h->W % 32 != 0) return 1;  // generic kernel: one turn per launch
-    int64_t cap = std::min<int64_t>(h->tb_depth, remaining);
+    int64_t cap = std::min<int64_t>(std::min(h->tb_depth, golk::max_depth_for(wpl_for(h))), remaining);
     if (halo) cap = std::min<int64_t>(cap, h->rows);
     return largest_depth(cap);
 }
@@ -235,8 +246,9 @@ int rows_per_wave_for(golhip_t h, int depth) {
     if (h->rows_per_wave > 0) return h->rows_per_wave;
     int &c = h->auto_rpw[depth_index(depth)];
     if (c == 0) {
-        const int slots = h->cu_count * golk::tb_blocks_per_cu(depth) * 4;
-        c = golk::auto_rows_per_wave(h->Ww, h->rows, depth, std::max(slots, 1), h->fill_skip);
+        const int wpl = wpl_for(h);
+        const int slots = h->cu_count * golk::tb_blocks_per_cu(depth, wpl) * 4;
+        c = golk::auto_rows_per_wave(h->Ww, h->rows, depth, std::max(slots, 1), h->fill_skip, wpl);
     }
     return c;
 }
@@ -313,7 +325,7 @@ int launch_depth(golhip_t h, int depth, bool count, bool halo) {
     }
     hipError_t e;
     if (h->W % 32 == 0)
-        e = golk::launch_step_tb(a, depth, h->stream, h->fill_skip);
+        e = golk::launch_step_tb(a, depth, h->stream, h->fill_skip, wpl_for(h));
     else
         e = golk::launch_step_generic(a, h->stream);
     if (e != hipSuccess) return fail(GOLHIP_EHIP, "step launch: %s", hipGetErrorString(e));
@@ -357,13 +369,15 @@ int sync_stream(golhip_t h) {
 int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     *rc = GOLHIP_OK;
     if (!h->persistent || h->W % 32 != 0 || !h->torus()) return 0;
-    const int depth = largest_depth(h->persist_depth > 0 ? h->persist_depth : h->tb_depth);
+    const int wpl = wpl_for(h);
+    const int depth = largest_depth(std::min(h->persist_depth > 0 ? h->persist_depth : h->tb_depth,
+                                             golk::max_depth_for(wpl)));
     if (depth < 4) return 0;
     const int64_t J = left / depth;
     if (J < 2) return 0;
-    if (golk::persist_blocks_per_cu(depth) < 1) return 0;
+    if (golk::persist_blocks_per_cu(depth, wpl) < 1) return 0;
     golk::PersistArgs p{};
-    if (!golk::plan_persist(h->Ww, h->rows, depth, h->cu_count, &p)) return 0;
+    if (!golk::plan_persist(h->Ww, h->rows, depth, h->cu_count, wpl, &p)) return 0;
     if (!h->d_sync) {
         if (hipMalloc(&h->d_sync, (size_t)(h->cu_count + 2) * sizeof(unsigned)) != hipSuccess ||
             hipHostMalloc(&h->h_err, sizeof(unsigned), hipHostMallocDefault) != hipSuccess) {
@@ -392,7 +406,7 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
         e1 = take_event(h);
         if (e0 && e1) e = hipEventRecord(e0, h->stream);
     }
-    if (e == hipSuccess) e = golk::launch_persist(p, depth, h->stream);
+    if (e == hipSuccess) e = golk::launch_persist(p, depth, wpl, h->stream);
     if (e == hipSuccess && e1) {
         e = hipEventRecord(e1, h->stream);
         h->ev_pending.push_back({e0, e1, true});
@@ -574,6 +588,12 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     if (int rc = check(h)) return rc;
     if (!key) return fail(GOLHIP_EINVAL, "null option");
     std::lock_guard<std::mutex> g(h->mu);
+    if (!strcmp(key, "wpl")) {
+        if (value != 0 && value != 1 && value != 2) return fail(GOLHIP_EINVAL, "wpl %lld not in {0,1,2}", (long long)value);
+        h->wpl_opt = (int)value;
+        for (int &c : h->auto_rpw) c = 0;
+        return GOLHIP_OK;
+    }
     if (!strcmp(key, "persistent")) {
         h->persistent = value != 0;
         return GOLHIP_OK;

@@ -99,7 +99,10 @@ void *golhip_stream(golhip_t h);
 int golhip_set_tb_depth(golhip_t h, int32_t turns);
 int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
 /* Named engine options (kernel variants for A/B measurement); results never
- * depend on them.  "fill_skip" (default 1): skip pipeline-fill stage-rows. */
+ * depend on them.  "fill_skip" (default 1): skip pipeline-fill stage-rows;
+ * "wpl" (default 0 = auto): words per lane, 1 or 2; "persistent" (default 1):
+ * resident multi-super-step kernel for long runs on a whole torus;
+ * "persist_depth" (default 0 = tb_depth): turns per super-step. */
 int golhip_set_option(golhip_t h, const char *key, int64_t value);
 
 /* ---- multi-GPU -------------------------------------------------------- */

@@ -159,19 +159,21 @@ def test_flips_after_multi_turn_step(fixtures):
 @pytest.mark.parametrize("depth", DEPTHS)
 @pytest.mark.parametrize("rpw", [0, 1, 2, 5, 37, 512])
 @pytest.mark.parametrize("fill_skip", [0, 1])
-def test_depth_and_strip_height_invariance(fixtures, depth, rpw, fill_skip):
+@pytest.mark.parametrize("wpl", [1, 2])
+def test_depth_and_strip_height_invariance(fixtures, depth, rpw, fill_skip, wpl):
     board = img(fixtures, 256)
-    assert np.array_equal(run_gpu(board, 70, depth, rpw, fill_skip=fill_skip), run_np(board, 70))
+    assert np.array_equal(run_gpu(board, 70, depth, rpw, fill_skip=fill_skip, wpl=wpl), run_np(board, 70))
 
 
 @pytest.mark.parametrize("W,H", [(32, 1), (32, 3), (64, 2), (96, 7), (2016, 9), (1984, 33), (4000 - 4000 % 32, 40),
-                                 (8192, 5), (320, 1000), (6272, 70)])
+                                 (8192, 5), (320, 1000), (6272, 70), (7936, 20), (8064, 12), (128, 64)])
 @pytest.mark.parametrize("depth", [1, 8, 32])
-def test_random_shapes(W, H, depth):
-    """Widths that are 1..many tiles (62 stored words/tile), heights below the depth."""
+@pytest.mark.parametrize("wpl", [1, 2])
+def test_random_shapes(W, H, depth, wpl):
+    """Widths that are 1..many tiles (62 x wpl stored words/tile), heights below the depth."""
     rng = np.random.default_rng(W * 7 + H)
     board = np.where(rng.random((H, W)) < 0.3, 255, 0).astype(np.uint8)
-    assert np.array_equal(run_gpu(board, 45, depth, 16), run_np(board, 45))
+    assert np.array_equal(run_gpu(board, 45, depth, 16, wpl=wpl), run_np(board, 45))
 
 
 @pytest.mark.parametrize("W,H", [(16, 16), (1, 1), (3, 5), (17, 9), (48, 20), (100, 37), (33, 64)])
@@ -296,13 +298,15 @@ def test_full_size_fill_sample_rows(coracle):
 
 # ---------------------------------------------------------------- persistent kernel (K1p)
 @pytest.mark.parametrize("N,depth", [(1024, 4), (2048, 8), (2048, 16), (4096, 32), (3968, 16)])
-def test_persistent_matches_oracle(coracle, N, depth):
+@pytest.mark.parametrize("wpl", [1, 2])
+def test_persistent_matches_oracle(coracle, N, depth, wpl):
     """Resident multi-super-step kernel vs the C oracle (and vs the per-launch path)."""
     board = coracle.fill_random(N, N // 2, 0x5EED0007)
     want = coracle.run(board, 3 * depth + 5)
     outs = {}
     for persistent in (1, 0):
         with golhip.Board(N, N // 2) as b:
+            b.set_option("wpl", wpl)
             b.set_option("persistent", persistent)
             b.set_tb_depth(depth)
             b.load_bytes(board)
