@@ -59,14 +59,15 @@ struct PersistArgs {
     int wg_tx, wg_sy;         // workgroup block of (tiles, strips)
     int cols, wg_y;           // workgroup grid
     int tiles_x;
+    int nw;                   // waves per workgroup
     unsigned *progress;       // per workgroup, zeroed before launch
     unsigned *error;          // set on a spin timeout
     long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
 };
 int persist_waves_for(int depth, int wpl);
-int persist_blocks_per_cu(int depth, int wpl);
+int persist_blocks_per_cu(int depth, int wpl, int nw);
 // Workgroup shape / band height for `cus` resident workgroups; false if none fits.
-bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, PersistArgs *p);
+bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, int nw, PersistArgs *p);
 hipError_t launch_persist(const PersistArgs &p, int depth, int wpl, hipStream_t s);
 
 hipError_t launch_pack(const uint8_t *bytes, uint32_t *words, int W, int Ww, int rows, hipStream_t s);

@@ -301,8 +301,8 @@ __global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int persist_waves(int depth, int wpl) { return depth * wpl <= 16 ? 16 : 8; }
 
-template <int D, int WPL>
-__global__ __launch_bounds__(persist_waves(D, WPL) * 64) void gol_persist_kernel(PersistArgs p) {
+template <int D, int WPL, int NW>
+__global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int b = blockIdx.x;
@@ -428,28 +428,33 @@ int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_sk
     return best_s;
 }
 
+// nw = waves per workgroup (one workgroup per CU): 4, 8 or 16; 0 = default.
 template <typename F>
-static hipError_t dispatch_persist(int depth, int wpl, F &&f) {
-#define GOL_PCASE(D, WP) \
-    if (depth == D && wpl == WP) return f(gol_persist_kernel<D, WP>, persist_waves(D, WP));
-    GOL_PCASE(4, 1) GOL_PCASE(8, 1) GOL_PCASE(16, 1) GOL_PCASE(32, 1) GOL_PCASE(4, 2) GOL_PCASE(8, 2)
-    GOL_PCASE(16, 2)
+static hipError_t dispatch_persist(int depth, int wpl, int nw, F &&f) {
+    if (nw == 0) nw = persist_waves(depth, wpl);
+#define GOL_PCASE(D, WP, NW) \
+    if (depth == D && wpl == WP && nw == NW) return f(gol_persist_kernel<D, WP, NW>, NW);
+    GOL_PCASE(4, 1, 16) GOL_PCASE(8, 1, 16) GOL_PCASE(16, 1, 16) GOL_PCASE(32, 1, 8) GOL_PCASE(4, 2, 16)
+    GOL_PCASE(8, 2, 16) GOL_PCASE(16, 2, 8)
+    GOL_PCASE(4, 1, 4) GOL_PCASE(8, 1, 4) GOL_PCASE(16, 1, 4) GOL_PCASE(8, 1, 8) GOL_PCASE(16, 1, 8)
+    GOL_PCASE(4, 2, 4) GOL_PCASE(8, 2, 4) GOL_PCASE(16, 2, 4) GOL_PCASE(4, 2, 8) GOL_PCASE(8, 2, 8)
 #undef GOL_PCASE
     return hipErrorInvalidValue;
 }
 
 int persist_waves_for(int depth, int wpl) { return persist_waves(depth, wpl); }
 
-int persist_blocks_per_cu(int depth, int wpl) {
+int persist_blocks_per_cu(int depth, int wpl, int nw) {
     int b = 0;
-    hipError_t e = dispatch_persist(depth, wpl, [&](auto kern, int nw) {
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 64 * nw, 0);
+    hipError_t e = dispatch_persist(depth, wpl, nw, [&](auto kern, int n) {
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 64 * n, 0);
     });
     return e == hipSuccess ? b : 0;
 }
 
-bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, PersistArgs *p) {
-    const int NW = persist_waves(depth, wpl);
+bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, int nw, PersistArgs *p) {
+    const int NW = nw > 0 ? nw : persist_waves(depth, wpl);
+    p->nw = NW;
     const int tiles_x = tb_tiles(Ww, wpl);
     bool found = false;
     long best_s = 0;
@@ -480,7 +485,7 @@ bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, PersistArgs *p)
 }
 
 hipError_t launch_persist(const PersistArgs &p, int depth, int wpl, hipStream_t s) {
-    return dispatch_persist(depth, wpl, [&](auto kern, int nw) {
+    return dispatch_persist(depth, wpl, p.nw, [&](auto kern, int nw) {
         hipLaunchKernelGGL(kern, dim3(p.cols * p.wg_y), dim3(64 * nw), 0, s, p);
         return hipGetLastError();
     });

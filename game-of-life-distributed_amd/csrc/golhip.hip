@@ -87,6 +87,7 @@ struct golhip {
     bool persistent = true;     // option "persistent": K1p for long torus runs
     int wpl_opt = 0;            // option "wpl": words per lane (0 = auto, 1, 2)
     int persist_depth = 0;      // option "persist_depth" (0: tb_depth)
+    int persist_waves = 0;      // option "persist_waves": waves per workgroup (0: default)
     unsigned *d_sync = nullptr; // persistent kernel: [0] error, [1..] progress per workgroup
     unsigned *h_err = nullptr;  // pinned copy of the error word
     bool persist_pending = false;
@@ -375,9 +376,9 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     if (depth < 4) return 0;
     const int64_t J = left / depth;
     if (J < 2) return 0;
-    if (golk::persist_blocks_per_cu(depth, wpl) < 1) return 0;
+    if (golk::persist_blocks_per_cu(depth, wpl, h->persist_waves) < 1) return 0;
     golk::PersistArgs p{};
-    if (!golk::plan_persist(h->Ww, h->rows, depth, h->cu_count, wpl, &p)) return 0;
+    if (!golk::plan_persist(h->Ww, h->rows, depth, h->cu_count, wpl, h->persist_waves, &p)) return 0;
     if (!h->d_sync) {
         if (hipMalloc(&h->d_sync, (size_t)(h->cu_count + 2) * sizeof(unsigned)) != hipSuccess ||
             hipHostMalloc(&h->h_err, sizeof(unsigned), hipHostMallocDefault) != hipSuccess) {
@@ -601,6 +602,12 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     if (!strcmp(key, "persist_depth")) {
         if (value < 0 || value > GOLHIP_MAX_TB_DEPTH) return fail(GOLHIP_EINVAL, "persist_depth %lld", (long long)value);
         h->persist_depth = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "persist_waves")) {
+        if (value != 0 && value != 4 && value != 8 && value != 16)
+            return fail(GOLHIP_EINVAL, "persist_waves %lld not in {0,4,8,16}", (long long)value);
+        h->persist_waves = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "fill_skip")) {

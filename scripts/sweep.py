@@ -43,7 +43,7 @@ for N in map(int, a.sizes.split(",")):
                     p = b.perf()
                     kms = p["step_kernel_ms"] + p["persist_kernel_ms"]
                     kern = kms / max(1, p["step_launches"] + p["persist_launches"])
-                    rec = dict(N=N, depth=d, rpw=s, variant=v, rpw_used=p["rows_per_wave"],
+                    rec = dict(N=N, depth=d, rpw=s, variant=v, rpw_used=p["rows_per_wave"], persist=p["persist_launches"],
                                wall_gcups=N * N * a.turns / dt / 1e9,
                                kernel_gcups=N * N * a.turns / (kms * 1e-3) / 1e9, launch_ms=kern)
                     if rec["wall_gcups"] > best.get(v, {"wall_gcups": 0})["wall_gcups"]:

@@ -326,3 +326,21 @@ def test_persistent_full_size_matches_per_launch(N, turns):
             b.step(turns)
             res.append((b.board_hash(), b.alive_count()))
     assert res[0] == res[1]
+
+
+@pytest.mark.parametrize("N,depth,wpl,nw", [(2048, 8, 1, 4), (2048, 16, 1, 4), (4096, 8, 2, 4), (4096, 16, 2, 4),
+                                            (2048, 8, 1, 8), (4096, 8, 2, 8), (1024, 4, 2, 4)])
+def test_persistent_waves_per_workgroup(coracle, N, depth, wpl, nw):
+    """Persistent kernel with 4 / 8 resident waves per workgroup vs the C oracle."""
+    board = coracle.fill_random(N, N // 2, 0x5EED0008)
+    turns = 4 * depth + 3
+    want = coracle.run(board, turns)
+    with golhip.Board(N, N // 2) as b:
+        b.set_option("wpl", wpl)
+        b.set_option("persist_waves", nw)
+        b.set_tb_depth(depth)
+        b.load_bytes(board)
+        b.step(turns)
+        assert b.perf()["persist_launches"] == 1
+        assert np.array_equal(b.snapshot_bytes(), want)
+        assert b.alive_count() == (int((want == 255).sum()), turns)
