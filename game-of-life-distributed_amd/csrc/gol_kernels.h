@@ -65,10 +65,16 @@ struct PersistArgs {
     long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
 };
 int persist_waves_for(int depth, int wpl);
-int persist_blocks_per_cu(int depth, int wpl, int nw);
-// Workgroup shape / band height for `cus` resident workgroups; false if none fits.
-bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, int nw, PersistArgs *p);
-hipError_t launch_persist(const PersistArgs &p, int depth, int wpl, hipStream_t s);
+// diag: diagonal (systolic) stage schedule instead of skewed 3-row groups.
+int persist_blocks_per_cu(int depth, int wpl, int nw, bool diag);
+// Workgroup shape / band height for `cus` resident workgroups of `units`
+// (tile, strip) units each; false if none fits.  Caller sets p->nw.
+bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, int units, PersistArgs *p);
+hipError_t launch_persist(const PersistArgs &p, int depth, int wpl, bool diag, hipStream_t s);
+// Stage-split persistent kernel K1s: p.nw = nws * (pipelines per workgroup).
+// gt = groups of 3 rows per tick.
+int pipe_blocks_per_cu(int depth, int wpl, int nws, int np, int gt);
+hipError_t launch_pipe(const PersistArgs &p, int depth, int wpl, int nws, int gt, hipStream_t s);
 
 hipError_t launch_pack(const uint8_t *bytes, uint32_t *words, int W, int Ww, int rows, hipStream_t s);
 hipError_t launch_unpack(const uint32_t *words, uint8_t *bytes, int W, int Ww, int rows, hipStream_t s);

@@ -33,12 +33,20 @@ constexpr unsigned tt3(F f) {
 // v_bitop3_b32 truth tables, operand order (a, b, c) -> index a*4 + b*2 + c.
 constexpr unsigned kXor3 = tt3([](int a, int b, int c) { return (a ^ b ^ c) != 0; });       // 0x96
 constexpr unsigned kMaj = tt3([](int a, int b, int c) { return a + b + c >= 2; });          // 0xE8
-// Column sum of three 2-bit row sums: sum9 = u0 + 2*(u1 + v0) + 4*v1 (centre included).
-// next = (sum9 == 3) | (centre & sum9 == 4)  <=>  B3/S23.
-constexpr unsigned kT1 = tt3([](int u1, int v0, int v1) { return ((u1 ^ v0) & !v1) != 0; });          // twos == 1
-constexpr unsigned kT2 = tt3([](int u1, int v0, int v1) { return ((!(u1 ^ v0)) & ((u1 & v0) ^ v1)) != 0; });  // twos == 2
-constexpr unsigned kBorn = tt3([](int c, int t2, int u0) { return (c & t2 & !u0) != 0; });
-constexpr unsigned kNext = tt3([](int u0, int t1, int b) { return ((u0 & t1) | b) != 0; });
+// Column sum of three 2-bit row sums (h0 + 2 h1 each, centre included):
+//   u = sum of the h0 bits = u0 + 2 u1,  v = sum of the h1 bits = v0 + 2 v1,
+//   sum9 = u0 + 2 T with T = u1 + v0 + 2 v1.
+// next = (sum9 == 3) | (centre & sum9 == 4) in three LUTs, found by exhaustive
+// search over 3-gate circuits; it leans on one unreachable input (centre
+// alive with sum9 == 0) and is checked against all 512 neighbourhoods in
+// tests/test_rule_circuit.py:
+//   g1   = [T == 0 or T == 2]
+//   g2   = !v1 & (!centre | u0) | !u0 & !centre
+//   next = u0 ? (!g1 & g2) : (g1 & !g2)
+constexpr unsigned kG1 = tt3([](int u1, int v0, int v1) { int T = u1 + v0 + 2 * v1; return T == 0 || T == 2; });
+constexpr unsigned kG2 = tt3([](int u0, int v1, int c) { return (!v1 && (!c || u0)) || (!u0 && !c); });
+constexpr unsigned kNext = tt3([](int u0, int g1, int g2) { return u0 ? (!g1 && g2) : (g1 && !g2); });
+static_assert(kG1 == 0x43 && kG2 == 0x35 && kNext == 0x24, "rule LUTs");
 static_assert(kXor3 == 0x96 && kMaj == 0xE8, "bitop3 table order");
 
 template <unsigned IMM>
@@ -86,9 +94,9 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 // 1..62 are exact and stored.  Vertically a wave reads D extra rows above and
 // below its band.
 // Per stage, row and word: 2/WPL DPP + 2 alignbit + 2 bitop3 (3-cell row sum,
-// shared by the three output rows that use it) + 8 bitop3 (column sum + rule).
+// shared by the three output rows that use it) + 7 bitop3 (column sum + rule).
 // DPP and alignbit issue at half rate on gfx950, bitop3 at full rate, so
-// WPL = 2 cuts a word-turn from ~18 to ~16 full-rate slots.
+// WPL = 2 cuts a word-turn from ~17 to ~15 full-rate slots.
 // HBM traffic per launch ~ 2 bits per cell (read + write) for D turns.
 // ---------------------------------------------------------------------------
 template <int WPL>
@@ -118,10 +126,9 @@ __device__ __forceinline__ void stage(int t, Lanes<WPL> &x, uint32_t (&h0)[3][D]
         const uint32_t u1 = bop<kMaj>(h0[P][t][k], h0[C][t][k], h0[N][t][k]);
         const uint32_t v0 = bop<kXor3>(h1[P][t][k], h1[C][t][k], h1[N][t][k]);
         const uint32_t v1 = bop<kMaj>(h1[P][t][k], h1[C][t][k], h1[N][t][k]);
-        const uint32_t t1 = bop<kT1>(u1, v0, v1);
-        const uint32_t t2 = bop<kT2>(u1, v0, v1);
-        const uint32_t born = bop<kBorn>(cc[C][t][k], t2, u0);
-        nx[k] = bop<kNext>(u0, t1, born);
+        const uint32_t g1 = bop<kG1>(u1, v0, v1);
+        const uint32_t g2 = bop<kG2>(u0, v1, cc[C][t][k]);
+        nx[k] = bop<kNext>(u0, g1, g2);
     }
 #pragma unroll
     for (int k = 0; k < WPL; ++k) {
@@ -265,6 +272,130 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
     return cnt;
 }
 
+// ---------------------------------------------------------------------------
+// Diagonal (systolic) schedule of the same D-stage pipeline.
+//
+// Iteration n feeds input row n into stage 0 while stage t works on row
+// n - t: the D stage-steps of an iteration are independent, so a wave has D
+// dependency chains in flight instead of the ~2.7 of a skewed 3-row group.
+// That keeps the VALU busy at 1-2 waves per SIMD, which in turn lets a
+// persistent launch use fewer, taller bands (less pipeline fill).  The set of
+// (row, stage) pairs computed is the group schedule's: stage t skips rows
+// that only carry pipeline-fill padding (n < 3t) and, after the last input,
+// rows that do not exist (n - t > last).
+// ---------------------------------------------------------------------------
+template <int D, int WPL, int U, int A0, int A1, int T>
+__device__ __forceinline__ void diag_stages(Lanes<WPL> (&xs)[D + 1], uint32_t (&h0)[3][D][WPL],
+                                            uint32_t (&h1)[3][D][WPL], uint32_t (&cc)[3][D][WPL]) {
+    if constexpr (T >= 0) {
+        if constexpr (T >= A0 && T < A1) {
+            constexpr int R = ((U - T) % 3 + 3) % 3;
+            Lanes<WPL> y = xs[T];
+            stage<D, R, WPL>(T, y, h0, h1, cc);
+            xs[T + 1] = y;
+        }
+        diag_stages<D, WPL, U, A0, A1, T - 1>(xs, h0, h1, cc);
+    }
+}
+
+template <int D, int SKIP_UNUSED, int WPL>
+__device__ __forceinline__ uint32_t stream_band_diag(const StepArgs &a, int r0, int rows_here, int t0) {
+    const int lane = threadIdx.x & 63;
+    const int Ww = a.Ww;
+    int col = (t0 + WPL * (lane - 1)) % Ww;
+    if (col < 0) col += Ww;
+    const bool keep = lane >= 1 && lane <= kTileValid && (t0 + WPL * (lane - 1)) < Ww;
+
+    int r = r0 - D + a.in.off;
+    const int wrap = a.in.wrap > 0 ? a.in.wrap : INT_MAX;
+    if (a.in.wrap > 0) {
+        r %= a.in.wrap;
+        if (r < 0) r += a.in.wrap;
+    }
+    const uint32_t *__restrict__ src = a.src + col;
+    auto load_next = [&]() -> Lanes<WPL> {
+        const int pr = a.in.base + min(r, a.in.rmax);
+        Lanes<WPL> v;
+        if constexpr (WPL == 1) {
+            v.w[0] = src[(size_t)pr * Ww];
+        } else {
+            const uint2 q = *reinterpret_cast<const uint2 *>(src + (size_t)pr * Ww);
+            v.w[0] = q.x;
+            v.w[1] = q.y;
+        }
+        r = (r + 1 == wrap) ? 0 : r + 1;
+        return v;
+    };
+    uint32_t *const dst_row0 = a.dst + (size_t)(a.dst_base + r0) * Ww + col;
+    uint32_t *const dummy = a.dst + col;
+    uint32_t cnt = 0;
+    auto emit = [&](const Lanes<WPL> &y, int out_idx) {
+        const bool ok = keep && (unsigned)out_idx < (unsigned)rows_here;
+        uint32_t *p = ok ? dst_row0 + (ptrdiff_t)out_idx * Ww : dummy;
+        uint32_t pc = 0;
+        if constexpr (WPL == 1) {
+            *p = y.w[0];
+            pc = __builtin_popcount(y.w[0]);
+        } else {
+            *reinterpret_cast<uint2 *>(p) = make_uint2(y.w[0], y.w[1]);
+            pc = __builtin_popcount(y.w[0]) + __builtin_popcount(y.w[1]);
+        }
+        cnt += ok ? pc : 0u;
+    };
+
+    uint32_t h0[3][D][WPL], h1[3][D][WPL], cc[3][D][WPL];
+    Lanes<WPL> xs[D + 1];
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int t = 0; t < D; ++t)
+#pragma unroll
+            for (int k = 0; k < WPL; ++k) h0[s][t][k] = h1[s][t][k] = cc[s][t][k] = 0u;
+#pragma unroll
+    for (int t = 0; t <= D; ++t)
+#pragma unroll
+        for (int k = 0; k < WPL; ++k) xs[t].w[k] = 0u;
+
+    // iteration n: out index n + 1 - 3D; the last row that matters enters at
+    // n = last = rows_here + 2D - 1 and leaves stage D-1 at n = last + D - 1
+    const int last = rows_here + 2 * D - 1;
+    const int n_end = last + D;  // exclusive
+    Lanes<WPL> x0 = vmov(load_next()), x1 = vmov(load_next()), x2 = vmov(load_next());
+    int n = 0;
+    auto body = [&](auto a0_tag, auto a1_tag) {
+        constexpr int A0 = decltype(a0_tag)::value;
+        constexpr int A1 = decltype(a1_tag)::value;
+        const Lanes<WPL> p0 = load_next(), p1 = load_next(), p2 = load_next();
+        __builtin_amdgcn_sched_barrier(0);
+        xs[0] = x0;
+        diag_stages<D, WPL, 0, A0, A1, D - 1>(xs, h0, h1, cc);
+        emit(xs[D], n + 1 - 3 * D);
+        xs[0] = x1;
+        diag_stages<D, WPL, 1, A0, A1, D - 1>(xs, h0, h1, cc);
+        emit(xs[D], n + 2 - 3 * D);
+        xs[0] = x2;
+        diag_stages<D, WPL, 2, A0, A1, D - 1>(xs, h0, h1, cc);
+        emit(xs[D], n + 3 - 3 * D);
+        __builtin_amdgcn_sched_barrier(0);
+        x0 = vmov(p0);
+        x1 = vmov(p1);
+        x2 = vmov(p2);
+        n += 3;
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using ID = std::integral_constant<int, D>;
+    // fill: body at n = 3q runs stages t <= q (n >= 3t)
+    while (n / 3 + 1 <= D / 4) body(I0(), std::integral_constant<int, D / 4>());
+    while (n / 3 + 1 <= D / 2) body(I0(), std::integral_constant<int, D / 2>());
+    while (n / 3 + 1 <= 3 * D / 4) body(I0(), std::integral_constant<int, 3 * D / 4>());
+    // steady state, then drain: skip stages t < n - last (rows past the end)
+    while (n - last < D / 4 && n < n_end) body(I0(), ID());
+    while (n - last < D / 2 && n < n_end) body(std::integral_constant<int, D / 4>(), ID());
+    while (n - last < 3 * D / 4 && n < n_end) body(std::integral_constant<int, D / 2>(), ID());
+    while (n < n_end) body(std::integral_constant<int, 3 * D / 4>(), ID());
+    return cnt;
+}
+
 __host__ __device__ constexpr int tile_words(int wpl) { return kTileValid * wpl; }
 
 template <int D, bool SKIP, int WPL>
@@ -301,7 +432,7 @@ __global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int persist_waves(int depth, int wpl) { return depth * wpl <= 16 ? 16 : 8; }
 
-template <int D, int WPL, int NW>
+template <int D, int WPL, int NW, bool DIAG>
 __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -351,7 +482,238 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
         const bool odd = ((p.first + j) & 1) != 0;
         a.src = odd ? p.buf1 : p.buf0;
         a.dst = odd ? p.buf0 : p.buf1;
-        cnt = rows_here > 0 ? stream_band<D, true, WPL>(a, r0, rows_here, tile * tile_words(WPL)) : 0u;
+        if constexpr (DIAG)
+            cnt = rows_here > 0 ? stream_band_diag<D, 1, WPL>(a, r0, rows_here, tile * tile_words(WPL)) : 0u;
+        else
+            cnt = rows_here > 0 ? stream_band<D, true, WPL>(a, r0, rows_here, tile * tile_words(WPL)) : 0u;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&p.progress[b], (unsigned)(j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (p.base.alive) {
+        const uint32_t tot = wave_sum_u32(cnt);
+        if (lane == 0 && tot) atomicAdd(p.base.alive, (unsigned long long)tot);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K1s: persistent kernel with the D stages of a band split over NWS waves.
+//
+// Same super-step protocol as K1p, but a workgroup runs P pipelines (one
+// (tile, strip) unit each) of NWS wavefronts: wave k of a pipeline owns
+// stages [k*DW, (k+1)*DW) and hands each 3-row group to wave k+1 through a
+// double-buffered LDS slot.  The waves advance in ticks separated by a
+// workgroup barrier; at tick tau wave k works on group tau - 2k.  A unit's
+// pipeline fill (2D input rows) is then paid once per NWS waves, so with the
+// same resident waves a band is NWS times taller and the fill fraction
+// (~1.25 D / S) NWS times smaller — the limit of K1p on boards whose
+// (tile, strip) units barely cover the machine (16384^2: S = 37 rows).
+// Waves whose stages would only see pipeline-fill padding skip the group.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int D, int WPL, int NWS, int GT>
+__device__ __forceinline__ uint32_t pipe_band(const StepArgs &a, int r0, int rows_here, int t0, int k, int T,
+                                              uint32_t *__restrict__ ring, bool count) {
+    constexpr int DW = D / NWS;
+    constexpr int SLOT = 3 * 64 * WPL;
+    const int lane = threadIdx.x & 63;
+    const int Ww = a.Ww;
+    int col = (t0 + WPL * (lane - 1)) % Ww;
+    if (col < 0) col += Ww;
+    const bool keep = lane >= 1 && lane <= kTileValid && (t0 + WPL * (lane - 1)) < Ww;
+    const int G = rows_here > 0 ? (rows_here + 2 * D + 2) / 3 : 0;
+
+    int r = r0 - D + a.in.off;
+    const int wrap = a.in.wrap > 0 ? a.in.wrap : INT_MAX;
+    if (a.in.wrap > 0) {
+        r %= a.in.wrap;
+        if (r < 0) r += a.in.wrap;
+    }
+    const uint32_t *__restrict__ src = a.src + col;
+    auto load_next = [&]() -> Lanes<WPL> {
+        const int pr = a.in.base + min(r, a.in.rmax);
+        Lanes<WPL> v;
+        if constexpr (WPL == 1) {
+            v.w[0] = src[(size_t)pr * Ww];
+        } else {
+            const uint2 q = *reinterpret_cast<const uint2 *>(src + (size_t)pr * Ww);
+            v.w[0] = q.x;
+            v.w[1] = q.y;
+        }
+        r = (r + 1 == wrap) ? 0 : r + 1;
+        return v;
+    };
+    uint32_t *const dst_row0 = a.dst + (size_t)(a.dst_base + r0) * Ww + col;
+    uint32_t *const dummy = a.dst + col;
+    uint32_t cnt = 0;
+    auto emit = [&](const Lanes<WPL> &y, int out_idx) {
+        const bool ok = keep && (unsigned)out_idx < (unsigned)rows_here;
+        uint32_t *q = ok ? dst_row0 + (ptrdiff_t)out_idx * Ww : dummy;
+        uint32_t pc = 0;
+        if constexpr (WPL == 1) {
+            *q = y.w[0];
+            pc = __builtin_popcount(y.w[0]);
+        } else {
+            *reinterpret_cast<uint2 *>(q) = make_uint2(y.w[0], y.w[1]);
+            pc = __builtin_popcount(y.w[0]) + __builtin_popcount(y.w[1]);
+        }
+        cnt += (ok && count) ? pc : 0u;
+    };
+    auto slot_put = [&](uint32_t *sl, const Lanes<WPL> &y, int row) {
+        if constexpr (WPL == 1) {
+            sl[row * 64 + lane] = y.w[0];
+        } else {
+            reinterpret_cast<uint2 *>(sl)[row * 64 + lane] = make_uint2(y.w[0], y.w[1]);
+        }
+    };
+    auto slot_get = [&](const uint32_t *sl, int row) -> Lanes<WPL> {
+        Lanes<WPL> v;
+        if constexpr (WPL == 1) {
+            v.w[0] = sl[row * 64 + lane];
+        } else {
+            const uint2 q = reinterpret_cast<const uint2 *>(sl)[row * 64 + lane];
+            v.w[0] = q.x;
+            v.w[1] = q.y;
+        }
+        return v;
+    };
+
+    uint32_t h0[3][DW][WPL], h1[3][DW][WPL], cc[3][DW][WPL];
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int t = 0; t < DW; ++t)
+#pragma unroll
+            for (int q = 0; q < WPL; ++q) h0[s][t][q] = h1[s][t][q] = cc[s][t][q] = 0u;
+
+    // Wave k works on the GT groups from GT * (tau - 2k) at tick tau: their
+    // input (written by wave k-1 at tick tau - 2) is read from LDS one tick
+    // ahead, so the LDS latency hides behind a tick of compute instead of
+    // stalling every wave right after the barrier.  Wave 0 streams from global
+    // memory the same way.
+    auto active = [&](int g) { return g >= 0 && g < G && (3 * g + 2) / 2 + 1 > k * DW; };
+    Lanes<WPL> x[GT][3];
+#pragma unroll
+    for (int q = 0; q < GT; ++q) x[q][0] = x[q][1] = x[q][2] = Lanes<WPL>{};
+    if (k == 0 && G > 0) {
+#pragma unroll
+        for (int q = 0; q < GT; ++q) {
+            x[q][0] = vmov(load_next());
+            x[q][1] = vmov(load_next());
+            x[q][2] = vmov(load_next());
+        }
+    }
+    for (int tau = 0; tau < T; ++tau) {
+        const int gb = GT * (tau - 2 * k);
+        Lanes<WPL> n[GT][3];
+#pragma unroll
+        for (int q = 0; q < GT; ++q) {
+            n[q][0] = n[q][1] = n[q][2] = Lanes<WPL>{};
+            if (k == 0) {
+                if (active(gb + q)) {
+                    n[q][0] = load_next();
+                    n[q][1] = load_next();
+                    n[q][2] = load_next();
+                }
+            } else if (active(gb + GT + q)) {
+                const uint32_t *in = ring + ((k - 1) * 2 * GT + ((gb + GT + q) % (2 * GT))) * SLOT;
+                n[q][0] = slot_get(in, 0);
+                n[q][1] = slot_get(in, 1);
+                n[q][2] = slot_get(in, 2);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < GT; ++q) {
+            const int g = gb + q;
+            if (active(g)) {
+                Lanes<WPL> y0 = x[q][0], y1 = x[q][1], y2 = x[q][2];
+                __builtin_amdgcn_sched_barrier(0);
+                push_group<DW, DW, WPL>(y0, y1, y2, h0, h1, cc);
+                if (k == NWS - 1) {
+                    const int oi = -2 * D + 3 * g;
+                    emit(y0, oi);
+                    emit(y1, oi + 1);
+                    emit(y2, oi + 2);
+                } else {
+                    uint32_t *out = ring + (k * 2 * GT + (g % (2 * GT))) * SLOT;
+                    slot_put(out, y0, 0);
+                    slot_put(out, y1, 1);
+                    slot_put(out, y2, 2);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < GT; ++q) {
+            x[q][0] = vmov(n[q][0]);
+            x[q][1] = vmov(n[q][1]);
+            x[q][2] = vmov(n[q][2]);
+        }
+        lds_barrier();
+    }
+    return cnt;
+}
+
+template <int D, int WPL, int NWS, int P, int GT>
+__global__ __launch_bounds__(NWS * P * 64) void gol_pipe_kernel(PersistArgs p) {
+    constexpr int SLOT = 3 * 64 * WPL;
+    __shared__ uint32_t ring[P][NWS > 1 ? 2 * GT * (NWS - 1) * SLOT : 1];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int k = w / P;
+    const int pipe = w - k * P;
+    const int b = blockIdx.x;
+    const int wx = b % p.cols, wy = b / p.cols;
+    const int tile = wx * p.wg_tx + pipe % p.wg_tx;
+    const int strip = wy * p.wg_sy + pipe / p.wg_tx;
+    const int r0 = strip * p.S;
+    const int rows_here = (tile < p.tiles_x && r0 < p.base.rows_out) ? min(p.S, p.base.rows_out - r0) : 0;
+    const int T = ((p.S + 2 * D + 2) / 3 + GT - 1) / GT + 2 * (NWS - 1);  // ticks: tallest band + ramp
+
+    int nb = b;
+    if (lane < 9) {
+        const int ny = (wy + lane / 3 - 1 + p.wg_y) % p.wg_y;
+        const int nx = (wx + lane % 3 - 1 + p.cols) % p.cols;
+        nb = ny * p.cols + nx;
+    }
+    __shared__ int s_abort;
+    if (threadIdx.x == 0) s_abort = 0;
+    __syncthreads();
+
+    uint32_t cnt = 0;
+    for (int j = 0; j < p.J; ++j) {
+        if (j > 0) {
+            if (w == 0) {
+                const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
+                for (;;) {
+                    const unsigned v = __hip_atomic_load(&p.progress[nb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (__all(v >= (unsigned)j)) break;
+                    const unsigned err = __hip_atomic_load(p.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (err || (long long)__builtin_amdgcn_s_memrealtime() - t_start > p.timeout_ticks) {
+                        if (lane == 0) {
+                            atomicOr(p.error, 1u);
+                            s_abort = 1;
+                        }
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if (lane == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();
+            if (s_abort) return;  // uniform over the workgroup
+        }
+        StepArgs a = p.base;
+        const bool odd = ((p.first + j) & 1) != 0;
+        a.src = odd ? p.buf1 : p.buf0;
+        a.dst = odd ? p.buf0 : p.buf1;
+        cnt = pipe_band<D, WPL, NWS, GT>(a, r0, rows_here, tile * tile_words(WPL), k, T, &ring[pipe][0], j == p.J - 1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -430,31 +792,35 @@ int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_sk
 
 // nw = waves per workgroup (one workgroup per CU): 4, 8 or 16; 0 = default.
 template <typename F>
-static hipError_t dispatch_persist(int depth, int wpl, int nw, F &&f) {
+static hipError_t dispatch_persist(int depth, int wpl, int nw, bool diag, F &&f) {
     if (nw == 0) nw = persist_waves(depth, wpl);
 #define GOL_PCASE(D, WP, NW) \
-    if (depth == D && wpl == WP && nw == NW) return f(gol_persist_kernel<D, WP, NW>, NW);
+    if (!diag && depth == D && wpl == WP && nw == NW) return f(gol_persist_kernel<D, WP, NW, false>, NW);
+#define GOL_DCASE(D, WP, NW) \
+    if (diag && depth == D && wpl == WP && nw == NW) return f(gol_persist_kernel<D, WP, NW, true>, NW);
     GOL_PCASE(4, 1, 16) GOL_PCASE(8, 1, 16) GOL_PCASE(16, 1, 16) GOL_PCASE(32, 1, 8) GOL_PCASE(4, 2, 16)
     GOL_PCASE(8, 2, 16) GOL_PCASE(16, 2, 8)
     GOL_PCASE(4, 1, 4) GOL_PCASE(8, 1, 4) GOL_PCASE(16, 1, 4) GOL_PCASE(8, 1, 8) GOL_PCASE(16, 1, 8)
     GOL_PCASE(4, 2, 4) GOL_PCASE(8, 2, 4) GOL_PCASE(16, 2, 4) GOL_PCASE(4, 2, 8) GOL_PCASE(8, 2, 8)
+    GOL_DCASE(8, 1, 4) GOL_DCASE(8, 1, 8) GOL_DCASE(16, 1, 4) GOL_DCASE(16, 1, 8)
+    GOL_DCASE(32, 1, 4) GOL_DCASE(8, 2, 4) GOL_DCASE(8, 2, 8) GOL_DCASE(16, 2, 4)
 #undef GOL_PCASE
+#undef GOL_DCASE
     return hipErrorInvalidValue;
 }
 
 int persist_waves_for(int depth, int wpl) { return persist_waves(depth, wpl); }
 
-int persist_blocks_per_cu(int depth, int wpl, int nw) {
+int persist_blocks_per_cu(int depth, int wpl, int nw, bool diag) {
     int b = 0;
-    hipError_t e = dispatch_persist(depth, wpl, nw, [&](auto kern, int n) {
+    hipError_t e = dispatch_persist(depth, wpl, nw, diag, [&](auto kern, int n) {
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 64 * n, 0);
     });
     return e == hipSuccess ? b : 0;
 }
 
-bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, int nw, PersistArgs *p) {
-    const int NW = nw > 0 ? nw : persist_waves(depth, wpl);
-    p->nw = NW;
+bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, int units, PersistArgs *p) {
+    const int NW = units;
     const int tiles_x = tb_tiles(Ww, wpl);
     bool found = false;
     long best_s = 0;
@@ -484,8 +850,39 @@ bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, int nw, Persist
     return found;
 }
 
-hipError_t launch_persist(const PersistArgs &p, int depth, int wpl, hipStream_t s) {
-    return dispatch_persist(depth, wpl, p.nw, [&](auto kern, int nw) {
+// (depth, wpl, stage waves NWS, pipelines P) of the stage-split kernel K1s.
+template <typename F>
+static hipError_t dispatch_pipe(int depth, int wpl, int nws, int np, int gt, F &&f) {
+#define GOL_SCASE(D, WP, NS, NP, GT) \
+    if (depth == D && wpl == WP && nws == NS && np == NP && gt == GT) return f(gol_pipe_kernel<D, WP, NS, NP, GT>, NS * NP);
+    GOL_SCASE(16, 1, 4, 4, 1) GOL_SCASE(16, 1, 4, 4, 2) GOL_SCASE(16, 1, 4, 4, 4)
+    GOL_SCASE(16, 1, 2, 8, 1) GOL_SCASE(16, 1, 2, 8, 2) GOL_SCASE(16, 1, 2, 8, 4)
+    GOL_SCASE(32, 1, 4, 4, 1) GOL_SCASE(32, 1, 4, 4, 2) GOL_SCASE(32, 1, 4, 4, 4)
+    GOL_SCASE(32, 1, 8, 2, 1) GOL_SCASE(32, 1, 8, 2, 2) GOL_SCASE(32, 1, 8, 2, 4)
+    GOL_SCASE(16, 2, 4, 4, 1) GOL_SCASE(16, 2, 4, 4, 2) GOL_SCASE(16, 2, 2, 8, 1) GOL_SCASE(16, 2, 2, 8, 2)
+    GOL_SCASE(32, 2, 4, 4, 1) GOL_SCASE(32, 2, 4, 4, 2) GOL_SCASE(8, 1, 2, 8, 1) GOL_SCASE(8, 2, 2, 8, 1)
+    GOL_SCASE(16, 1, 8, 2, 1) GOL_SCASE(16, 1, 8, 2, 2)
+#undef GOL_SCASE
+    return hipErrorInvalidValue;
+}
+
+int pipe_blocks_per_cu(int depth, int wpl, int nws, int np, int gt) {
+    int b = 0;
+    hipError_t e = dispatch_pipe(depth, wpl, nws, np, gt, [&](auto kern, int n) {
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 64 * n, 0);
+    });
+    return e == hipSuccess ? b : 0;
+}
+
+hipError_t launch_pipe(const PersistArgs &p, int depth, int wpl, int nws, int gt, hipStream_t s) {
+    return dispatch_pipe(depth, wpl, nws, p.nw / nws, gt, [&](auto kern, int n) {
+        hipLaunchKernelGGL(kern, dim3(p.cols * p.wg_y), dim3(64 * n), 0, s, p);
+        return hipGetLastError();
+    });
+}
+
+hipError_t launch_persist(const PersistArgs &p, int depth, int wpl, bool diag, hipStream_t s) {
+    return dispatch_persist(depth, wpl, p.nw, diag, [&](auto kern, int nw) {
         hipLaunchKernelGGL(kern, dim3(p.cols * p.wg_y), dim3(64 * nw), 0, s, p);
         return hipGetLastError();
     });

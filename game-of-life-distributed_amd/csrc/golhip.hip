@@ -88,6 +88,10 @@ struct golhip {
     int wpl_opt = 0;            // option "wpl": words per lane (0 = auto, 1, 2)
     int persist_depth = 0;      // option "persist_depth" (0: tb_depth)
     int persist_waves = 0;      // option "persist_waves": waves per workgroup (0: default)
+    int stage_waves = 0;        // option "stage_waves": >= 2 selects K1s (waves per pipeline)
+    int pipe_units = 0;         // option "pipe_units": K1s pipelines per workgroup (0: 16 / stage_waves)
+    bool diag = false;          // option "diag": diagonal stage schedule in K1p
+    int pipe_groups = 1;        // option "pipe_groups": K1s 3-row groups per tick (1, 2, 4)
     unsigned *d_sync = nullptr; // persistent kernel: [0] error, [1..] progress per workgroup
     unsigned *h_err = nullptr;  // pinned copy of the error word
     bool persist_pending = false;
@@ -371,14 +375,25 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     *rc = GOLHIP_OK;
     if (!h->persistent || h->W % 32 != 0 || !h->torus()) return 0;
     const int wpl = wpl_for(h);
-    const int depth = largest_depth(std::min(h->persist_depth > 0 ? h->persist_depth : h->tb_depth,
-                                             golk::max_depth_for(wpl)));
+    const int nws = h->stage_waves;  // >= 2: stage-split kernel K1s
+    const int max_d = nws >= 2 ? GOLHIP_MAX_TB_DEPTH : golk::max_depth_for(wpl);
+    const int depth = largest_depth(std::min(h->persist_depth > 0 ? h->persist_depth : h->tb_depth, max_d));
     if (depth < 4) return 0;
     const int64_t J = left / depth;
     if (J < 2) return 0;
-    if (golk::persist_blocks_per_cu(depth, wpl, h->persist_waves) < 1) return 0;
+    int nw = 0, units = 0;
+    if (nws >= 2) {
+        units = h->pipe_units > 0 ? h->pipe_units : 16 / nws;
+        if (depth % nws != 0 || golk::pipe_blocks_per_cu(depth, wpl, nws, units, h->pipe_groups) < 1) return 0;
+        nw = nws * units;
+    } else {
+        nw = h->persist_waves > 0 ? h->persist_waves : golk::persist_waves_for(depth, wpl);
+        if (golk::persist_blocks_per_cu(depth, wpl, nw, h->diag) < 1) return 0;
+        units = nw;
+    }
     golk::PersistArgs p{};
-    if (!golk::plan_persist(h->Ww, h->rows, depth, h->cu_count, wpl, h->persist_waves, &p)) return 0;
+    if (!golk::plan_persist(h->Ww, h->rows, depth, h->cu_count, wpl, units, &p)) return 0;
+    p.nw = nw;
     if (!h->d_sync) {
         if (hipMalloc(&h->d_sync, (size_t)(h->cu_count + 2) * sizeof(unsigned)) != hipSuccess ||
             hipHostMalloc(&h->h_err, sizeof(unsigned), hipHostMallocDefault) != hipSuccess) {
@@ -407,7 +422,8 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
         e1 = take_event(h);
         if (e0 && e1) e = hipEventRecord(e0, h->stream);
     }
-    if (e == hipSuccess) e = golk::launch_persist(p, depth, wpl, h->stream);
+    if (e == hipSuccess)
+        e = nws >= 2 ? golk::launch_pipe(p, depth, wpl, nws, h->pipe_groups, h->stream) : golk::launch_persist(p, depth, wpl, h->diag, h->stream);
     if (e == hipSuccess && e1) {
         e = hipEventRecord(e1, h->stream);
         h->ev_pending.push_back({e0, e1, true});
@@ -608,6 +624,26 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         if (value != 0 && value != 4 && value != 8 && value != 16)
             return fail(GOLHIP_EINVAL, "persist_waves %lld not in {0,4,8,16}", (long long)value);
         h->persist_waves = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "stage_waves")) {
+        if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
+            return fail(GOLHIP_EINVAL, "stage_waves %lld not in {0,1,2,4,8}", (long long)value);
+        h->stage_waves = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "diag")) {
+        h->diag = value != 0;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "pipe_groups")) {
+        if (value != 1 && value != 2 && value != 4) return fail(GOLHIP_EINVAL, "pipe_groups %lld", (long long)value);
+        h->pipe_groups = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "pipe_units")) {
+        if (value < 0 || value > 16) return fail(GOLHIP_EINVAL, "pipe_units %lld", (long long)value);
+        h->pipe_units = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "fill_skip")) {

@@ -20,6 +20,9 @@ ap.add_argument("--turns", type=int, default=256)
 ap.add_argument("--repeats", type=int, default=1)
 a = ap.parse_args()
 variants = [v for v in a.variants.split(";") if v] or [""]
+# engine options are sticky on a handle: every variant starts from the defaults
+DEFAULTS = {"wpl": 0, "persistent": 1, "persist_depth": 0, "persist_waves": 0, "stage_waves": 0, "pipe_units": 0,
+            "pipe_groups": 1, "diag": 0, "fill_skip": 1}
 for N in map(int, a.sizes.split(",")):
     b = golhip.Board(N, N, timing=True)
     b.fill_random(0x5EED0001)
@@ -28,7 +31,8 @@ for N in map(int, a.sizes.split(",")):
             best = {}
             for _ in range(a.repeats):
                 for v in variants:
-                    opts = dict(kv.split("=") for kv in v.split(",") if kv)
+                    opts = dict(DEFAULTS)
+                    opts.update(kv.split("=") for kv in v.split(",") if kv)
                     for k, val in opts.items():
                         b.set_option(k, int(val))
                     b.set_tb_depth(d)

@@ -344,3 +344,63 @@ def test_persistent_waves_per_workgroup(coracle, N, depth, wpl, nw):
         assert b.perf()["persist_launches"] == 1
         assert np.array_equal(b.snapshot_bytes(), want)
         assert b.alive_count() == (int((want == 255).sum()), turns)
+
+
+@pytest.mark.parametrize("N,depth,wpl,nws,units", [
+    (2048, 16, 1, 4, 4), (2048, 16, 1, 2, 8), (4096, 32, 1, 4, 4), (4096, 32, 1, 8, 2), (4096, 16, 2, 4, 4),
+    (4096, 16, 2, 2, 8), (4096, 32, 2, 4, 4), (2048, 8, 1, 2, 8), (4096, 8, 2, 2, 8), (2048, 16, 1, 8, 2),
+    (3968, 16, 1, 4, 4), (1024, 16, 1, 4, 4)])
+@pytest.mark.parametrize("gt", [1, 2, 4])
+def test_stage_split_matches_oracle(coracle, N, depth, wpl, nws, units, gt):
+    """Stage-split persistent kernel (K1s: the D stages spread over `nws` waves
+    that hand rows over through LDS) vs the C oracle, board and alive count."""
+    board = coracle.fill_random(N, N // 2, 0x5EED0009)
+    turns = 3 * depth + 7
+    want = coracle.run(board, turns)
+    with golhip.Board(N, N // 2) as b:
+        b.set_option("wpl", wpl)
+        b.set_option("stage_waves", nws)
+        b.set_option("pipe_units", units)
+        b.set_option("pipe_groups", gt)
+        b.set_tb_depth(depth)
+        b.load_bytes(board)
+        b.step(turns)
+        if b.perf()["persist_launches"] != 1:
+            pytest.skip("combination not instantiated")
+        assert np.array_equal(b.snapshot_bytes(), want)
+        assert b.alive_count() == (int((want == 255).sum()), turns)
+
+
+@pytest.mark.parametrize("nws,units,depth", [(4, 4, 16), (4, 4, 32), (2, 8, 16)])
+def test_stage_split_full_size(nws, units, depth):
+    """16384^2 synthetic board: K1s and the per-launch kernel agree (hash + count)."""
+    res = []
+    for opts in ({"stage_waves": nws, "pipe_units": units}, {"persistent": 0}):
+        with golhip.Board(16384, 16384) as b:
+            for k, v in opts.items():
+                b.set_option(k, v)
+            b.set_tb_depth(depth)
+            b.fill_random(0x5EED0001)
+            b.step(4 * depth + 3)
+            res.append((b.board_hash(), b.alive_count()))
+    assert res[0] == res[1]
+
+
+@pytest.mark.parametrize("N,depth,wpl,nw", [(2048, 8, 1, 4), (2048, 8, 1, 8), (2048, 16, 1, 4), (4096, 16, 1, 8),
+                                            (4096, 32, 1, 4), (4096, 8, 2, 4), (4096, 8, 2, 8), (4096, 16, 2, 4),
+                                            (3968, 16, 1, 4), (1024, 16, 1, 8)])
+def test_diagonal_schedule_matches_oracle(coracle, N, depth, wpl, nw):
+    """Persistent kernel with the diagonal (systolic) stage schedule vs the C oracle."""
+    board = coracle.fill_random(N, N // 2, 0x5EED000A)
+    turns = 3 * depth + 2
+    want = coracle.run(board, turns)
+    with golhip.Board(N, N // 2) as b:
+        b.set_option("wpl", wpl)
+        b.set_option("diag", 1)
+        b.set_option("persist_waves", nw)
+        b.set_tb_depth(depth)
+        b.load_bytes(board)
+        b.step(turns)
+        assert b.perf()["persist_launches"] == 1
+        assert np.array_equal(b.snapshot_bytes(), want)
+        assert b.alive_count() == (int((want == 255).sum()), turns)
