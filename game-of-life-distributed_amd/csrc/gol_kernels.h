@@ -36,7 +36,7 @@ struct StepArgs {
 };
 
 // Bit-sliced temporal-blocked step: `depth` in {1,2,4,8,16,32}; requires W % 32 == 0
-// (wpl = 2: W % 64 == 0 and depth <= 16).  fill_skip: skip the pipeline-fill
+// (wpl = 2: W % 64 == 0, depth <= 16, board in the interleaved pair layout).  fill_skip: skip the pipeline-fill
 // stage-rows that only see padding.  wpl: words per lane (1 or 2).
 hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s, bool fill_skip, int wpl);
 int max_depth_for(int wpl);
@@ -56,6 +56,7 @@ struct PersistArgs {
     int first;                // buffer holding generation 0 (0 -> buf0)
     int J;                    // super-steps of `depth` turns
     int S;                    // rows per wavefront
+    int Sb;                   // K1n: rows of a workgroup's bottom band
     int wg_tx, wg_sy;         // workgroup block of (tiles, strips)
     int cols, wg_y;           // workgroup grid
     int tiles_x;
@@ -63,6 +64,7 @@ struct PersistArgs {
     unsigned *progress;       // per workgroup, zeroed before launch
     unsigned *error;          // set on a spin timeout
     long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
+    unsigned long long *trace; // nullable diagnostics (golhip_persist_trace)
 };
 int persist_waves_for(int depth, int wpl);
 // diag: diagonal (systolic) stage schedule instead of skewed 3-row groups.
@@ -70,18 +72,28 @@ int persist_blocks_per_cu(int depth, int wpl, int nw, bool diag);
 // Workgroup shape / band height for `cus` resident workgroups of `units`
 // (tile, strip) units each; false if none fits.  Caller sets p->nw.
 bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, int units, PersistArgs *p);
-hipError_t launch_persist(const PersistArgs &p, int depth, int wpl, bool diag, hipStream_t s);
+// wt: write-through (sc1) output stores.
+hipError_t launch_persist(const PersistArgs &p, int depth, int wpl, bool diag, bool wt, hipStream_t s);
+// K1n: bands without the vertical halo (LDS hand-off of each stage's first
+// two rows to the band above inside a workgroup); p.nw = bands per workgroup.
+int k1n_blocks_per_cu(int depth, int wpl, int nw);
+bool plan_k1n(int Ww, int rows, int depth, int cus, int wpl, int nw, PersistArgs *p);
+hipError_t launch_k1n(const PersistArgs &p, int depth, int wpl, hipStream_t s);
 // Stage-split persistent kernel K1s: p.nw = nws * (pipelines per workgroup).
 // gt = groups of 3 rows per tick.
 int pipe_blocks_per_cu(int depth, int wpl, int nws, int np, int gt);
 hipError_t launch_pipe(const PersistArgs &p, int depth, int wpl, int nws, int gt, hipStream_t s);
 
 hipError_t launch_pack(const uint8_t *bytes, uint32_t *words, int W, int Ww, int rows, hipStream_t s);
-hipError_t launch_unpack(const uint32_t *words, uint8_t *bytes, int W, int Ww, int rows, hipStream_t s);
+// il: the words are in the interleaved pair layout of the wpl = 2 step kernels
+// (W % 64 == 0); pack / fill_random / load write canonical words, which the
+// engine converts in place with launch_convert_layout.
+hipError_t launch_unpack(const uint32_t *words, uint8_t *bytes, int W, int Ww, int rows, bool il, hipStream_t s);
+hipError_t launch_convert_layout(uint32_t *words, int64_t nwords, bool to_il, hipStream_t s);
 hipError_t launch_fill_random(uint32_t *words, int W, int Ww, int rows, int64_t row0, uint64_t seed,
                               hipStream_t s);
 hipError_t launch_popcount(const uint32_t *words, int64_t nwords, unsigned long long *out, hipStream_t s);
-hipError_t launch_hash(const uint32_t *words, int64_t nwords, int64_t word0, unsigned long long *out,
+hipError_t launch_hash(const uint32_t *words, int64_t nwords, int64_t word0, unsigned long long *out, bool il,
                        hipStream_t s);
 
 // Row-major compaction of set bits of (a ^ b) (b nullable -> a alone) into
@@ -92,6 +104,7 @@ hipError_t launch_compact_count(const uint32_t *a, const uint32_t *b, int64_t nw
                                 hipStream_t s);
 hipError_t launch_compact_scan(unsigned long long *blk, int64_t nblk, unsigned long long *total, hipStream_t s);
 hipError_t launch_compact_scatter(const uint32_t *a, const uint32_t *b, int64_t nwords, int Ww,
-                                  int64_t row0, const unsigned long long *blk_off, int32_t *xy, hipStream_t s);
+                                  int64_t row0, const unsigned long long *blk_off, int32_t *xy, bool il,
+                                  hipStream_t s);
 
 }  // namespace golk

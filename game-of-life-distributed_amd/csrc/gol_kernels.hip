@@ -82,6 +82,66 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 }
 
 // ---------------------------------------------------------------------------
+// Interleaved pair layout (boards run with two words per lane, W % 64 == 0).
+// A row's canonical words (2c, 2c+1) hold cells 64c .. 64c+63 in order; the
+// interleaved pair holds the even cells 64c+2k in bit k of word 2c and the
+// odd cells 64c+2k+1 in bit k of word 2c+1.  Rows stay rows, so halo rows,
+// strips and popcounts are layout-agnostic; only cell positions change.
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint32_t unshuffle32(uint32_t x) {  // even bits -> low half, odd -> high
+    uint32_t t;
+    t = (x ^ (x >> 1)) & 0x22222222u; x ^= t ^ (t << 1);
+    t = (x ^ (x >> 2)) & 0x0C0C0C0Cu; x ^= t ^ (t << 2);
+    t = (x ^ (x >> 4)) & 0x00F000F0u; x ^= t ^ (t << 4);
+    t = (x ^ (x >> 8)) & 0x0000FF00u; x ^= t ^ (t << 8);
+    return x;
+}
+__host__ __device__ __forceinline__ uint32_t shuffle32(uint32_t x) {  // inverse of unshuffle32
+    uint32_t t;
+    t = (x ^ (x >> 8)) & 0x0000FF00u; x ^= t ^ (t << 8);
+    t = (x ^ (x >> 4)) & 0x00F000F0u; x ^= t ^ (t << 4);
+    t = (x ^ (x >> 2)) & 0x0C0C0C0Cu; x ^= t ^ (t << 2);
+    t = (x ^ (x >> 1)) & 0x22222222u; x ^= t ^ (t << 1);
+    return x;
+}
+__host__ __device__ __forceinline__ void il_encode(uint32_t a, uint32_t b, uint32_t &e, uint32_t &o) {
+    const uint32_t ua = unshuffle32(a), ub = unshuffle32(b);
+    e = (ua & 0xFFFFu) | (ub << 16);
+    o = (ua >> 16) | (ub & 0xFFFF0000u);
+}
+__host__ __device__ __forceinline__ void il_decode(uint32_t e, uint32_t o, uint32_t &a, uint32_t &b) {
+    a = shuffle32((e & 0xFFFFu) | (o << 16));
+    b = shuffle32((e >> 16) | (o & 0xFFFF0000u));
+}
+// Canonical word i of a board stored in layout `il`.
+__device__ __forceinline__ uint32_t canon_word(const uint32_t *w, int64_t i, bool il) {
+    if (!il) return w[i];
+    uint32_t a, b;
+    il_decode(w[i & ~(int64_t)1], w[i | 1], a, b);
+    return (i & 1) ? b : a;
+}
+
+__global__ __launch_bounds__(256) void convert_layout_kernel(uint32_t *__restrict__ w, int64_t npairs, int to_il) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npairs) return;
+    uint2 v = reinterpret_cast<uint2 *>(w)[i];
+    uint32_t p, q;
+    if (to_il)
+        il_encode(v.x, v.y, p, q);
+    else
+        il_decode(v.x, v.y, p, q);
+    reinterpret_cast<uint2 *>(w)[i] = make_uint2(p, q);
+}
+
+hipError_t launch_convert_layout(uint32_t *words, int64_t nwords, bool to_il, hipStream_t s) {
+    const int64_t np = nwords / 2;
+    if (np == 0) return hipSuccess;
+    hipLaunchKernelGGL(convert_layout_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, words, np,
+                       to_il ? 1 : 0);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // K1: temporal-blocked bit-sliced step.
 //
 // One wavefront = one tile of 64 lanes x WPL consecutive words of a row band
@@ -111,17 +171,31 @@ __device__ __forceinline__ void stage(int t, Lanes<WPL> &x, uint32_t (&h0)[3][D]
     constexpr int N = R;            // slot of the row entering now
     constexpr int C = (R + 2) % 3;  // previous row (the one we emit)
     constexpr int P = (R + 1) % 3;  // the row before it
-    const uint32_t l = from_left_lane(x.w[WPL - 1]);  // left lane's last word
-    const uint32_t r = from_right_lane(x.w[0]);       // right lane's first word
+    // Horizontal 3-cell sums.  WPL == 1: the lane's word plus one edge bit
+    // from each adjacent lane (alignbit).  WPL == 2 uses the interleaved pair
+    // layout (see il_encode): w0 holds the even cells 2k and w1 the odd cells
+    // 2k+1 of the lane's 64-cell chunk, so the west neighbour of an odd cell
+    // and the east neighbour of an even cell are the other word as is; only
+    // one word per side needs a one-bit funnel shift with the edge lane's bit.
+    uint32_t west[WPL], east[WPL];
+    if constexpr (WPL == 1) {
+        const uint32_t l = from_left_lane(x.w[0]);
+        const uint32_t r = from_right_lane(x.w[0]);
+        west[0] = __builtin_amdgcn_alignbit(x.w[0], l, 31);  // bit b = cell b-1
+        east[0] = __builtin_amdgcn_alignbit(r, x.w[0], 1);   // bit b = cell b+1
+    } else {
+        const uint32_t l1 = from_left_lane(x.w[1]);   // left chunk's odd cells (bit 31 = its cell 63)
+        const uint32_t r0 = from_right_lane(x.w[0]);  // right chunk's even cells (bit 0 = its cell 0)
+        west[0] = __builtin_amdgcn_alignbit(x.w[1], l1, 31);  // cell 2k-1
+        east[0] = x.w[1];                                     // cell 2k+1
+        west[1] = x.w[0];                                     // cell 2k
+        east[1] = __builtin_amdgcn_alignbit(r0, x.w[0], 1);   // cell 2k+2
+    }
     uint32_t nx[WPL];
 #pragma unroll
     for (int k = 0; k < WPL; ++k) {
-        const uint32_t lo = k == 0 ? l : x.w[k - 1];
-        const uint32_t hi = k == WPL - 1 ? r : x.w[k + 1];
-        const uint32_t west = __builtin_amdgcn_alignbit(x.w[k], lo, 31);  // bit b = cell b-1
-        const uint32_t east = __builtin_amdgcn_alignbit(hi, x.w[k], 1);   // bit b = cell b+1
-        h0[N][t][k] = bop<kXor3>(west, x.w[k], east);
-        h1[N][t][k] = bop<kMaj>(west, x.w[k], east);
+        h0[N][t][k] = bop<kXor3>(west[k], x.w[k], east[k]);
+        h1[N][t][k] = bop<kMaj>(west[k], x.w[k], east[k]);
         const uint32_t u0 = bop<kXor3>(h0[P][t][k], h0[C][t][k], h0[N][t][k]);
         const uint32_t u1 = bop<kMaj>(h0[P][t][k], h0[C][t][k], h0[N][t][k]);
         const uint32_t v0 = bop<kXor3>(h1[P][t][k], h1[C][t][k], h1[N][t][k]);
@@ -166,7 +240,10 @@ __device__ __forceinline__ Lanes<WPL> vmov(const Lanes<WPL> &v) {
 // One wavefront streams output rows [r0, r0 + rows_here) of the tile whose
 // first stored word is t0, D turns ahead; returns the popcount of its stored
 // output words.  Shared by the per-launch and the persistent kernel.
-template <int D, bool SKIP, int WPL>
+// WT: write the output rows through to memory (sc1 stores, the line leaves the
+// XCD's L2) so a persistent kernel's per-super-step agent release has no
+// dirty L2 lines to write back.
+template <int D, bool SKIP, int WPL, bool WT = false>
 __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int rows_here, int t0) {
     const int lane = threadIdx.x & 63;
     const int Ww = a.Ww;
@@ -208,10 +285,17 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
         uint32_t *p = ok ? dst_row0 + (ptrdiff_t)out_idx * Ww : dummy;
         uint32_t pc = 0;
         if constexpr (WPL == 1) {
-            *p = y.w[0];
+            if constexpr (WT)
+                __hip_atomic_store(p, y.w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                *p = y.w[0];
             pc = __builtin_popcount(y.w[0]);
         } else {
-            *reinterpret_cast<uint2 *>(p) = make_uint2(y.w[0], y.w[1]);
+            if constexpr (WT)
+                __hip_atomic_store(reinterpret_cast<uint64_t *>(p), (uint64_t)y.w[0] | ((uint64_t)y.w[1] << 32),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                *reinterpret_cast<uint2 *>(p) = make_uint2(y.w[0], y.w[1]);
             pc = __builtin_popcount(y.w[0]) + __builtin_popcount(y.w[1]);
         }
         cnt += ok ? pc : 0u;
@@ -396,6 +480,218 @@ __device__ __forceinline__ uint32_t stream_band_diag(const StepArgs &a, int r0, 
     return cnt;
 }
 
+// push_group over stages [A0, A1) with per-stage hooks: pre(t, u, x) may
+// replace row u's input to stage t, post(t, u, x) sees stage t's output.
+template <int D, int A0, int A1, int WPL, typename Pre, typename Post>
+__device__ __forceinline__ void push_group_h(Lanes<WPL> &x0, Lanes<WPL> &x1, Lanes<WPL> &x2,
+                                             uint32_t (&h0)[3][D][WPL], uint32_t (&h1)[3][D][WPL],
+                                             uint32_t (&cc)[3][D][WPL], Pre &&pre, Post &&post) {
+#pragma unroll
+    for (int s = A0; s < A1 + 2; ++s) {
+        if (s < A1) {
+            pre(s, 0, x0);
+            stage<D, 0, WPL>(s, x0, h0, h1, cc);
+            post(s, 0, x0);
+        }
+        if (s - 1 >= A0 && s - 1 < A1) {
+            pre(s - 1, 1, x1);
+            stage<D, 1, WPL>(s - 1, x1, h0, h1, cc);
+            post(s - 1, 1, x1);
+        }
+        if (s - 2 >= A0 && s - 2 < A1) {
+            pre(s - 2, 2, x2);
+            stage<D, 2, WPL>(s - 2, x2, h0, h1, cc);
+            post(s - 2, 2, x2);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K1n: band without the vertical halo (persistent, torus).
+//
+// A K1p band recomputes D halo rows above and below itself every super-step
+// (the pipeline fill, ~1.25 D + D/2 rows of D stages for S rows of output).
+// Here a band streams its own rows r0 .. r0+S+1 only and lets the output
+// drift down by one row per stage: stage t emits rows r0+t+1 .. r0+S+t, so
+// the top needs nothing from above.  At the bottom, stage t needs two rows of
+// generation t below the band, which are exactly the first two outputs of
+// stage t-1 of the band below: every band publishes those 2(D-1) rows in LDS
+// during its first 2D input rows, and the band above picks them up when its
+// stream reaches row S (S >= 2D + 3, so a band's exports are complete before
+// it needs imports; there is no cycle inside a workgroup).  The bottom band
+// of a workgroup has no band below in LDS and runs the classic trapezoid
+// bottom (2D extra input rows).  After D stages the band's output is rows
+// r0+D .. r0+D+S-1 of generation D: bands stay put, each super-step's output
+// is written D rows lower, and every row is still written exactly once.
+// Work per band ~ D (S + 2) stage-rows instead of ~ D (S + 1.75 D).
+// ---------------------------------------------------------------------------
+template <int D, int WPL>
+__device__ __forceinline__ uint32_t stream_band_n(const StepArgs &a, int r0, int rows_here, int t0,
+                                                  uint32_t *ex_mine, const uint32_t *ex_below, uint32_t *ex_dummy,
+                                                  volatile int *flag_mine, volatile int *flag_below, int flag_val,
+                                                  bool count, unsigned *error, long long timeout_ticks) {
+    constexpr int ROW = 64 * WPL;
+    const int lane = threadIdx.x & 63;
+    const int Ww = a.Ww;
+    int col = (t0 + WPL * (lane - 1)) % Ww;
+    if (col < 0) col += Ww;
+    const bool keep = lane >= 1 && lane <= kTileValid && (t0 + WPL * (lane - 1)) < Ww;
+    const bool imports = ex_below != nullptr;
+    const int G = (rows_here + 2 * D + 2) / 3;
+
+    int r = r0 + a.in.off;  // no halo above: the stream starts at the band's first row
+    const int wrap = a.in.wrap > 0 ? a.in.wrap : INT_MAX;
+    if (a.in.wrap > 0) {
+        r %= a.in.wrap;
+        if (r < 0) r += a.in.wrap;
+    }
+    const uint32_t *__restrict__ src = a.src + col;
+    auto load_next = [&]() -> Lanes<WPL> {
+        const int pr = a.in.base + min(r, a.in.rmax);
+        Lanes<WPL> v;
+        if constexpr (WPL == 1) {
+            v.w[0] = src[(size_t)pr * Ww];
+        } else {
+            const uint2 q = *reinterpret_cast<const uint2 *>(src + (size_t)pr * Ww);
+            v.w[0] = q.x;
+            v.w[1] = q.y;
+        }
+        r = (r + 1 == wrap) ? 0 : r + 1;
+        return v;
+    };
+    uint32_t *const dummy = a.dst + col;
+    uint32_t cnt = 0;
+    auto emit = [&](const Lanes<WPL> &y, int oi) {  // output index oi -> row r0 + D + oi (torus)
+        const bool ok = keep && (unsigned)oi < (unsigned)rows_here;
+        int orow = r0 + D + oi;
+        if (orow >= a.rows_out) orow -= a.rows_out;
+        uint32_t *q = ok ? a.dst + (size_t)(a.dst_base + orow) * Ww + col : dummy;
+        uint32_t pc = 0;
+        if constexpr (WPL == 1) {
+            *q = y.w[0];
+            pc = __builtin_popcount(y.w[0]);
+        } else {
+            *reinterpret_cast<uint2 *>(q) = make_uint2(y.w[0], y.w[1]);
+            pc = __builtin_popcount(y.w[0]) + __builtin_popcount(y.w[1]);
+        }
+        cnt += (ok && count) ? pc : 0u;
+    };
+    // LDS rows are planar (word k of all 64 lanes contiguous).  Exports go
+    // through ds_write_addtid_b32 (address = M0 + 4 * lane): the slot base is
+    // wave-uniform, so no per-stage address VGPRs stay live in the fill.
+    auto lds_put = [&](uint32_t *row, const Lanes<WPL> &y) {
+#pragma unroll
+        for (int k = 0; k < WPL; ++k) {
+            const uint32_t base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)(row + 64 * k);
+            uint32_t saved;
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tds_write_addtid_b32 %2\n\ts_mov_b32 m0, %0"
+                         : "=&s"(saved)
+                         : "s"(base), "v"(y.w[k])
+                         : "memory");
+        }
+    };
+    auto lds_get = [&](const uint32_t *row) -> Lanes<WPL> {
+        Lanes<WPL> v;
+#pragma unroll
+        for (int k = 0; k < WPL; ++k) v.w[k] = row[64 * k + lane];
+        return v;
+    };
+
+    uint32_t h0[3][D][WPL], h1[3][D][WPL], cc[3][D][WPL];
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int t = 0; t < D; ++t)
+#pragma unroll
+            for (int k = 0; k < WPL; ++k) h0[s][t][k] = h1[s][t][k] = cc[s][t][k] = 0u;
+
+    Lanes<WPL> x0 = vmov(load_next()), x1 = vmov(load_next()), x2 = vmov(load_next());
+    int q = 0;  // group: input tokens 3q .. 3q+2 (token m = row r0 + m)
+    auto no_pre = [](int, int, Lanes<WPL> &) {};
+    auto no_post = [](int, int, const Lanes<WPL> &) {};
+    // exports: stage t's first two valid outputs (tokens 2t+2, 2t+3: rows r0+t+1, r0+t+2)
+    auto export_post = [&](int t, int u, const Lanes<WPL> &y) {
+        if (t <= D - 2) {
+            const int idx = 3 * q + u - 2 * t - 2;
+            uint32_t *row = (idx == 0 || idx == 1) ? ex_mine + (2 * t + idx) * ROW : ex_dummy;
+            lds_put(row, y);
+        }
+    };
+    auto body = [&](auto a0_tag, auto a1_tag, auto pre, auto post, const Lanes<WPL> *imp) {
+        constexpr int A0 = decltype(a0_tag)::value;
+        constexpr int A1 = decltype(a1_tag)::value;
+        const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
+        __builtin_amdgcn_sched_barrier(0);
+        Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
+        push_group_h<D, A0, A1, WPL>(y0, y1, y2, h0, h1, cc, pre, post);
+        if constexpr (A1 == D) {
+            const int oi = 3 * q - 2 * D;
+            emit(y0, oi);
+            emit(y1, oi + 1);
+            emit(y2, oi + 2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        x0 = vmov(n0);
+        x1 = vmov(n1);
+        x2 = vmov(n2);
+        ++q;
+        (void)imp;
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using ID = std::integral_constant<int, D>;
+    // fill (stage t idle before token 2t) with exports
+    while ((3 * q + 2) / 2 + 1 <= D / 4) body(I0(), std::integral_constant<int, D / 4>(), no_pre, export_post, nullptr);
+    while ((3 * q + 2) / 2 + 1 <= D / 2) body(I0(), std::integral_constant<int, D / 2>(), no_pre, export_post, nullptr);
+    while ((3 * q + 2) / 2 + 1 <= 3 * D / 4)
+        body(I0(), std::integral_constant<int, 3 * D / 4>(), no_pre, export_post, nullptr);
+    while (3 * q < 2 * D) body(I0(), ID(), no_pre, export_post, nullptr);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) *flag_mine = flag_val;
+    if (!imports) {
+        while (q < G) body(I0(), ID(), no_pre, no_post, nullptr);
+        return cnt;
+    }
+    while (3 * q + 2 < rows_here) body(I0(), ID(), no_pre, no_post, nullptr);
+    // imports from the band below (published in LDS during its first 2D rows)
+    {
+        const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
+        while (*flag_below < flag_val) {
+            if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > timeout_ticks) {
+                if (lane == 0) atomicOr(error, 2u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    // drain: token m >= rows_here feeds stage t = (m - rows_here) / 2 with import
+    // row m - rows_here - 2; stages t with 2t + rows_here + 2 <= 3q are done
+    Lanes<WPL> imp[3];
+    auto load_imports = [&]() {
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int i = 3 * q + u - rows_here - 2;
+            imp[u] = lds_get((i >= 0 && i < 2 * (D - 1)) ? ex_below + i * ROW : ex_dummy);
+        }
+    };
+    auto import_pre = [&](int t, int u, Lanes<WPL> &x) {
+        if (t >= 1) {
+            const int rel = 3 * q + u - rows_here;
+            const bool take = rel >= 2 && (rel >> 1) == t;
+#pragma unroll
+            for (int k = 0; k < WPL; ++k) x.w[k] = take ? imp[u].w[k] : x.w[k];
+        }
+    };
+    auto drain = [&](auto a0_tag) {
+        load_imports();
+        body(a0_tag, ID(), import_pre, no_post, imp);
+    };
+    while (q < G && 3 * q < D / 2 + rows_here) drain(I0());
+    while (q < G && 3 * q < D + rows_here) drain(std::integral_constant<int, D / 4>());
+    while (q < G && 3 * q < 3 * D / 2 + rows_here) drain(std::integral_constant<int, D / 2>());
+    while (q < G) drain(std::integral_constant<int, 3 * D / 4>());
+    return cnt;
+}
+
 __host__ __device__ constexpr int tile_words(int wpl) { return kTileValid * wpl; }
 
 template <int D, bool SKIP, int WPL>
@@ -432,7 +728,7 @@ __global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int persist_waves(int depth, int wpl) { return depth * wpl <= 16 ? 16 : 8; }
 
-template <int D, int WPL, int NW, bool DIAG>
+template <int D, int WPL, int NW, bool DIAG, bool WT = false>
 __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -455,7 +751,10 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
     __syncthreads();
 
     uint32_t cnt = 0;
+    long long tr_wait = 0, tr_band = 0, tr_max = 0;
+    const long long tr_t0 = (long long)__builtin_amdgcn_s_memrealtime();
     for (int j = 0; j < p.J; ++j) {
+        const long long tr_w0 = (long long)__builtin_amdgcn_s_memrealtime();
         if (j > 0) {
             if (w == 0) {
                 const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
@@ -478,6 +777,8 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
             __syncthreads();
             if (s_abort) return;  // uniform over the workgroup
         }
+        const long long tr_b0 = (long long)__builtin_amdgcn_s_memrealtime();
+        tr_wait += tr_b0 - tr_w0;
         StepArgs a = p.base;
         const bool odd = ((p.first + j) & 1) != 0;
         a.src = odd ? p.buf1 : p.buf0;
@@ -485,13 +786,32 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
         if constexpr (DIAG)
             cnt = rows_here > 0 ? stream_band_diag<D, 1, WPL>(a, r0, rows_here, tile * tile_words(WPL)) : 0u;
         else
-            cnt = rows_here > 0 ? stream_band<D, true, WPL>(a, r0, rows_here, tile * tile_words(WPL)) : 0u;
+            cnt = rows_here > 0 ? stream_band<D, true, WPL, WT>(a, r0, rows_here, tile * tile_words(WPL)) : 0u;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        {
+            const long long tr_e = (long long)__builtin_amdgcn_s_memrealtime();
+            const long long d = tr_e - tr_b0;
+            tr_band += d;
+            tr_max = d > tr_max ? d : tr_max;
+            if (p.trace && j == p.J / 2 && lane == 0) {  // per-wave (start, end) of one super-step
+                p.trace[8 + 2 * (b * 64 + w)] = (unsigned long long)tr_b0;
+                p.trace[8 + 2 * (b * 64 + w) + 1] = (unsigned long long)tr_e;
+            }
+        }
         __syncthreads();
         if (threadIdx.x == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(&p.progress[b], (unsigned)(j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (p.trace && lane == 0) {  // diagnostics: per-wave band time, workgroup wait time
+        atomicAdd(&p.trace[0], (unsigned long long)tr_band);
+        atomicMax(&p.trace[1], (unsigned long long)tr_max);
+        if (w == 0) {
+            atomicAdd(&p.trace[2], (unsigned long long)tr_wait);
+            atomicAdd(&p.trace[3], (unsigned long long)((long long)__builtin_amdgcn_s_memrealtime() - tr_t0));
+            atomicAdd(&p.trace[4], 1ull);
         }
     }
     if (p.base.alive) {
@@ -728,6 +1048,113 @@ __global__ __launch_bounds__(NWS * P * 64) void gol_pipe_kernel(PersistArgs p) {
     }
 }
 
+template <int D, int WPL, int NW>
+__global__ __launch_bounds__(NW * 64) void gol_k1n_kernel(PersistArgs p) {
+    constexpr int ROW = 64 * WPL;
+    __shared__ uint32_t ex[NW][2 * (D - 1) * ROW];
+    __shared__ uint32_t ex_dummy[ROW];
+    __shared__ int flags[NW];
+    __shared__ int s_abort;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = blockIdx.x;
+    const int wx = b % p.cols, wy = b / p.cols;
+    const int tile = wx;                  // one tile column per workgroup
+    // NW stacked bands: NW-1 importing bands of S rows, then the workgroup's
+    // bottom band of Sb rows (it pays the trapezoid bottom, ~D rows more work
+    // per stage, so it is that much shorter to keep the bands balanced)
+    const int wg_rows = (NW - 1) * p.S + p.Sb;
+    auto band_r0 = [&](int k) { return wy * wg_rows + k * p.S; };
+    auto band_rows = [&](int k) {
+        const int rr = band_r0(k);
+        const int want = k < NW - 1 ? p.S : p.Sb;
+        return (tile < p.tiles_x && rr < p.base.rows_out) ? min(want, p.base.rows_out - rr) : 0;
+    };
+    const int r0 = band_r0(w);
+    const int rows_here = band_rows(w);
+    const bool imports = w + 1 < NW && rows_here == p.S && band_rows(w + 1) > 0;
+
+    int nb = b;
+    if (lane < 9) {
+        const int ny = (wy + lane / 3 - 1 + p.wg_y) % p.wg_y;
+        const int nx = (wx + lane % 3 - 1 + p.cols) % p.cols;
+        nb = ny * p.cols + nx;
+    }
+    if (lane == 0) flags[w] = 0;
+    if (threadIdx.x == 0) s_abort = 0;
+    __syncthreads();
+
+    uint32_t cnt = 0;
+    long long tr_wait = 0, tr_band = 0, tr_max = 0;
+    const long long tr_t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    for (int j = 0; j < p.J; ++j) {
+        const long long tr_w0 = (long long)__builtin_amdgcn_s_memrealtime();
+        if (j > 0) {
+            if (w == 0) {
+                const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
+                for (;;) {
+                    const unsigned v = __hip_atomic_load(&p.progress[nb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (__all(v >= (unsigned)j)) break;
+                    const unsigned err = __hip_atomic_load(p.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (err || (long long)__builtin_amdgcn_s_memrealtime() - t_start > p.timeout_ticks) {
+                        if (lane == 0) {
+                            atomicOr(p.error, 1u);
+                            s_abort = 1;
+                        }
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if (lane == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();
+            if (s_abort) return;  // uniform over the workgroup
+        }
+        const long long tr_b0 = (long long)__builtin_amdgcn_s_memrealtime();
+        tr_wait += tr_b0 - tr_w0;
+        StepArgs a = p.base;
+        const bool odd = ((p.first + j) & 1) != 0;
+        a.src = odd ? p.buf1 : p.buf0;
+        a.dst = odd ? p.buf0 : p.buf1;
+        cnt = rows_here > 0 ? stream_band_n<D, WPL>(a, r0, rows_here, tile * tile_words(WPL), &ex[w][0],
+                                                     imports ? &ex[w + 1][0] : nullptr, ex_dummy, &flags[w],
+                                                     &flags[imports ? w + 1 : w], j + 1, j == p.J - 1, p.error,
+                                                     p.timeout_ticks)
+                            : 0u;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        {
+            const long long tr_e = (long long)__builtin_amdgcn_s_memrealtime();
+            const long long d = tr_e - tr_b0;
+            tr_band += d;
+            tr_max = d > tr_max ? d : tr_max;
+            if (p.trace && j == p.J / 2 && lane == 0) {  // per-wave (start, end) of one super-step
+                p.trace[8 + 2 * (b * 64 + w)] = (unsigned long long)tr_b0;
+                p.trace[8 + 2 * (b * 64 + w) + 1] = (unsigned long long)tr_e;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&p.progress[b], (unsigned)(j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (p.trace && lane == 0) {  // diagnostics: per-wave band time, workgroup wait time
+        atomicAdd(&p.trace[0], (unsigned long long)tr_band);
+        atomicMax(&p.trace[1], (unsigned long long)tr_max);
+        if (w == 0) {
+            atomicAdd(&p.trace[2], (unsigned long long)tr_wait);
+            atomicAdd(&p.trace[3], (unsigned long long)((long long)__builtin_amdgcn_s_memrealtime() - tr_t0));
+            atomicAdd(&p.trace[4], 1ull);
+        }
+    }
+    if (p.base.alive) {
+        const uint32_t tot = wave_sum_u32(cnt);
+        if (lane == 0 && tot) atomicAdd(p.base.alive, (unsigned long long)tot);
+    }
+}
+
 // ---- host-side dispatch over (depth, fill skip, words per lane) ----------
 // WPL = 2 is instantiated up to depth 16 (depth 32 would exceed 256 VGPRs).
 template <typename F>
@@ -792,16 +1219,16 @@ int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_sk
 
 // nw = waves per workgroup (one workgroup per CU): 4, 8 or 16; 0 = default.
 template <typename F>
-static hipError_t dispatch_persist(int depth, int wpl, int nw, bool diag, F &&f) {
+static hipError_t dispatch_persist(int depth, int wpl, int nw, bool diag, bool wt, F &&f) {
     if (nw == 0) nw = persist_waves(depth, wpl);
-#define GOL_PCASE(D, WP, NW) \
-    if (!diag && depth == D && wpl == WP && nw == NW) return f(gol_persist_kernel<D, WP, NW, false>, NW);
+#define GOL_PCASE(D, WP, NW)                                                                           \
+    if (!diag && depth == D && wpl == WP && nw == NW)                                                  \
+        return wt ? f(gol_persist_kernel<D, WP, NW, false, true>, NW) : f(gol_persist_kernel<D, WP, NW, false, false>, NW);
 #define GOL_DCASE(D, WP, NW) \
     if (diag && depth == D && wpl == WP && nw == NW) return f(gol_persist_kernel<D, WP, NW, true>, NW);
     GOL_PCASE(4, 1, 16) GOL_PCASE(8, 1, 16) GOL_PCASE(16, 1, 16) GOL_PCASE(32, 1, 8) GOL_PCASE(4, 2, 16)
     GOL_PCASE(8, 2, 16) GOL_PCASE(16, 2, 8)
-    GOL_PCASE(4, 1, 4) GOL_PCASE(8, 1, 4) GOL_PCASE(16, 1, 4) GOL_PCASE(8, 1, 8) GOL_PCASE(16, 1, 8)
-    GOL_PCASE(4, 2, 4) GOL_PCASE(8, 2, 4) GOL_PCASE(16, 2, 4) GOL_PCASE(4, 2, 8) GOL_PCASE(8, 2, 8)
+    GOL_PCASE(8, 1, 8) GOL_PCASE(16, 1, 8) GOL_PCASE(8, 2, 8)
     GOL_DCASE(8, 1, 4) GOL_DCASE(8, 1, 8) GOL_DCASE(16, 1, 4) GOL_DCASE(16, 1, 8)
     GOL_DCASE(32, 1, 4) GOL_DCASE(8, 2, 4) GOL_DCASE(8, 2, 8) GOL_DCASE(16, 2, 4)
 #undef GOL_PCASE
@@ -813,7 +1240,7 @@ int persist_waves_for(int depth, int wpl) { return persist_waves(depth, wpl); }
 
 int persist_blocks_per_cu(int depth, int wpl, int nw, bool diag) {
     int b = 0;
-    hipError_t e = dispatch_persist(depth, wpl, nw, diag, [&](auto kern, int n) {
+    hipError_t e = dispatch_persist(depth, wpl, nw, diag, false, [&](auto kern, int n) {
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 64 * n, 0);
     });
     return e == hipSuccess ? b : 0;
@@ -881,8 +1308,55 @@ hipError_t launch_pipe(const PersistArgs &p, int depth, int wpl, int nws, int gt
     });
 }
 
-hipError_t launch_persist(const PersistArgs &p, int depth, int wpl, bool diag, hipStream_t s) {
-    return dispatch_persist(depth, wpl, p.nw, diag, [&](auto kern, int nw) {
+template <typename F>
+static hipError_t dispatch_k1n(int depth, int wpl, int nw, F &&f) {
+#define GOL_NCASE(D, WP, NW) \
+    if (depth == D && wpl == WP && nw == NW) return f(gol_k1n_kernel<D, WP, NW>, NW);
+    GOL_NCASE(8, 1, 8) GOL_NCASE(16, 1, 8) GOL_NCASE(16, 1, 16) GOL_NCASE(32, 1, 8) GOL_NCASE(8, 2, 8)
+    GOL_NCASE(16, 2, 8) GOL_NCASE(8, 1, 16) GOL_NCASE(8, 2, 16)
+#undef GOL_NCASE
+    return hipErrorInvalidValue;
+}
+
+int k1n_blocks_per_cu(int depth, int wpl, int nw) {
+    int b = 0;
+    hipError_t e = dispatch_k1n(depth, wpl, nw, [&](auto kern, int n) {
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 64 * n, 0);
+    });
+    return e == hipSuccess ? b : 0;
+}
+
+bool plan_k1n(int Ww, int rows, int depth, int cus, int wpl, int nw, PersistArgs *p) {
+    const int tiles_x = tb_tiles(Ww, wpl);
+    const int cols = tiles_x;  // one tile per workgroup, nw stacked bands
+    const int wg_y = std::min(cus / cols, rows / (nw * (2 * depth + 3)));
+    if (wg_y < 1 || nw < 2) return false;
+    // workgroup rows R = (nw - 1) S + Sb with Sb = S - depth + 1 (balanced bottom band)
+    const int R = (rows + wg_y - 1) / wg_y;
+    const int S = (R + depth - 1 + nw - 1) / nw;
+    const int Sb = std::max(1, S - depth + 1);
+    if (S < 2 * depth + 3) return false;
+    if ((long)((nw - 1) * S + Sb) * wg_y < rows) return false;
+    p->wg_tx = 1;
+    p->wg_sy = nw;
+    p->cols = cols;
+    p->wg_y = wg_y;
+    p->S = S;
+    p->Sb = Sb;
+    p->tiles_x = tiles_x;
+    p->nw = nw;
+    return true;
+}
+
+hipError_t launch_k1n(const PersistArgs &p, int depth, int wpl, hipStream_t s) {
+    return dispatch_k1n(depth, wpl, p.nw, [&](auto kern, int nw) {
+        hipLaunchKernelGGL(kern, dim3(p.cols * p.wg_y), dim3(64 * nw), 0, s, p);
+        return hipGetLastError();
+    });
+}
+
+hipError_t launch_persist(const PersistArgs &p, int depth, int wpl, bool diag, bool wt, hipStream_t s) {
+    return dispatch_persist(depth, wpl, p.nw, diag, wt, [&](auto kern, int nw) {
         hipLaunchKernelGGL(kern, dim3(p.cols * p.wg_y), dim3(64 * nw), 0, s, p);
         return hipGetLastError();
     });
@@ -968,14 +1442,14 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t *__restrict__ b
 }
 
 __global__ __launch_bounds__(256) void unpack_kernel(const uint32_t *__restrict__ words, uint8_t *__restrict__ bytes,
-                                                      int W, int Ww, int rows) {
+                                                      int W, int Ww, int rows, bool il) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (int64_t)rows * Ww) return;
     const int row = (int)(idx / Ww);
     const int wc = (int)(idx - (int64_t)row * Ww);
     uint8_t *p = bytes + (size_t)row * W + (size_t)wc * 32;
     const int n = min(32, W - wc * 32);
-    const uint32_t w = words[idx];
+    const uint32_t w = canon_word(words, idx, il);
     if (n == 32 && (W & 15) == 0) {
         uint32_t d[8];
 #pragma unroll
@@ -1000,11 +1474,11 @@ hipError_t launch_pack(const uint8_t *bytes, uint32_t *words, int W, int Ww, int
     return hipGetLastError();
 }
 
-hipError_t launch_unpack(const uint32_t *words, uint8_t *bytes, int W, int Ww, int rows, hipStream_t s) {
+hipError_t launch_unpack(const uint32_t *words, uint8_t *bytes, int W, int Ww, int rows, bool il, hipStream_t s) {
     const int64_t n = (int64_t)rows * Ww;
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, words, bytes, W, Ww,
-                       rows);
+                       rows, il);
     return hipGetLastError();
 }
 
@@ -1055,20 +1529,20 @@ hipError_t launch_popcount(const uint32_t *words, int64_t nwords, unsigned long 
 }
 
 __global__ __launch_bounds__(256) void hash_kernel(const uint32_t *__restrict__ w, int64_t n, int64_t word0,
-                                                    unsigned long long *out) {
+                                                    unsigned long long *out, bool il) {
     unsigned long long h = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-        h += splitmix64(((uint64_t)(word0 + i) << 32) | (uint64_t)w[i]);
+        h += splitmix64(((uint64_t)(word0 + i) << 32) | (uint64_t)canon_word(w, i, il));
     h = wave_sum_u64(h);
     if ((threadIdx.x & 63) == 0) atomicAdd(out, h);
 }
 
-hipError_t launch_hash(const uint32_t *words, int64_t nwords, int64_t word0, unsigned long long *out,
+hipError_t launch_hash(const uint32_t *words, int64_t nwords, int64_t word0, unsigned long long *out, bool il,
                        hipStream_t s) {
     if (nwords == 0) return hipSuccess;
     const int64_t blocks = std::min<int64_t>((nwords + 255) / 256, 4096);
-    hipLaunchKernelGGL(hash_kernel, dim3((unsigned)blocks), dim3(256), 0, s, words, nwords, word0, out);
+    hipLaunchKernelGGL(hash_kernel, dim3((unsigned)blocks), dim3(256), 0, s, words, nwords, word0, out, il);
     return hipGetLastError();
 }
 
@@ -1086,6 +1560,12 @@ int64_t compact_blocks(int64_t nwords) { return (nwords + kBlkWords - 1) / kBlkW
 __device__ __forceinline__ uint32_t cword(const uint32_t *a, const uint32_t *b, int64_t i) {
     return b ? (a[i] ^ b[i]) : a[i];
 }
+// Canonical (row-major cell order) word i of a ^ b.  Per block and per
+// thread chunk (kWpt even) the set-bit count is the same in either layout.
+__device__ __forceinline__ uint32_t cword_canon(const uint32_t *a, const uint32_t *b, int64_t i, bool il) {
+    return b ? (canon_word(a, i, il) ^ canon_word(b, i, il)) : canon_word(a, i, il);
+}
+static_assert(kWpt % 2 == 0, "pairs must not straddle compaction chunks");
 
 __device__ uint32_t block_excl_scan(uint32_t v, uint32_t *total) {
     __shared__ uint32_t wsum[4];
@@ -1151,7 +1631,7 @@ __global__ __launch_bounds__(1024) void compact_scan_kernel(unsigned long long *
 __global__ __launch_bounds__(256) void compact_scatter_kernel(const uint32_t *__restrict__ a,
                                                                const uint32_t *__restrict__ b, int64_t n, int Ww,
                                                                int64_t row0, const unsigned long long *blk_off,
-                                                               int32_t *__restrict__ xy) {
+                                                               int32_t *__restrict__ xy, bool il) {
     const int64_t base = (int64_t)blockIdx.x * kBlkWords + (int64_t)threadIdx.x * kWpt;
     uint32_t c = 0;
     for (int k = 0; k < kWpt; ++k)
@@ -1161,7 +1641,7 @@ __global__ __launch_bounds__(256) void compact_scatter_kernel(const uint32_t *__
     for (int k = 0; k < kWpt; ++k) {
         const int64_t i = base + k;
         if (i >= n) break;
-        uint32_t m = cword(a, b, i);
+        uint32_t m = cword_canon(a, b, i, il);
         if (!m) continue;
         const int64_t row = i / Ww;
         const int wc = (int)(i - row * Ww);
@@ -1189,11 +1669,11 @@ hipError_t launch_compact_scan(unsigned long long *blk, int64_t nblk, unsigned l
 }
 
 hipError_t launch_compact_scatter(const uint32_t *a, const uint32_t *b, int64_t nwords, int Ww, int64_t row0,
-                                  const unsigned long long *blk_off, int32_t *xy, hipStream_t s) {
+                                  const unsigned long long *blk_off, int32_t *xy, bool il, hipStream_t s) {
     const int64_t nb = compact_blocks(nwords);
     if (nb == 0) return hipSuccess;
     hipLaunchKernelGGL(compact_scatter_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, b, nwords, Ww, row0, blk_off,
-                       xy);
+                       xy, il);
     return hipGetLastError();
 }
 

@@ -64,6 +64,8 @@ int fail(int code, const char *fmt, ...) {
     } while (0)
 
 constexpr int kDepths[] = {32, 16, 8, 4, 2, 1};
+// trace buffer: 8 totals + (start, end) per (workgroup < 1024, wave < 64)
+constexpr int64_t kTraceWords = 8 + 2 * 1024 * 64;
 
 }  // namespace
 
@@ -90,6 +92,9 @@ struct golhip {
     int persist_waves = 0;      // option "persist_waves": waves per workgroup (0: default)
     int stage_waves = 0;        // option "stage_waves": >= 2 selects K1s (waves per pipeline)
     int pipe_units = 0;         // option "pipe_units": K1s pipelines per workgroup (0: 16 / stage_waves)
+    unsigned long long *d_trace = nullptr;  // option "trace": persistent-kernel diagnostics
+    bool k1n = false;           // option "k1n": bands without the vertical halo (K1n)
+    bool persist_wt = false;    // option "persist_wt": write-through output stores in K1p
     bool diag = false;          // option "diag": diagonal stage schedule in K1p
     int pipe_groups = 1;        // option "pipe_groups": K1s 3-row groups per tick (1, 2, 4)
     unsigned *d_sync = nullptr; // persistent kernel: [0] error, [1..] progress per workgroup
@@ -98,6 +103,7 @@ struct golhip {
     int64_t persist_launches = 0;
     int auto_rpw[6] = {0, 0, 0, 0, 0, 0};  // cache per depth index
     bool loaded = false;
+    bool il = false;            // board words in the interleaved pair layout (wpl = 2 kernels)
     std::atomic<int64_t> turns{0};
 
     // side-channel scratch
@@ -202,6 +208,23 @@ int wpl_for(golhip_t h) {
     if (h->wpl_opt == 1 || h->wpl_opt == 2) return h->wpl_opt;
     const long w1 = (long)golk::tb_tiles(h->Ww, 1) * 64, w2 = (long)golk::tb_tiles(h->Ww, 2) * 128;
     return w2 <= w1 ? 2 : 1;
+}
+
+// The wpl = 2 step kernels run on the interleaved pair layout; every other
+// kernel reads canonical words (or is layout-agnostic: popcount, row halos).
+// Converts the current board in place when the wanted layout changes.
+int set_layout(golhip_t h, bool il) {
+    if (h->il == il) return GOLHIP_OK;
+    if (h->loaded) HIP_OR_FAIL(golk::launch_convert_layout(h->cur_rows(), h->local_words(), il, h->stream));
+    h->il = il;
+    return GOLHIP_OK;
+}
+bool want_il(golhip_t h) { return wpl_for(h) == 2; }
+// After canonical words were written into the current buffer.
+int loaded_canonical(golhip_t h) {
+    h->il = false;
+    h->loaded = true;
+    return set_layout(h, want_il(h));
 }
 
 // How many turns the next launch fuses.  In halo mode the `depth` halo rows
@@ -382,7 +405,13 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     const int64_t J = left / depth;
     if (J < 2) return 0;
     int nw = 0, units = 0;
-    if (nws >= 2) {
+    golk::PersistArgs p{};
+    const bool k1n = h->k1n && nws < 2 && !h->diag;
+    if (k1n) {
+        nw = h->persist_waves > 0 ? h->persist_waves : 8;
+        if (golk::k1n_blocks_per_cu(depth, wpl, nw) < 1) return 0;
+        if (!golk::plan_k1n(h->Ww, h->rows, depth, h->cu_count, wpl, nw, &p)) return 0;
+    } else if (nws >= 2) {
         units = h->pipe_units > 0 ? h->pipe_units : 16 / nws;
         if (depth % nws != 0 || golk::pipe_blocks_per_cu(depth, wpl, nws, units, h->pipe_groups) < 1) return 0;
         nw = nws * units;
@@ -391,9 +420,10 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
         if (golk::persist_blocks_per_cu(depth, wpl, nw, h->diag) < 1) return 0;
         units = nw;
     }
-    golk::PersistArgs p{};
-    if (!golk::plan_persist(h->Ww, h->rows, depth, h->cu_count, wpl, units, &p)) return 0;
-    p.nw = nw;
+    if (!k1n) {
+        if (!golk::plan_persist(h->Ww, h->rows, depth, h->cu_count, wpl, units, &p)) return 0;
+        p.nw = nw;
+    }
     if (!h->d_sync) {
         if (hipMalloc(&h->d_sync, (size_t)(h->cu_count + 2) * sizeof(unsigned)) != hipSuccess ||
             hipHostMalloc(&h->h_err, sizeof(unsigned), hipHostMallocDefault) != hipSuccess) {
@@ -416,6 +446,7 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     p.error = h->d_sync;
     p.progress = h->d_sync + 1;
     p.timeout_ticks = 100000000ll;  // 1 s at the 100 MHz s_memrealtime clock
+    p.trace = h->d_trace;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (e == hipSuccess && (h->flags & GOLHIP_FLAG_TIMING)) {
         e0 = take_event(h);
@@ -423,7 +454,9 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
         if (e0 && e1) e = hipEventRecord(e0, h->stream);
     }
     if (e == hipSuccess)
-        e = nws >= 2 ? golk::launch_pipe(p, depth, wpl, nws, h->pipe_groups, h->stream) : golk::launch_persist(p, depth, wpl, h->diag, h->stream);
+        e = k1n         ? golk::launch_k1n(p, depth, wpl, h->stream)
+            : nws >= 2  ? golk::launch_pipe(p, depth, wpl, nws, h->pipe_groups, h->stream)
+                        : golk::launch_persist(p, depth, wpl, h->diag, h->persist_wt, h->stream);
     if (e == hipSuccess && e1) {
         e = hipEventRecord(e1, h->stream);
         h->ev_pending.push_back({e0, e1, true});
@@ -467,7 +500,7 @@ int finish_compact(golhip_t h, const uint32_t *a, const uint32_t *b, int32_t *xy
     if (total == 0) return GOLHIP_OK;
     int rc = ensure_xy(h, (int64_t)total);
     if (rc) return rc;
-    HIP_OR_FAIL(golk::launch_compact_scatter(a, b, h->local_words(), h->Ww, h->row0, h->d_blk, h->d_xy, h->stream));
+    HIP_OR_FAIL(golk::launch_compact_scatter(a, b, h->local_words(), h->Ww, h->row0, h->d_blk, h->d_xy, h->il, h->stream));
     HIP_OR_FAIL(hipMemcpyAsync(xy, h->d_xy, total * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, h->stream));
     if (int rc_ = sync_stream(h)) return rc_;
     return GOLHIP_OK;
@@ -566,6 +599,7 @@ int golhip_destroy(golhip_t h) {
     HIP_RC(hipFree(h->d_xy));
     HIP_RC(hipFree(h->d_stage));
     HIP_RC(hipFree(h->d_sync));
+    HIP_RC(hipFree(h->d_trace));
     if (h->h_err) HIP_RC(hipHostFree(h->h_err));
     if (h->own_stream && h->stream) HIP_RC(hipStreamDestroy(h->stream));
     delete h;
@@ -630,6 +664,23 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
             return fail(GOLHIP_EINVAL, "stage_waves %lld not in {0,1,2,4,8}", (long long)value);
         h->stage_waves = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "trace")) {
+        if (value && !h->d_trace) {
+            if (hipMalloc(&h->d_trace, kTraceWords * sizeof(unsigned long long)) != hipSuccess)
+                return fail(GOLHIP_ENOMEM, "trace buffer");
+            if (hipMemset(h->d_trace, 0, kTraceWords * sizeof(unsigned long long)) != hipSuccess)
+                return fail(GOLHIP_EHIP, "trace buffer memset");
+        }
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "k1n")) {
+        h->k1n = value != 0;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "persist_wt")) {
+        h->persist_wt = value != 0;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "diag")) {
@@ -699,8 +750,8 @@ int golhip_load_bytes(golhip_t h, const uint8_t *cells) {
         HIP_OR_FAIL(hipMemcpyAsync(h->d_stage, cells + r * h->W, (size_t)(n * h->W), hipMemcpyHostToDevice, h->stream));
         HIP_OR_FAIL(golk::launch_pack(h->d_stage, h->cur_rows() + r * h->Ww, h->W, h->Ww, (int)n, h->stream));
     }
+    if (int rc = loaded_canonical(h)) return rc;
     if (int rc_ = sync_stream(h)) return rc_;
-    h->loaded = true;
     h->turns = 0;
     h->alive_turn = -1;
     h->flips_valid = false;
@@ -713,8 +764,8 @@ int golhip_load_bits(golhip_t h, const uint32_t *words) {
     std::lock_guard<std::mutex> g(h->mu);
     if (int rc = set_dev(h)) return rc;
     HIP_OR_FAIL(hipMemcpyAsync(h->cur_rows(), words, (size_t)h->local_words() * 4, hipMemcpyHostToDevice, h->stream));
+    if (int rc = loaded_canonical(h)) return rc;
     if (int rc_ = sync_stream(h)) return rc_;
-    h->loaded = true;
     h->turns = 0;
     h->alive_turn = -1;
     h->flips_valid = false;
@@ -726,8 +777,8 @@ int golhip_fill_random(golhip_t h, uint64_t seed) {
     std::lock_guard<std::mutex> g(h->mu);
     if (int rc = set_dev(h)) return rc;
     HIP_OR_FAIL(golk::launch_fill_random(h->cur_rows(), h->W, h->Ww, h->rows, h->row0, seed, h->stream));
+    if (int rc = loaded_canonical(h)) return rc;
     if (int rc_ = sync_stream(h)) return rc_;
-    h->loaded = true;
     h->turns = 0;
     h->alive_turn = -1;
     h->flips_valid = false;
@@ -741,6 +792,7 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     if (!h->loaded) return fail(GOLHIP_EINVAL, "no board loaded");
     if (h->nranks == 1 && !h->torus()) return fail(GOLHIP_EINVAL, "strip handle needs golhip_comm_init or golhip_group_step");
     if (int rc = set_dev(h)) return rc;
+    if (int rc = set_layout(h, want_il(h))) return rc;
     h->flips_valid = false;
     int64_t left = nturns;
     const int64_t tail = want_flips ? 1 : 0;
@@ -784,6 +836,8 @@ int golhip_group_step(golhip_t *hs, int32_t n, int64_t nturns) {
     for (int i = 0; i < n; ++i) {
         HIP_RC(hipSetDevice(hs[i]->device));
         HIP_RC(hipEventCreateWithFlags(&ready[i], hipEventDisableTiming));
+        if (!rc && want_il(hs[i]) != want_il(hs[0])) rc = fail(GOLHIP_EINVAL, "strip %d uses another word layout", i);
+        if (!rc) rc = set_layout(hs[i], want_il(hs[i]));
         hs[i]->flips_valid = false;
     }
     int64_t left = nturns;
@@ -910,7 +964,7 @@ int golhip_snapshot_bytes(golhip_t h, uint8_t *out) {
     if (int rc = ensure_stage(h, chunk * h->W)) return rc;
     for (int64_t r = 0; r < h->rows; r += chunk) {
         const int64_t n = std::min<int64_t>(chunk, h->rows - r);
-        HIP_OR_FAIL(golk::launch_unpack(h->cur_rows() + r * h->Ww, h->d_stage, h->W, h->Ww, (int)n, h->stream));
+        HIP_OR_FAIL(golk::launch_unpack(h->cur_rows() + r * h->Ww, h->d_stage, h->W, h->Ww, (int)n, h->il, h->stream));
         HIP_OR_FAIL(hipMemcpyAsync(out + r * h->W, h->d_stage, (size_t)(n * h->W), hipMemcpyDeviceToHost, h->stream));
     }
     if (int rc_ = sync_stream(h)) return rc_;
@@ -922,7 +976,10 @@ int golhip_snapshot_bits(golhip_t h, uint32_t *out) {
     if (!out) return fail(GOLHIP_EINVAL, "out is null");
     std::lock_guard<std::mutex> g(h->mu);
     if (int rc = set_dev(h)) return rc;
+    const bool il = h->il;
+    if (il) HIP_OR_FAIL(golk::launch_convert_layout(h->cur_rows(), h->local_words(), false, h->stream));
     HIP_OR_FAIL(hipMemcpyAsync(out, h->cur_rows(), (size_t)h->local_words() * 4, hipMemcpyDeviceToHost, h->stream));
+    if (il) HIP_OR_FAIL(golk::launch_convert_layout(h->cur_rows(), h->local_words(), true, h->stream));
     if (int rc_ = sync_stream(h)) return rc_;
     return GOLHIP_OK;
 }
@@ -933,7 +990,8 @@ int golhip_board_hash(golhip_t h, uint64_t *hash) {
     std::lock_guard<std::mutex> g(h->mu);
     if (int rc = set_dev(h)) return rc;
     HIP_OR_FAIL(hipMemsetAsync(h->d_scalars + 2, 0, sizeof(unsigned long long), h->stream));
-    HIP_OR_FAIL(golk::launch_hash(h->cur_rows(), h->local_words(), (int64_t)h->row0 * h->Ww, h->d_scalars + 2, h->stream));
+    HIP_OR_FAIL(golk::launch_hash(h->cur_rows(), h->local_words(), (int64_t)h->row0 * h->Ww, h->d_scalars + 2, h->il,
+                                  h->stream));
     HIP_OR_FAIL(hipMemcpyAsync(h->h_scalars + 2, h->d_scalars + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost,
                                h->stream));
     if (int rc_ = sync_stream(h)) return rc_;
@@ -962,6 +1020,29 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     out->tb_depth = h->tb_depth;
     out->rows_per_wave = rows_per_wave_for(h, next_depth(h, h->tb_depth, h->nranks > 1));
     out->kernel_variant = h->W % 32 == 0 ? 1 : 0;
+    return GOLHIP_OK;
+}
+
+int golhip_persist_trace_waves(golhip_t h, uint64_t *out, int64_t n) {
+    if (int rc = check(h)) return rc;
+    if (!out || n < 0 || n > kTraceWords - 8) return fail(GOLHIP_EINVAL, "bad out");
+    std::lock_guard<std::mutex> g(h->mu);
+    if (!h->d_trace) return fail(GOLHIP_EINVAL, "set option \"trace\" first");
+    if (int rc = set_dev(h)) return rc;
+    if (int rc = sync_stream(h)) return rc;
+    HIP_OR_FAIL(hipMemcpy(out, h->d_trace + 8, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return GOLHIP_OK;
+}
+
+int golhip_persist_trace(golhip_t h, uint64_t out[5]) {
+    if (int rc = check(h)) return rc;
+    if (!out) return fail(GOLHIP_EINVAL, "null out");
+    std::lock_guard<std::mutex> g(h->mu);
+    if (!h->d_trace) return fail(GOLHIP_EINVAL, "set option \"trace\" first");
+    if (int rc = set_dev(h)) return rc;
+    if (int rc = sync_stream(h)) return rc;
+    HIP_OR_FAIL(hipMemcpy(out, h->d_trace, 5 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    HIP_OR_FAIL(hipMemset(h->d_trace, 0, 8 * sizeof(unsigned long long)));
     return GOLHIP_OK;
 }
 

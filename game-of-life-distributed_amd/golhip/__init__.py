@@ -112,6 +112,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "golhip_board_hash": ([H, P(u64)], ctypes.c_int),
         "golhip_perf": ([H, P(Perf)], ctypes.c_int),
         "golhip_perf_reset": ([H], ctypes.c_int),
+        "golhip_persist_trace": ([H, P(u64)], ctypes.c_int),
+        "golhip_persist_trace_waves": ([H, ctypes.c_void_p, i64], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -274,6 +276,19 @@ class Board:
         p = Perf()
         _check(load().golhip_perf(self._h, ctypes.byref(p)))
         return p.as_dict()
+
+    def persist_trace(self) -> dict:
+        """Persistent-kernel diagnostics (set_option("trace", 1) before stepping)."""
+        out = (ctypes.c_uint64 * 5)()
+        _check(load().golhip_persist_trace(self._h, out))
+        band, mx, wait, tot, wgs = (int(x) for x in out)
+        return {"band_ticks": band, "max_band_ticks": mx, "wait_ticks": wait, "kernel_ticks": tot, "workgroups": wgs}
+
+    def persist_trace_waves(self, workgroups: int) -> np.ndarray:
+        """(start, end) ticks per (workgroup, wave) of one super-step: shape (workgroups, 64, 2)."""
+        out = np.zeros(workgroups * 128, dtype=np.uint64)
+        _check(load().golhip_persist_trace_waves(self._h, _ptr(out), out.size))
+        return out.reshape(workgroups, 64, 2)
 
     def perf_reset(self) -> None:
         _check(load().golhip_perf_reset(self._h))

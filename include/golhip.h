@@ -162,6 +162,16 @@ int golhip_board_hash(golhip_t h, uint64_t *hash);
 
 /* ---- measurement ------------------------------------------------------ */
 int golhip_perf(golhip_t h, golhip_perf_t *out);
+/* Diagnostics of the persistent step kernels since the last call (option
+ * "trace" must be set before stepping): out[0] = sum over waves of band
+ * compute time, out[1] = longest band of one super-step, out[2] = sum over
+ * workgroups of time spent waiting for neighbour workgroups, out[3] = sum
+ * over workgroups of kernel time, out[4] = workgroup count; times in
+ * s_memrealtime ticks (100 MHz).  No reference counterpart (measurement). */
+int golhip_persist_trace(golhip_t h, uint64_t out[5]);
+/* Per-wave (start, end) ticks of the middle super-step of the last persistent
+ * launch: out[2 * (workgroup * 64 + wave) + {0, 1}], n words. */
+int golhip_persist_trace_waves(golhip_t h, uint64_t *out, int64_t n);
 int golhip_perf_reset(golhip_t h);
 
 #ifdef __cplusplus

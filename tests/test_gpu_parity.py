@@ -328,16 +328,19 @@ def test_persistent_full_size_matches_per_launch(N, turns):
     assert res[0] == res[1]
 
 
-@pytest.mark.parametrize("N,depth,wpl,nw", [(2048, 8, 1, 4), (2048, 16, 1, 4), (4096, 8, 2, 4), (4096, 16, 2, 4),
-                                            (2048, 8, 1, 8), (4096, 8, 2, 8), (1024, 4, 2, 4)])
-def test_persistent_waves_per_workgroup(coracle, N, depth, wpl, nw):
-    """Persistent kernel with 4 / 8 resident waves per workgroup vs the C oracle."""
+@pytest.mark.parametrize("N,depth,wpl,nw", [(2048, 8, 1, 8), (2048, 16, 1, 8), (4096, 8, 2, 8), (4096, 16, 2, 8),
+                                            (1024, 8, 1, 8), (4096, 4, 2, 16)])
+@pytest.mark.parametrize("wt", [0, 1])
+def test_persistent_waves_per_workgroup(coracle, N, depth, wpl, nw, wt):
+    """Persistent kernel with 8 / 16 resident waves per workgroup, plain or
+    write-through (sc1) output stores, vs the C oracle."""
     board = coracle.fill_random(N, N // 2, 0x5EED0008)
     turns = 4 * depth + 3
     want = coracle.run(board, turns)
     with golhip.Board(N, N // 2) as b:
         b.set_option("wpl", wpl)
         b.set_option("persist_waves", nw)
+        b.set_option("persist_wt", wt)
         b.set_tb_depth(depth)
         b.load_bytes(board)
         b.step(turns)
@@ -404,3 +407,97 @@ def test_diagonal_schedule_matches_oracle(coracle, N, depth, wpl, nw):
         assert b.perf()["persist_launches"] == 1
         assert np.array_equal(b.snapshot_bytes(), want)
         assert b.alive_count() == (int((want == 255).sum()), turns)
+
+
+# ---------------------------------------------------------------- interleaved pair layout (wpl = 2)
+@pytest.mark.parametrize("W,H", [(1024, 96), (640, 128), (4096, 64)])
+def test_interleaved_layout_side_channels(coracle, W, H):
+    """wpl = 2 boards live in the interleaved pair layout: every canonical view
+    (bytes, bits, hash, flips, alive list) must be unaffected, including after
+    switching the layout mid-run and after load_bits."""
+    board = coracle.fill_random(W, H, 0x5EED000B)
+    with golhip.Board(W, H) as b:
+        b.set_option("wpl", 2)
+        b.load_bytes(board)
+        assert np.array_equal(b.snapshot_bytes(), board)
+        assert np.array_equal(b.snapshot_bits(), pack_bits(board))
+        assert b.board_hash() == golhip.board_hash_np(pack_bits(board))
+        b.step(6, want_flips=True)
+        want5 = coracle.run(board, 5)
+        want6 = coracle.run(board, 6)
+        assert np.array_equal(b.flips(), flips_np(want5, want6))
+        assert np.array_equal(b.snapshot_bytes(), want6)
+        assert np.array_equal(b.alive_cells(), alive_cells_np(want6))
+        assert b.board_hash() == golhip.board_hash_np(pack_bits(want6))
+        b.set_option("wpl", 1)      # converted back to canonical at the next step
+        b.step(7)
+        want13 = coracle.run(board, 13)
+        assert np.array_equal(b.snapshot_bits(), pack_bits(want13))
+        b.set_option("wpl", 2)
+        b.step(9, want_flips=True)
+        want21, want22 = coracle.run(board, 21), coracle.run(board, 22)
+        assert np.array_equal(b.flips(), flips_np(want21, want22))
+        assert np.array_equal(b.snapshot_bytes(), want22)
+        b.load_bits(pack_bits(board))
+        assert np.array_equal(b.snapshot_bits(), pack_bits(board))
+        b.step(22)
+        assert np.array_equal(b.snapshot_bytes(), want22)
+        assert b.alive_count() == (int((want22 == 255).sum()), 22)
+
+
+def test_interleaved_fill_random_and_strips(coracle):
+    """fill_random + in-process strips on a wpl = 2 board vs the C oracle."""
+    W, H = 2048, 256
+    want = coracle.run(coracle.fill_random(W, H, 0x5EED000C), 40)
+    hs = []
+    try:
+        for r0, rows in ((0, 100), (100, 60), (160, 96)):
+            h = golhip.Board(W, H, row0=r0, rows=rows)
+            h.set_option("wpl", 2)
+            h.fill_random(0x5EED000C)
+            hs.append(h)
+        golhip.group_step(hs, 40)
+        got = np.concatenate([h.snapshot_bytes() for h in hs])
+        assert np.array_equal(got, want)
+        assert sum(h.board_hash() for h in hs) & (2**64 - 1) == golhip.board_hash_np(pack_bits(want))
+    finally:
+        for h in hs:
+            h.close()
+
+
+# ---------------------------------------------------------------- K1n: bands without the vertical halo
+@pytest.mark.parametrize("W,H,depth,wpl,nw", [(2048, 1024, 16, 1, 8), (2048, 1024, 8, 1, 8), (2048, 1536, 8, 1, 16),
+                                              (4096, 1024, 8, 2, 8), (4096, 2048, 8, 2, 16), (1984, 1000, 16, 1, 8),
+                                              (2048, 997, 8, 1, 8), (640, 4096, 16, 1, 8)])
+def test_k1n_matches_oracle(coracle, W, H, depth, wpl, nw):
+    """K1n (each stage's first two rows handed to the band above through LDS,
+    output drifting D rows down per super-step) vs the C oracle."""
+    board = coracle.fill_random(W, H, 0x5EED000D)
+    turns = 4 * depth + 3
+    want = coracle.run(board, turns)
+    with golhip.Board(W, H) as b:
+        b.set_option("wpl", wpl)
+        b.set_option("k1n", 1)
+        b.set_option("persist_waves", nw)
+        b.set_tb_depth(depth)
+        b.load_bytes(board)
+        b.step(turns)
+        assert b.perf()["persist_launches"] == 1
+        assert np.array_equal(b.snapshot_bytes(), want)
+        assert b.alive_count() == (int((want == 255).sum()), turns)
+
+
+@pytest.mark.parametrize("N,depth,nw,turns", [(16384, 16, 8, 512), (16384, 8, 16, 256), (65536, 16, 8, 64)])
+def test_k1n_full_size(N, depth, nw, turns):
+    res = []
+    for opts in ({"k1n": 1, "persist_waves": nw}, {"persistent": 0}):
+        with golhip.Board(N, N) as b:
+            for k, v in opts.items():
+                b.set_option(k, v)
+            b.set_tb_depth(depth)
+            b.fill_random(0x5EED0001)
+            b.step(turns)
+            if "k1n" in opts:
+                assert b.perf()["persist_launches"] == 1
+            res.append((b.board_hash(), b.alive_count()))
+    assert res[0] == res[1]
