@@ -56,7 +56,6 @@ struct PersistArgs {
     int first;                // buffer holding generation 0 (0 -> buf0)
     int J;                    // super-steps of `depth` turns
     int S;                    // rows per wavefront
-    int Sb;                   // K1n: rows of a workgroup's bottom band
     int wg_tx, wg_sy;         // workgroup block of (tiles, strips)
     int cols, wg_y;           // workgroup grid
     int tiles_x;
@@ -67,22 +66,11 @@ struct PersistArgs {
     unsigned long long *trace; // nullable diagnostics (golhip_persist_trace)
 };
 int persist_waves_for(int depth, int wpl);
-// diag: diagonal (systolic) stage schedule instead of skewed 3-row groups.
-int persist_blocks_per_cu(int depth, int wpl, int nw, bool diag);
+int persist_blocks_per_cu(int depth, int wpl, int nw);
 // Workgroup shape / band height for `cus` resident workgroups of `units`
 // (tile, strip) units each; false if none fits.  Caller sets p->nw.
 bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, int units, PersistArgs *p);
-// wt: write-through (sc1) output stores.
-hipError_t launch_persist(const PersistArgs &p, int depth, int wpl, bool diag, bool wt, hipStream_t s);
-// K1n: bands without the vertical halo (LDS hand-off of each stage's first
-// two rows to the band above inside a workgroup); p.nw = bands per workgroup.
-int k1n_blocks_per_cu(int depth, int wpl, int nw);
-bool plan_k1n(int Ww, int rows, int depth, int cus, int wpl, int nw, PersistArgs *p);
-hipError_t launch_k1n(const PersistArgs &p, int depth, int wpl, hipStream_t s);
-// Stage-split persistent kernel K1s: p.nw = nws * (pipelines per workgroup).
-// gt = groups of 3 rows per tick.
-int pipe_blocks_per_cu(int depth, int wpl, int nws, int np, int gt);
-hipError_t launch_pipe(const PersistArgs &p, int depth, int wpl, int nws, int gt, hipStream_t s);
+hipError_t launch_persist(const PersistArgs &p, int depth, int wpl, hipStream_t s);
 
 hipError_t launch_pack(const uint8_t *bytes, uint32_t *words, int W, int Ww, int rows, hipStream_t s);
 // il: the words are in the interleaved pair layout of the wpl = 2 step kernels

@@ -240,10 +240,7 @@ __device__ __forceinline__ Lanes<WPL> vmov(const Lanes<WPL> &v) {
 // One wavefront streams output rows [r0, r0 + rows_here) of the tile whose
 // first stored word is t0, D turns ahead; returns the popcount of its stored
 // output words.  Shared by the per-launch and the persistent kernel.
-// WT: write the output rows through to memory (sc1 stores, the line leaves the
-// XCD's L2) so a persistent kernel's per-super-step agent release has no
-// dirty L2 lines to write back.
-template <int D, bool SKIP, int WPL, bool WT = false>
+template <int D, bool SKIP, int WPL>
 __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int rows_here, int t0) {
     const int lane = threadIdx.x & 63;
     const int Ww = a.Ww;
@@ -285,17 +282,10 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
         uint32_t *p = ok ? dst_row0 + (ptrdiff_t)out_idx * Ww : dummy;
         uint32_t pc = 0;
         if constexpr (WPL == 1) {
-            if constexpr (WT)
-                __hip_atomic_store(p, y.w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else
-                *p = y.w[0];
+            *p = y.w[0];
             pc = __builtin_popcount(y.w[0]);
         } else {
-            if constexpr (WT)
-                __hip_atomic_store(reinterpret_cast<uint64_t *>(p), (uint64_t)y.w[0] | ((uint64_t)y.w[1] << 32),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else
-                *reinterpret_cast<uint2 *>(p) = make_uint2(y.w[0], y.w[1]);
+            *reinterpret_cast<uint2 *>(p) = make_uint2(y.w[0], y.w[1]);
             pc = __builtin_popcount(y.w[0]) + __builtin_popcount(y.w[1]);
         }
         cnt += ok ? pc : 0u;
@@ -356,342 +346,6 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
     return cnt;
 }
 
-// ---------------------------------------------------------------------------
-// Diagonal (systolic) schedule of the same D-stage pipeline.
-//
-// Iteration n feeds input row n into stage 0 while stage t works on row
-// n - t: the D stage-steps of an iteration are independent, so a wave has D
-// dependency chains in flight instead of the ~2.7 of a skewed 3-row group.
-// That keeps the VALU busy at 1-2 waves per SIMD, which in turn lets a
-// persistent launch use fewer, taller bands (less pipeline fill).  The set of
-// (row, stage) pairs computed is the group schedule's: stage t skips rows
-// that only carry pipeline-fill padding (n < 3t) and, after the last input,
-// rows that do not exist (n - t > last).
-// ---------------------------------------------------------------------------
-template <int D, int WPL, int U, int A0, int A1, int T>
-__device__ __forceinline__ void diag_stages(Lanes<WPL> (&xs)[D + 1], uint32_t (&h0)[3][D][WPL],
-                                            uint32_t (&h1)[3][D][WPL], uint32_t (&cc)[3][D][WPL]) {
-    if constexpr (T >= 0) {
-        if constexpr (T >= A0 && T < A1) {
-            constexpr int R = ((U - T) % 3 + 3) % 3;
-            Lanes<WPL> y = xs[T];
-            stage<D, R, WPL>(T, y, h0, h1, cc);
-            xs[T + 1] = y;
-        }
-        diag_stages<D, WPL, U, A0, A1, T - 1>(xs, h0, h1, cc);
-    }
-}
-
-template <int D, int SKIP_UNUSED, int WPL>
-__device__ __forceinline__ uint32_t stream_band_diag(const StepArgs &a, int r0, int rows_here, int t0) {
-    const int lane = threadIdx.x & 63;
-    const int Ww = a.Ww;
-    int col = (t0 + WPL * (lane - 1)) % Ww;
-    if (col < 0) col += Ww;
-    const bool keep = lane >= 1 && lane <= kTileValid && (t0 + WPL * (lane - 1)) < Ww;
-
-    int r = r0 - D + a.in.off;
-    const int wrap = a.in.wrap > 0 ? a.in.wrap : INT_MAX;
-    if (a.in.wrap > 0) {
-        r %= a.in.wrap;
-        if (r < 0) r += a.in.wrap;
-    }
-    const uint32_t *__restrict__ src = a.src + col;
-    auto load_next = [&]() -> Lanes<WPL> {
-        const int pr = a.in.base + min(r, a.in.rmax);
-        Lanes<WPL> v;
-        if constexpr (WPL == 1) {
-            v.w[0] = src[(size_t)pr * Ww];
-        } else {
-            const uint2 q = *reinterpret_cast<const uint2 *>(src + (size_t)pr * Ww);
-            v.w[0] = q.x;
-            v.w[1] = q.y;
-        }
-        r = (r + 1 == wrap) ? 0 : r + 1;
-        return v;
-    };
-    uint32_t *const dst_row0 = a.dst + (size_t)(a.dst_base + r0) * Ww + col;
-    uint32_t *const dummy = a.dst + col;
-    uint32_t cnt = 0;
-    auto emit = [&](const Lanes<WPL> &y, int out_idx) {
-        const bool ok = keep && (unsigned)out_idx < (unsigned)rows_here;
-        uint32_t *p = ok ? dst_row0 + (ptrdiff_t)out_idx * Ww : dummy;
-        uint32_t pc = 0;
-        if constexpr (WPL == 1) {
-            *p = y.w[0];
-            pc = __builtin_popcount(y.w[0]);
-        } else {
-            *reinterpret_cast<uint2 *>(p) = make_uint2(y.w[0], y.w[1]);
-            pc = __builtin_popcount(y.w[0]) + __builtin_popcount(y.w[1]);
-        }
-        cnt += ok ? pc : 0u;
-    };
-
-    uint32_t h0[3][D][WPL], h1[3][D][WPL], cc[3][D][WPL];
-    Lanes<WPL> xs[D + 1];
-#pragma unroll
-    for (int s = 0; s < 3; ++s)
-#pragma unroll
-        for (int t = 0; t < D; ++t)
-#pragma unroll
-            for (int k = 0; k < WPL; ++k) h0[s][t][k] = h1[s][t][k] = cc[s][t][k] = 0u;
-#pragma unroll
-    for (int t = 0; t <= D; ++t)
-#pragma unroll
-        for (int k = 0; k < WPL; ++k) xs[t].w[k] = 0u;
-
-    // iteration n: out index n + 1 - 3D; the last row that matters enters at
-    // n = last = rows_here + 2D - 1 and leaves stage D-1 at n = last + D - 1
-    const int last = rows_here + 2 * D - 1;
-    const int n_end = last + D;  // exclusive
-    Lanes<WPL> x0 = vmov(load_next()), x1 = vmov(load_next()), x2 = vmov(load_next());
-    int n = 0;
-    auto body = [&](auto a0_tag, auto a1_tag) {
-        constexpr int A0 = decltype(a0_tag)::value;
-        constexpr int A1 = decltype(a1_tag)::value;
-        const Lanes<WPL> p0 = load_next(), p1 = load_next(), p2 = load_next();
-        __builtin_amdgcn_sched_barrier(0);
-        xs[0] = x0;
-        diag_stages<D, WPL, 0, A0, A1, D - 1>(xs, h0, h1, cc);
-        emit(xs[D], n + 1 - 3 * D);
-        xs[0] = x1;
-        diag_stages<D, WPL, 1, A0, A1, D - 1>(xs, h0, h1, cc);
-        emit(xs[D], n + 2 - 3 * D);
-        xs[0] = x2;
-        diag_stages<D, WPL, 2, A0, A1, D - 1>(xs, h0, h1, cc);
-        emit(xs[D], n + 3 - 3 * D);
-        __builtin_amdgcn_sched_barrier(0);
-        x0 = vmov(p0);
-        x1 = vmov(p1);
-        x2 = vmov(p2);
-        n += 3;
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using ID = std::integral_constant<int, D>;
-    // fill: body at n = 3q runs stages t <= q (n >= 3t)
-    while (n / 3 + 1 <= D / 4) body(I0(), std::integral_constant<int, D / 4>());
-    while (n / 3 + 1 <= D / 2) body(I0(), std::integral_constant<int, D / 2>());
-    while (n / 3 + 1 <= 3 * D / 4) body(I0(), std::integral_constant<int, 3 * D / 4>());
-    // steady state, then drain: skip stages t < n - last (rows past the end)
-    while (n - last < D / 4 && n < n_end) body(I0(), ID());
-    while (n - last < D / 2 && n < n_end) body(std::integral_constant<int, D / 4>(), ID());
-    while (n - last < 3 * D / 4 && n < n_end) body(std::integral_constant<int, D / 2>(), ID());
-    while (n < n_end) body(std::integral_constant<int, 3 * D / 4>(), ID());
-    return cnt;
-}
-
-// push_group over stages [A0, A1) with per-stage hooks: pre(t, u, x) may
-// replace row u's input to stage t, post(t, u, x) sees stage t's output.
-template <int D, int A0, int A1, int WPL, typename Pre, typename Post>
-__device__ __forceinline__ void push_group_h(Lanes<WPL> &x0, Lanes<WPL> &x1, Lanes<WPL> &x2,
-                                             uint32_t (&h0)[3][D][WPL], uint32_t (&h1)[3][D][WPL],
-                                             uint32_t (&cc)[3][D][WPL], Pre &&pre, Post &&post) {
-#pragma unroll
-    for (int s = A0; s < A1 + 2; ++s) {
-        if (s < A1) {
-            pre(s, 0, x0);
-            stage<D, 0, WPL>(s, x0, h0, h1, cc);
-            post(s, 0, x0);
-        }
-        if (s - 1 >= A0 && s - 1 < A1) {
-            pre(s - 1, 1, x1);
-            stage<D, 1, WPL>(s - 1, x1, h0, h1, cc);
-            post(s - 1, 1, x1);
-        }
-        if (s - 2 >= A0 && s - 2 < A1) {
-            pre(s - 2, 2, x2);
-            stage<D, 2, WPL>(s - 2, x2, h0, h1, cc);
-            post(s - 2, 2, x2);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// K1n: band without the vertical halo (persistent, torus).
-//
-// A K1p band recomputes D halo rows above and below itself every super-step
-// (the pipeline fill, ~1.25 D + D/2 rows of D stages for S rows of output).
-// Here a band streams its own rows r0 .. r0+S+1 only and lets the output
-// drift down by one row per stage: stage t emits rows r0+t+1 .. r0+S+t, so
-// the top needs nothing from above.  At the bottom, stage t needs two rows of
-// generation t below the band, which are exactly the first two outputs of
-// stage t-1 of the band below: every band publishes those 2(D-1) rows in LDS
-// during its first 2D input rows, and the band above picks them up when its
-// stream reaches row S (S >= 2D + 3, so a band's exports are complete before
-// it needs imports; there is no cycle inside a workgroup).  The bottom band
-// of a workgroup has no band below in LDS and runs the classic trapezoid
-// bottom (2D extra input rows).  After D stages the band's output is rows
-// r0+D .. r0+D+S-1 of generation D: bands stay put, each super-step's output
-// is written D rows lower, and every row is still written exactly once.
-// Work per band ~ D (S + 2) stage-rows instead of ~ D (S + 1.75 D).
-// ---------------------------------------------------------------------------
-template <int D, int WPL>
-__device__ __forceinline__ uint32_t stream_band_n(const StepArgs &a, int r0, int rows_here, int t0,
-                                                  uint32_t *ex_mine, const uint32_t *ex_below, uint32_t *ex_dummy,
-                                                  volatile int *flag_mine, volatile int *flag_below, int flag_val,
-                                                  bool count, unsigned *error, long long timeout_ticks) {
-    constexpr int ROW = 64 * WPL;
-    const int lane = threadIdx.x & 63;
-    const int Ww = a.Ww;
-    int col = (t0 + WPL * (lane - 1)) % Ww;
-    if (col < 0) col += Ww;
-    const bool keep = lane >= 1 && lane <= kTileValid && (t0 + WPL * (lane - 1)) < Ww;
-    const bool imports = ex_below != nullptr;
-    const int G = (rows_here + 2 * D + 2) / 3;
-
-    int r = r0 + a.in.off;  // no halo above: the stream starts at the band's first row
-    const int wrap = a.in.wrap > 0 ? a.in.wrap : INT_MAX;
-    if (a.in.wrap > 0) {
-        r %= a.in.wrap;
-        if (r < 0) r += a.in.wrap;
-    }
-    const uint32_t *__restrict__ src = a.src + col;
-    auto load_next = [&]() -> Lanes<WPL> {
-        const int pr = a.in.base + min(r, a.in.rmax);
-        Lanes<WPL> v;
-        if constexpr (WPL == 1) {
-            v.w[0] = src[(size_t)pr * Ww];
-        } else {
-            const uint2 q = *reinterpret_cast<const uint2 *>(src + (size_t)pr * Ww);
-            v.w[0] = q.x;
-            v.w[1] = q.y;
-        }
-        r = (r + 1 == wrap) ? 0 : r + 1;
-        return v;
-    };
-    uint32_t *const dummy = a.dst + col;
-    uint32_t cnt = 0;
-    auto emit = [&](const Lanes<WPL> &y, int oi) {  // output index oi -> row r0 + D + oi (torus)
-        const bool ok = keep && (unsigned)oi < (unsigned)rows_here;
-        int orow = r0 + D + oi;
-        if (orow >= a.rows_out) orow -= a.rows_out;
-        uint32_t *q = ok ? a.dst + (size_t)(a.dst_base + orow) * Ww + col : dummy;
-        uint32_t pc = 0;
-        if constexpr (WPL == 1) {
-            *q = y.w[0];
-            pc = __builtin_popcount(y.w[0]);
-        } else {
-            *reinterpret_cast<uint2 *>(q) = make_uint2(y.w[0], y.w[1]);
-            pc = __builtin_popcount(y.w[0]) + __builtin_popcount(y.w[1]);
-        }
-        cnt += (ok && count) ? pc : 0u;
-    };
-    // LDS rows are planar (word k of all 64 lanes contiguous).  Exports go
-    // through ds_write_addtid_b32 (address = M0 + 4 * lane): the slot base is
-    // wave-uniform, so no per-stage address VGPRs stay live in the fill.
-    auto lds_put = [&](uint32_t *row, const Lanes<WPL> &y) {
-#pragma unroll
-        for (int k = 0; k < WPL; ++k) {
-            const uint32_t base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)(row + 64 * k);
-            uint32_t saved;
-            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tds_write_addtid_b32 %2\n\ts_mov_b32 m0, %0"
-                         : "=&s"(saved)
-                         : "s"(base), "v"(y.w[k])
-                         : "memory");
-        }
-    };
-    auto lds_get = [&](const uint32_t *row) -> Lanes<WPL> {
-        Lanes<WPL> v;
-#pragma unroll
-        for (int k = 0; k < WPL; ++k) v.w[k] = row[64 * k + lane];
-        return v;
-    };
-
-    uint32_t h0[3][D][WPL], h1[3][D][WPL], cc[3][D][WPL];
-#pragma unroll
-    for (int s = 0; s < 3; ++s)
-#pragma unroll
-        for (int t = 0; t < D; ++t)
-#pragma unroll
-            for (int k = 0; k < WPL; ++k) h0[s][t][k] = h1[s][t][k] = cc[s][t][k] = 0u;
-
-    Lanes<WPL> x0 = vmov(load_next()), x1 = vmov(load_next()), x2 = vmov(load_next());
-    int q = 0;  // group: input tokens 3q .. 3q+2 (token m = row r0 + m)
-    auto no_pre = [](int, int, Lanes<WPL> &) {};
-    auto no_post = [](int, int, const Lanes<WPL> &) {};
-    // exports: stage t's first two valid outputs (tokens 2t+2, 2t+3: rows r0+t+1, r0+t+2)
-    auto export_post = [&](int t, int u, const Lanes<WPL> &y) {
-        if (t <= D - 2) {
-            const int idx = 3 * q + u - 2 * t - 2;
-            uint32_t *row = (idx == 0 || idx == 1) ? ex_mine + (2 * t + idx) * ROW : ex_dummy;
-            lds_put(row, y);
-        }
-    };
-    auto body = [&](auto a0_tag, auto a1_tag, auto pre, auto post, const Lanes<WPL> *imp) {
-        constexpr int A0 = decltype(a0_tag)::value;
-        constexpr int A1 = decltype(a1_tag)::value;
-        const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
-        __builtin_amdgcn_sched_barrier(0);
-        Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
-        push_group_h<D, A0, A1, WPL>(y0, y1, y2, h0, h1, cc, pre, post);
-        if constexpr (A1 == D) {
-            const int oi = 3 * q - 2 * D;
-            emit(y0, oi);
-            emit(y1, oi + 1);
-            emit(y2, oi + 2);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        x0 = vmov(n0);
-        x1 = vmov(n1);
-        x2 = vmov(n2);
-        ++q;
-        (void)imp;
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using ID = std::integral_constant<int, D>;
-    // fill (stage t idle before token 2t) with exports
-    while ((3 * q + 2) / 2 + 1 <= D / 4) body(I0(), std::integral_constant<int, D / 4>(), no_pre, export_post, nullptr);
-    while ((3 * q + 2) / 2 + 1 <= D / 2) body(I0(), std::integral_constant<int, D / 2>(), no_pre, export_post, nullptr);
-    while ((3 * q + 2) / 2 + 1 <= 3 * D / 4)
-        body(I0(), std::integral_constant<int, 3 * D / 4>(), no_pre, export_post, nullptr);
-    while (3 * q < 2 * D) body(I0(), ID(), no_pre, export_post, nullptr);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) *flag_mine = flag_val;
-    if (!imports) {
-        while (q < G) body(I0(), ID(), no_pre, no_post, nullptr);
-        return cnt;
-    }
-    while (3 * q + 2 < rows_here) body(I0(), ID(), no_pre, no_post, nullptr);
-    // imports from the band below (published in LDS during its first 2D rows)
-    {
-        const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
-        while (*flag_below < flag_val) {
-            if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > timeout_ticks) {
-                if (lane == 0) atomicOr(error, 2u);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    // drain: token m >= rows_here feeds stage t = (m - rows_here) / 2 with import
-    // row m - rows_here - 2; stages t with 2t + rows_here + 2 <= 3q are done
-    Lanes<WPL> imp[3];
-    auto load_imports = [&]() {
-#pragma unroll
-        for (int u = 0; u < 3; ++u) {
-            const int i = 3 * q + u - rows_here - 2;
-            imp[u] = lds_get((i >= 0 && i < 2 * (D - 1)) ? ex_below + i * ROW : ex_dummy);
-        }
-    };
-    auto import_pre = [&](int t, int u, Lanes<WPL> &x) {
-        if (t >= 1) {
-            const int rel = 3 * q + u - rows_here;
-            const bool take = rel >= 2 && (rel >> 1) == t;
-#pragma unroll
-            for (int k = 0; k < WPL; ++k) x.w[k] = take ? imp[u].w[k] : x.w[k];
-        }
-    };
-    auto drain = [&](auto a0_tag) {
-        load_imports();
-        body(a0_tag, ID(), import_pre, no_post, imp);
-    };
-    while (q < G && 3 * q < D / 2 + rows_here) drain(I0());
-    while (q < G && 3 * q < D + rows_here) drain(std::integral_constant<int, D / 4>());
-    while (q < G && 3 * q < 3 * D / 2 + rows_here) drain(std::integral_constant<int, D / 2>());
-    while (q < G) drain(std::integral_constant<int, 3 * D / 4>());
-    return cnt;
-}
-
 __host__ __device__ constexpr int tile_words(int wpl) { return kTileValid * wpl; }
 
 template <int D, bool SKIP, int WPL>
@@ -728,7 +382,7 @@ __global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int persist_waves(int depth, int wpl) { return depth * wpl <= 16 ? 16 : 8; }
 
-template <int D, int WPL, int NW, bool DIAG, bool WT = false>
+template <int D, int WPL, int NW>
 __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -783,345 +437,7 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
         const bool odd = ((p.first + j) & 1) != 0;
         a.src = odd ? p.buf1 : p.buf0;
         a.dst = odd ? p.buf0 : p.buf1;
-        if constexpr (DIAG)
-            cnt = rows_here > 0 ? stream_band_diag<D, 1, WPL>(a, r0, rows_here, tile * tile_words(WPL)) : 0u;
-        else
-            cnt = rows_here > 0 ? stream_band<D, true, WPL, WT>(a, r0, rows_here, tile * tile_words(WPL)) : 0u;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        {
-            const long long tr_e = (long long)__builtin_amdgcn_s_memrealtime();
-            const long long d = tr_e - tr_b0;
-            tr_band += d;
-            tr_max = d > tr_max ? d : tr_max;
-            if (p.trace && j == p.J / 2 && lane == 0) {  // per-wave (start, end) of one super-step
-                p.trace[8 + 2 * (b * 64 + w)] = (unsigned long long)tr_b0;
-                p.trace[8 + 2 * (b * 64 + w) + 1] = (unsigned long long)tr_e;
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(&p.progress[b], (unsigned)(j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    if (p.trace && lane == 0) {  // diagnostics: per-wave band time, workgroup wait time
-        atomicAdd(&p.trace[0], (unsigned long long)tr_band);
-        atomicMax(&p.trace[1], (unsigned long long)tr_max);
-        if (w == 0) {
-            atomicAdd(&p.trace[2], (unsigned long long)tr_wait);
-            atomicAdd(&p.trace[3], (unsigned long long)((long long)__builtin_amdgcn_s_memrealtime() - tr_t0));
-            atomicAdd(&p.trace[4], 1ull);
-        }
-    }
-    if (p.base.alive) {
-        const uint32_t tot = wave_sum_u32(cnt);
-        if (lane == 0 && tot) atomicAdd(p.base.alive, (unsigned long long)tot);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// K1s: persistent kernel with the D stages of a band split over NWS waves.
-//
-// Same super-step protocol as K1p, but a workgroup runs P pipelines (one
-// (tile, strip) unit each) of NWS wavefronts: wave k of a pipeline owns
-// stages [k*DW, (k+1)*DW) and hands each 3-row group to wave k+1 through a
-// double-buffered LDS slot.  The waves advance in ticks separated by a
-// workgroup barrier; at tick tau wave k works on group tau - 2k.  A unit's
-// pipeline fill (2D input rows) is then paid once per NWS waves, so with the
-// same resident waves a band is NWS times taller and the fill fraction
-// (~1.25 D / S) NWS times smaller — the limit of K1p on boards whose
-// (tile, strip) units barely cover the machine (16384^2: S = 37 rows).
-// Waves whose stages would only see pipeline-fill padding skip the group.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-template <int D, int WPL, int NWS, int GT>
-__device__ __forceinline__ uint32_t pipe_band(const StepArgs &a, int r0, int rows_here, int t0, int k, int T,
-                                              uint32_t *__restrict__ ring, bool count) {
-    constexpr int DW = D / NWS;
-    constexpr int SLOT = 3 * 64 * WPL;
-    const int lane = threadIdx.x & 63;
-    const int Ww = a.Ww;
-    int col = (t0 + WPL * (lane - 1)) % Ww;
-    if (col < 0) col += Ww;
-    const bool keep = lane >= 1 && lane <= kTileValid && (t0 + WPL * (lane - 1)) < Ww;
-    const int G = rows_here > 0 ? (rows_here + 2 * D + 2) / 3 : 0;
-
-    int r = r0 - D + a.in.off;
-    const int wrap = a.in.wrap > 0 ? a.in.wrap : INT_MAX;
-    if (a.in.wrap > 0) {
-        r %= a.in.wrap;
-        if (r < 0) r += a.in.wrap;
-    }
-    const uint32_t *__restrict__ src = a.src + col;
-    auto load_next = [&]() -> Lanes<WPL> {
-        const int pr = a.in.base + min(r, a.in.rmax);
-        Lanes<WPL> v;
-        if constexpr (WPL == 1) {
-            v.w[0] = src[(size_t)pr * Ww];
-        } else {
-            const uint2 q = *reinterpret_cast<const uint2 *>(src + (size_t)pr * Ww);
-            v.w[0] = q.x;
-            v.w[1] = q.y;
-        }
-        r = (r + 1 == wrap) ? 0 : r + 1;
-        return v;
-    };
-    uint32_t *const dst_row0 = a.dst + (size_t)(a.dst_base + r0) * Ww + col;
-    uint32_t *const dummy = a.dst + col;
-    uint32_t cnt = 0;
-    auto emit = [&](const Lanes<WPL> &y, int out_idx) {
-        const bool ok = keep && (unsigned)out_idx < (unsigned)rows_here;
-        uint32_t *q = ok ? dst_row0 + (ptrdiff_t)out_idx * Ww : dummy;
-        uint32_t pc = 0;
-        if constexpr (WPL == 1) {
-            *q = y.w[0];
-            pc = __builtin_popcount(y.w[0]);
-        } else {
-            *reinterpret_cast<uint2 *>(q) = make_uint2(y.w[0], y.w[1]);
-            pc = __builtin_popcount(y.w[0]) + __builtin_popcount(y.w[1]);
-        }
-        cnt += (ok && count) ? pc : 0u;
-    };
-    auto slot_put = [&](uint32_t *sl, const Lanes<WPL> &y, int row) {
-        if constexpr (WPL == 1) {
-            sl[row * 64 + lane] = y.w[0];
-        } else {
-            reinterpret_cast<uint2 *>(sl)[row * 64 + lane] = make_uint2(y.w[0], y.w[1]);
-        }
-    };
-    auto slot_get = [&](const uint32_t *sl, int row) -> Lanes<WPL> {
-        Lanes<WPL> v;
-        if constexpr (WPL == 1) {
-            v.w[0] = sl[row * 64 + lane];
-        } else {
-            const uint2 q = reinterpret_cast<const uint2 *>(sl)[row * 64 + lane];
-            v.w[0] = q.x;
-            v.w[1] = q.y;
-        }
-        return v;
-    };
-
-    uint32_t h0[3][DW][WPL], h1[3][DW][WPL], cc[3][DW][WPL];
-#pragma unroll
-    for (int s = 0; s < 3; ++s)
-#pragma unroll
-        for (int t = 0; t < DW; ++t)
-#pragma unroll
-            for (int q = 0; q < WPL; ++q) h0[s][t][q] = h1[s][t][q] = cc[s][t][q] = 0u;
-
-    // Wave k works on the GT groups from GT * (tau - 2k) at tick tau: their
-    // input (written by wave k-1 at tick tau - 2) is read from LDS one tick
-    // ahead, so the LDS latency hides behind a tick of compute instead of
-    // stalling every wave right after the barrier.  Wave 0 streams from global
-    // memory the same way.
-    auto active = [&](int g) { return g >= 0 && g < G && (3 * g + 2) / 2 + 1 > k * DW; };
-    Lanes<WPL> x[GT][3];
-#pragma unroll
-    for (int q = 0; q < GT; ++q) x[q][0] = x[q][1] = x[q][2] = Lanes<WPL>{};
-    if (k == 0 && G > 0) {
-#pragma unroll
-        for (int q = 0; q < GT; ++q) {
-            x[q][0] = vmov(load_next());
-            x[q][1] = vmov(load_next());
-            x[q][2] = vmov(load_next());
-        }
-    }
-    for (int tau = 0; tau < T; ++tau) {
-        const int gb = GT * (tau - 2 * k);
-        Lanes<WPL> n[GT][3];
-#pragma unroll
-        for (int q = 0; q < GT; ++q) {
-            n[q][0] = n[q][1] = n[q][2] = Lanes<WPL>{};
-            if (k == 0) {
-                if (active(gb + q)) {
-                    n[q][0] = load_next();
-                    n[q][1] = load_next();
-                    n[q][2] = load_next();
-                }
-            } else if (active(gb + GT + q)) {
-                const uint32_t *in = ring + ((k - 1) * 2 * GT + ((gb + GT + q) % (2 * GT))) * SLOT;
-                n[q][0] = slot_get(in, 0);
-                n[q][1] = slot_get(in, 1);
-                n[q][2] = slot_get(in, 2);
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < GT; ++q) {
-            const int g = gb + q;
-            if (active(g)) {
-                Lanes<WPL> y0 = x[q][0], y1 = x[q][1], y2 = x[q][2];
-                __builtin_amdgcn_sched_barrier(0);
-                push_group<DW, DW, WPL>(y0, y1, y2, h0, h1, cc);
-                if (k == NWS - 1) {
-                    const int oi = -2 * D + 3 * g;
-                    emit(y0, oi);
-                    emit(y1, oi + 1);
-                    emit(y2, oi + 2);
-                } else {
-                    uint32_t *out = ring + (k * 2 * GT + (g % (2 * GT))) * SLOT;
-                    slot_put(out, y0, 0);
-                    slot_put(out, y1, 1);
-                    slot_put(out, y2, 2);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < GT; ++q) {
-            x[q][0] = vmov(n[q][0]);
-            x[q][1] = vmov(n[q][1]);
-            x[q][2] = vmov(n[q][2]);
-        }
-        lds_barrier();
-    }
-    return cnt;
-}
-
-template <int D, int WPL, int NWS, int P, int GT>
-__global__ __launch_bounds__(NWS * P * 64) void gol_pipe_kernel(PersistArgs p) {
-    constexpr int SLOT = 3 * 64 * WPL;
-    __shared__ uint32_t ring[P][NWS > 1 ? 2 * GT * (NWS - 1) * SLOT : 1];
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int k = w / P;
-    const int pipe = w - k * P;
-    const int b = blockIdx.x;
-    const int wx = b % p.cols, wy = b / p.cols;
-    const int tile = wx * p.wg_tx + pipe % p.wg_tx;
-    const int strip = wy * p.wg_sy + pipe / p.wg_tx;
-    const int r0 = strip * p.S;
-    const int rows_here = (tile < p.tiles_x && r0 < p.base.rows_out) ? min(p.S, p.base.rows_out - r0) : 0;
-    const int T = ((p.S + 2 * D + 2) / 3 + GT - 1) / GT + 2 * (NWS - 1);  // ticks: tallest band + ramp
-
-    int nb = b;
-    if (lane < 9) {
-        const int ny = (wy + lane / 3 - 1 + p.wg_y) % p.wg_y;
-        const int nx = (wx + lane % 3 - 1 + p.cols) % p.cols;
-        nb = ny * p.cols + nx;
-    }
-    __shared__ int s_abort;
-    if (threadIdx.x == 0) s_abort = 0;
-    __syncthreads();
-
-    uint32_t cnt = 0;
-    for (int j = 0; j < p.J; ++j) {
-        if (j > 0) {
-            if (w == 0) {
-                const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
-                for (;;) {
-                    const unsigned v = __hip_atomic_load(&p.progress[nb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (__all(v >= (unsigned)j)) break;
-                    const unsigned err = __hip_atomic_load(p.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (err || (long long)__builtin_amdgcn_s_memrealtime() - t_start > p.timeout_ticks) {
-                        if (lane == 0) {
-                            atomicOr(p.error, 1u);
-                            s_abort = 1;
-                        }
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                }
-                if (lane == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            __syncthreads();
-            if (s_abort) return;  // uniform over the workgroup
-        }
-        StepArgs a = p.base;
-        const bool odd = ((p.first + j) & 1) != 0;
-        a.src = odd ? p.buf1 : p.buf0;
-        a.dst = odd ? p.buf0 : p.buf1;
-        cnt = pipe_band<D, WPL, NWS, GT>(a, r0, rows_here, tile * tile_words(WPL), k, T, &ring[pipe][0], j == p.J - 1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(&p.progress[b], (unsigned)(j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    if (p.base.alive) {
-        const uint32_t tot = wave_sum_u32(cnt);
-        if (lane == 0 && tot) atomicAdd(p.base.alive, (unsigned long long)tot);
-    }
-}
-
-template <int D, int WPL, int NW>
-__global__ __launch_bounds__(NW * 64) void gol_k1n_kernel(PersistArgs p) {
-    constexpr int ROW = 64 * WPL;
-    __shared__ uint32_t ex[NW][2 * (D - 1) * ROW];
-    __shared__ uint32_t ex_dummy[ROW];
-    __shared__ int flags[NW];
-    __shared__ int s_abort;
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int b = blockIdx.x;
-    const int wx = b % p.cols, wy = b / p.cols;
-    const int tile = wx;                  // one tile column per workgroup
-    // NW stacked bands: NW-1 importing bands of S rows, then the workgroup's
-    // bottom band of Sb rows (it pays the trapezoid bottom, ~D rows more work
-    // per stage, so it is that much shorter to keep the bands balanced)
-    const int wg_rows = (NW - 1) * p.S + p.Sb;
-    auto band_r0 = [&](int k) { return wy * wg_rows + k * p.S; };
-    auto band_rows = [&](int k) {
-        const int rr = band_r0(k);
-        const int want = k < NW - 1 ? p.S : p.Sb;
-        return (tile < p.tiles_x && rr < p.base.rows_out) ? min(want, p.base.rows_out - rr) : 0;
-    };
-    const int r0 = band_r0(w);
-    const int rows_here = band_rows(w);
-    const bool imports = w + 1 < NW && rows_here == p.S && band_rows(w + 1) > 0;
-
-    int nb = b;
-    if (lane < 9) {
-        const int ny = (wy + lane / 3 - 1 + p.wg_y) % p.wg_y;
-        const int nx = (wx + lane % 3 - 1 + p.cols) % p.cols;
-        nb = ny * p.cols + nx;
-    }
-    if (lane == 0) flags[w] = 0;
-    if (threadIdx.x == 0) s_abort = 0;
-    __syncthreads();
-
-    uint32_t cnt = 0;
-    long long tr_wait = 0, tr_band = 0, tr_max = 0;
-    const long long tr_t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    for (int j = 0; j < p.J; ++j) {
-        const long long tr_w0 = (long long)__builtin_amdgcn_s_memrealtime();
-        if (j > 0) {
-            if (w == 0) {
-                const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
-                for (;;) {
-                    const unsigned v = __hip_atomic_load(&p.progress[nb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (__all(v >= (unsigned)j)) break;
-                    const unsigned err = __hip_atomic_load(p.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (err || (long long)__builtin_amdgcn_s_memrealtime() - t_start > p.timeout_ticks) {
-                        if (lane == 0) {
-                            atomicOr(p.error, 1u);
-                            s_abort = 1;
-                        }
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                }
-                if (lane == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            __syncthreads();
-            if (s_abort) return;  // uniform over the workgroup
-        }
-        const long long tr_b0 = (long long)__builtin_amdgcn_s_memrealtime();
-        tr_wait += tr_b0 - tr_w0;
-        StepArgs a = p.base;
-        const bool odd = ((p.first + j) & 1) != 0;
-        a.src = odd ? p.buf1 : p.buf0;
-        a.dst = odd ? p.buf0 : p.buf1;
-        cnt = rows_here > 0 ? stream_band_n<D, WPL>(a, r0, rows_here, tile * tile_words(WPL), &ex[w][0],
-                                                     imports ? &ex[w + 1][0] : nullptr, ex_dummy, &flags[w],
-                                                     &flags[imports ? w + 1 : w], j + 1, j == p.J - 1, p.error,
-                                                     p.timeout_ticks)
-                            : 0u;
+        cnt = rows_here > 0 ? stream_band<D, true, WPL>(a, r0, rows_here, tile * tile_words(WPL)) : 0u;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         {
             const long long tr_e = (long long)__builtin_amdgcn_s_memrealtime();
@@ -1219,28 +535,21 @@ int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_sk
 
 // nw = waves per workgroup (one workgroup per CU): 4, 8 or 16; 0 = default.
 template <typename F>
-static hipError_t dispatch_persist(int depth, int wpl, int nw, bool diag, bool wt, F &&f) {
+static hipError_t dispatch_persist(int depth, int wpl, int nw, F &&f) {
     if (nw == 0) nw = persist_waves(depth, wpl);
-#define GOL_PCASE(D, WP, NW)                                                                           \
-    if (!diag && depth == D && wpl == WP && nw == NW)                                                  \
-        return wt ? f(gol_persist_kernel<D, WP, NW, false, true>, NW) : f(gol_persist_kernel<D, WP, NW, false, false>, NW);
-#define GOL_DCASE(D, WP, NW) \
-    if (diag && depth == D && wpl == WP && nw == NW) return f(gol_persist_kernel<D, WP, NW, true>, NW);
+#define GOL_PCASE(D, WP, NW) \
+    if (depth == D && wpl == WP && nw == NW) return f(gol_persist_kernel<D, WP, NW>, NW);
     GOL_PCASE(4, 1, 16) GOL_PCASE(8, 1, 16) GOL_PCASE(16, 1, 16) GOL_PCASE(32, 1, 8) GOL_PCASE(4, 2, 16)
-    GOL_PCASE(8, 2, 16) GOL_PCASE(16, 2, 8)
-    GOL_PCASE(8, 1, 8) GOL_PCASE(16, 1, 8) GOL_PCASE(8, 2, 8)
-    GOL_DCASE(8, 1, 4) GOL_DCASE(8, 1, 8) GOL_DCASE(16, 1, 4) GOL_DCASE(16, 1, 8)
-    GOL_DCASE(32, 1, 4) GOL_DCASE(8, 2, 4) GOL_DCASE(8, 2, 8) GOL_DCASE(16, 2, 4)
+    GOL_PCASE(8, 2, 16) GOL_PCASE(16, 2, 8) GOL_PCASE(8, 1, 8) GOL_PCASE(16, 1, 8) GOL_PCASE(8, 2, 8)
 #undef GOL_PCASE
-#undef GOL_DCASE
     return hipErrorInvalidValue;
 }
 
 int persist_waves_for(int depth, int wpl) { return persist_waves(depth, wpl); }
 
-int persist_blocks_per_cu(int depth, int wpl, int nw, bool diag) {
+int persist_blocks_per_cu(int depth, int wpl, int nw) {
     int b = 0;
-    hipError_t e = dispatch_persist(depth, wpl, nw, diag, false, [&](auto kern, int n) {
+    hipError_t e = dispatch_persist(depth, wpl, nw, [&](auto kern, int n) {
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 64 * n, 0);
     });
     return e == hipSuccess ? b : 0;
@@ -1277,86 +586,8 @@ bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, int units, Pers
     return found;
 }
 
-// (depth, wpl, stage waves NWS, pipelines P) of the stage-split kernel K1s.
-template <typename F>
-static hipError_t dispatch_pipe(int depth, int wpl, int nws, int np, int gt, F &&f) {
-#define GOL_SCASE(D, WP, NS, NP, GT) \
-    if (depth == D && wpl == WP && nws == NS && np == NP && gt == GT) return f(gol_pipe_kernel<D, WP, NS, NP, GT>, NS * NP);
-    GOL_SCASE(16, 1, 4, 4, 1) GOL_SCASE(16, 1, 4, 4, 2) GOL_SCASE(16, 1, 4, 4, 4)
-    GOL_SCASE(16, 1, 2, 8, 1) GOL_SCASE(16, 1, 2, 8, 2) GOL_SCASE(16, 1, 2, 8, 4)
-    GOL_SCASE(32, 1, 4, 4, 1) GOL_SCASE(32, 1, 4, 4, 2) GOL_SCASE(32, 1, 4, 4, 4)
-    GOL_SCASE(32, 1, 8, 2, 1) GOL_SCASE(32, 1, 8, 2, 2) GOL_SCASE(32, 1, 8, 2, 4)
-    GOL_SCASE(16, 2, 4, 4, 1) GOL_SCASE(16, 2, 4, 4, 2) GOL_SCASE(16, 2, 2, 8, 1) GOL_SCASE(16, 2, 2, 8, 2)
-    GOL_SCASE(32, 2, 4, 4, 1) GOL_SCASE(32, 2, 4, 4, 2) GOL_SCASE(8, 1, 2, 8, 1) GOL_SCASE(8, 2, 2, 8, 1)
-    GOL_SCASE(16, 1, 8, 2, 1) GOL_SCASE(16, 1, 8, 2, 2)
-#undef GOL_SCASE
-    return hipErrorInvalidValue;
-}
-
-int pipe_blocks_per_cu(int depth, int wpl, int nws, int np, int gt) {
-    int b = 0;
-    hipError_t e = dispatch_pipe(depth, wpl, nws, np, gt, [&](auto kern, int n) {
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 64 * n, 0);
-    });
-    return e == hipSuccess ? b : 0;
-}
-
-hipError_t launch_pipe(const PersistArgs &p, int depth, int wpl, int nws, int gt, hipStream_t s) {
-    return dispatch_pipe(depth, wpl, nws, p.nw / nws, gt, [&](auto kern, int n) {
-        hipLaunchKernelGGL(kern, dim3(p.cols * p.wg_y), dim3(64 * n), 0, s, p);
-        return hipGetLastError();
-    });
-}
-
-template <typename F>
-static hipError_t dispatch_k1n(int depth, int wpl, int nw, F &&f) {
-#define GOL_NCASE(D, WP, NW) \
-    if (depth == D && wpl == WP && nw == NW) return f(gol_k1n_kernel<D, WP, NW>, NW);
-    GOL_NCASE(8, 1, 8) GOL_NCASE(16, 1, 8) GOL_NCASE(16, 1, 16) GOL_NCASE(32, 1, 8) GOL_NCASE(8, 2, 8)
-    GOL_NCASE(16, 2, 8) GOL_NCASE(8, 1, 16) GOL_NCASE(8, 2, 16)
-#undef GOL_NCASE
-    return hipErrorInvalidValue;
-}
-
-int k1n_blocks_per_cu(int depth, int wpl, int nw) {
-    int b = 0;
-    hipError_t e = dispatch_k1n(depth, wpl, nw, [&](auto kern, int n) {
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 64 * n, 0);
-    });
-    return e == hipSuccess ? b : 0;
-}
-
-bool plan_k1n(int Ww, int rows, int depth, int cus, int wpl, int nw, PersistArgs *p) {
-    const int tiles_x = tb_tiles(Ww, wpl);
-    const int cols = tiles_x;  // one tile per workgroup, nw stacked bands
-    const int wg_y = std::min(cus / cols, rows / (nw * (2 * depth + 3)));
-    if (wg_y < 1 || nw < 2) return false;
-    // workgroup rows R = (nw - 1) S + Sb with Sb = S - depth + 1 (balanced bottom band)
-    const int R = (rows + wg_y - 1) / wg_y;
-    const int S = (R + depth - 1 + nw - 1) / nw;
-    const int Sb = std::max(1, S - depth + 1);
-    if (S < 2 * depth + 3) return false;
-    if ((long)((nw - 1) * S + Sb) * wg_y < rows) return false;
-    p->wg_tx = 1;
-    p->wg_sy = nw;
-    p->cols = cols;
-    p->wg_y = wg_y;
-    p->S = S;
-    p->Sb = Sb;
-    p->tiles_x = tiles_x;
-    p->nw = nw;
-    return true;
-}
-
-hipError_t launch_k1n(const PersistArgs &p, int depth, int wpl, hipStream_t s) {
-    return dispatch_k1n(depth, wpl, p.nw, [&](auto kern, int nw) {
-        hipLaunchKernelGGL(kern, dim3(p.cols * p.wg_y), dim3(64 * nw), 0, s, p);
-        return hipGetLastError();
-    });
-}
-
-hipError_t launch_persist(const PersistArgs &p, int depth, int wpl, bool diag, bool wt, hipStream_t s) {
-    return dispatch_persist(depth, wpl, p.nw, diag, wt, [&](auto kern, int nw) {
+hipError_t launch_persist(const PersistArgs &p, int depth, int wpl, hipStream_t s) {
+    return dispatch_persist(depth, wpl, p.nw, [&](auto kern, int nw) {
         hipLaunchKernelGGL(kern, dim3(p.cols * p.wg_y), dim3(64 * nw), 0, s, p);
         return hipGetLastError();
     });

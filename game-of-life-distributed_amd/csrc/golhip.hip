@@ -90,13 +90,7 @@ struct golhip {
     int wpl_opt = 0;            // option "wpl": words per lane (0 = auto, 1, 2)
     int persist_depth = 0;      // option "persist_depth" (0: tb_depth)
     int persist_waves = 0;      // option "persist_waves": waves per workgroup (0: default)
-    int stage_waves = 0;        // option "stage_waves": >= 2 selects K1s (waves per pipeline)
-    int pipe_units = 0;         // option "pipe_units": K1s pipelines per workgroup (0: 16 / stage_waves)
     unsigned long long *d_trace = nullptr;  // option "trace": persistent-kernel diagnostics
-    bool k1n = false;           // option "k1n": bands without the vertical halo (K1n)
-    bool persist_wt = false;    // option "persist_wt": write-through output stores in K1p
-    bool diag = false;          // option "diag": diagonal stage schedule in K1p
-    int pipe_groups = 1;        // option "pipe_groups": K1s 3-row groups per tick (1, 2, 4)
     unsigned *d_sync = nullptr; // persistent kernel: [0] error, [1..] progress per workgroup
     unsigned *h_err = nullptr;  // pinned copy of the error word
     bool persist_pending = false;
@@ -200,14 +194,44 @@ int largest_depth(int64_t want) {
     return 1;
 }
 
-// Words per lane of the step kernels: 2 halves the DPP work per word but
-// quantises tiles at 124 words instead of 62; auto picks the variant that
-// computes fewer words (ties -> 2).
+// Relative rate of a (words per lane, waves per workgroup) choice for the
+// persistent torus kernel: stored fraction of the computed tile words x band
+// efficiency S / (S + 1.75 D) (pipeline fill, see stream_band) x occupancy /
+// VALU slots per word-turn (wpl 1: 9 LUT + 2 half-rate shifts + 2 half-rate
+// DPP = 17 slots; wpl 2 interleaved: 9 + 1 + 1 half-rate = 13).  Fitted to
+// the round-1c sweeps (profiles/r1c): 16384^2 -> wpl 1 with 8 waves,
+// 65536^2 -> wpl 2.
+double plan_rate(golhip_t h, int wpl, int nw, int depth) {
+    const int tiles = golk::tb_tiles(h->Ww, wpl);
+    const double util = (double)h->Ww / (tiles * 62.0 * wpl);
+    const double S = (double)h->rows * tiles / std::max(1.0, (double)h->cu_count * nw);
+    const double occ = nw >= 16 ? 1.0 : 0.95;
+    return util * S / (S + 1.75 * depth) * occ / (wpl == 2 ? 13.0 : 17.0);
+}
+
+int default_depth(golhip_t h, int wpl) { return largest_depth(std::min(h->tb_depth, golk::max_depth_for(wpl))); }
+
+// Waves per workgroup of the persistent kernel: the option, or the better of
+// 16 (4 per SIMD: hides VALU latency) and 8 (taller bands: less fill).
+int persist_nw_for(golhip_t h, int depth, int wpl) {
+    if (h->persist_waves > 0) return h->persist_waves;
+    const int def = golk::persist_waves_for(depth, wpl);
+    if (def == 16 && plan_rate(h, wpl, 8, depth) > plan_rate(h, wpl, 16, depth)) return 8;
+    return def;
+}
+
+// Words per lane of the step kernels: 2 (interleaved pair layout) cuts the
+// shift work per word but quantises tiles at 124 words and halves the band
+// height; the option, or whichever plan_rate prefers.
 int wpl_for(golhip_t h) {
     if (h->W % 64 != 0) return 1;
     if (h->wpl_opt == 1 || h->wpl_opt == 2) return h->wpl_opt;
-    const long w1 = (long)golk::tb_tiles(h->Ww, 1) * 64, w2 = (long)golk::tb_tiles(h->Ww, 2) * 128;
-    return w2 <= w1 ? 2 : 1;
+    auto best = [&](int wpl) {
+        const int d = default_depth(h, wpl);
+        const int def = golk::persist_waves_for(d, wpl);
+        return std::max(plan_rate(h, wpl, def, d), def == 16 ? plan_rate(h, wpl, 8, d) : 0.0);
+    };
+    return best(2) >= best(1) ? 2 : 1;
 }
 
 // The wpl = 2 step kernels run on the interleaved pair layout; every other
@@ -398,32 +422,16 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     *rc = GOLHIP_OK;
     if (!h->persistent || h->W % 32 != 0 || !h->torus()) return 0;
     const int wpl = wpl_for(h);
-    const int nws = h->stage_waves;  // >= 2: stage-split kernel K1s
-    const int max_d = nws >= 2 ? GOLHIP_MAX_TB_DEPTH : golk::max_depth_for(wpl);
-    const int depth = largest_depth(std::min(h->persist_depth > 0 ? h->persist_depth : h->tb_depth, max_d));
+    const int depth = largest_depth(std::min(h->persist_depth > 0 ? h->persist_depth : h->tb_depth,
+                                             golk::max_depth_for(wpl)));
     if (depth < 4) return 0;
     const int64_t J = left / depth;
     if (J < 2) return 0;
-    int nw = 0, units = 0;
+    const int nw = persist_nw_for(h, depth, wpl);
+    if (golk::persist_blocks_per_cu(depth, wpl, nw) < 1) return 0;
     golk::PersistArgs p{};
-    const bool k1n = h->k1n && nws < 2 && !h->diag;
-    if (k1n) {
-        nw = h->persist_waves > 0 ? h->persist_waves : 8;
-        if (golk::k1n_blocks_per_cu(depth, wpl, nw) < 1) return 0;
-        if (!golk::plan_k1n(h->Ww, h->rows, depth, h->cu_count, wpl, nw, &p)) return 0;
-    } else if (nws >= 2) {
-        units = h->pipe_units > 0 ? h->pipe_units : 16 / nws;
-        if (depth % nws != 0 || golk::pipe_blocks_per_cu(depth, wpl, nws, units, h->pipe_groups) < 1) return 0;
-        nw = nws * units;
-    } else {
-        nw = h->persist_waves > 0 ? h->persist_waves : golk::persist_waves_for(depth, wpl);
-        if (golk::persist_blocks_per_cu(depth, wpl, nw, h->diag) < 1) return 0;
-        units = nw;
-    }
-    if (!k1n) {
-        if (!golk::plan_persist(h->Ww, h->rows, depth, h->cu_count, wpl, units, &p)) return 0;
-        p.nw = nw;
-    }
+    if (!golk::plan_persist(h->Ww, h->rows, depth, h->cu_count, wpl, nw, &p)) return 0;
+    p.nw = nw;
     if (!h->d_sync) {
         if (hipMalloc(&h->d_sync, (size_t)(h->cu_count + 2) * sizeof(unsigned)) != hipSuccess ||
             hipHostMalloc(&h->h_err, sizeof(unsigned), hipHostMallocDefault) != hipSuccess) {
@@ -454,9 +462,7 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
         if (e0 && e1) e = hipEventRecord(e0, h->stream);
     }
     if (e == hipSuccess)
-        e = k1n         ? golk::launch_k1n(p, depth, wpl, h->stream)
-            : nws >= 2  ? golk::launch_pipe(p, depth, wpl, nws, h->pipe_groups, h->stream)
-                        : golk::launch_persist(p, depth, wpl, h->diag, h->persist_wt, h->stream);
+        e = golk::launch_persist(p, depth, wpl, h->stream);
     if (e == hipSuccess && e1) {
         e = hipEventRecord(e1, h->stream);
         h->ev_pending.push_back({e0, e1, true});
@@ -660,12 +666,6 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         h->persist_waves = (int)value;
         return GOLHIP_OK;
     }
-    if (!strcmp(key, "stage_waves")) {
-        if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
-            return fail(GOLHIP_EINVAL, "stage_waves %lld not in {0,1,2,4,8}", (long long)value);
-        h->stage_waves = (int)value;
-        return GOLHIP_OK;
-    }
     if (!strcmp(key, "trace")) {
         if (value && !h->d_trace) {
             if (hipMalloc(&h->d_trace, kTraceWords * sizeof(unsigned long long)) != hipSuccess)
@@ -673,28 +673,6 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
             if (hipMemset(h->d_trace, 0, kTraceWords * sizeof(unsigned long long)) != hipSuccess)
                 return fail(GOLHIP_EHIP, "trace buffer memset");
         }
-        return GOLHIP_OK;
-    }
-    if (!strcmp(key, "k1n")) {
-        h->k1n = value != 0;
-        return GOLHIP_OK;
-    }
-    if (!strcmp(key, "persist_wt")) {
-        h->persist_wt = value != 0;
-        return GOLHIP_OK;
-    }
-    if (!strcmp(key, "diag")) {
-        h->diag = value != 0;
-        return GOLHIP_OK;
-    }
-    if (!strcmp(key, "pipe_groups")) {
-        if (value != 1 && value != 2 && value != 4) return fail(GOLHIP_EINVAL, "pipe_groups %lld", (long long)value);
-        h->pipe_groups = (int)value;
-        return GOLHIP_OK;
-    }
-    if (!strcmp(key, "pipe_units")) {
-        if (value < 0 || value > 16) return fail(GOLHIP_EINVAL, "pipe_units %lld", (long long)value);
-        h->pipe_units = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "fill_skip")) {

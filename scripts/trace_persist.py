@@ -1,5 +1,5 @@
 """Persistent-kernel time split (band compute vs neighbour wait) per variant.
-usage: python scripts/trace_persist.py --size 16384 --variants "k1n=0;k1n=1" """
+usage: python scripts/trace_persist.py --size 16384 --variants "persist_waves=8;persist_waves=16" """
 import argparse
 import json
 import os
@@ -21,7 +21,7 @@ with golhip.Board(a.size, a.size, timing=True) as b:
     b.fill_random(0x5EED0001)
     for d in map(int, a.depths.split(",")):
         for v in [x for x in a.variants.split(";") if x] or [""]:
-            opts = {"wpl": 0, "persistent": 1, "persist_waves": 0, "k1n": 0, "stage_waves": 0, "diag": 0}
+            opts = {"wpl": 0, "persistent": 1, "persist_waves": 0}
             opts.update({k: int(x) for k, x in (kv.split("=") for kv in v.split(",") if kv)})
             for k, x in opts.items():
                 b.set_option(k, x)
