@@ -9,7 +9,9 @@ namespace golk {
 // Physical board buffers hold `rows + 2*kHalo` rows of Ww uint32 words; local
 // row i lives at physical row kHalo + i.  Halo rows are filled by the ring
 // exchange (strip mode) and unused in torus mode.
-constexpr int kHalo = 32;        // == GOLHIP_MAX_TB_DEPTH
+// Halo rows above and below a strip buffer (== GOLHIP_HALO_ROWS): deeper than
+// one launch (GOLHIP_MAX_TB_DEPTH) so one exchange can feed several launches.
+constexpr int kHalo = 64;
 constexpr int kWave = 64;
 constexpr int kTileValid = 62;   // lanes per wavefront tile that are stored (lanes 1..62)
 

@@ -115,7 +115,9 @@ struct golhip {
 
     // ring
     ncclComm_t comm = nullptr;
+    bool force_halo = false;    // option "force_halo": one-rank RCCL ring on a whole board (tests)
     int nranks = 1, rank = 0;
+    int ring_rows = 0;          // smallest strip of the ring (every rank plans from it)
 
     // measurement
     std::vector<hipEvent_t> ev_pool;
@@ -194,6 +196,11 @@ int largest_depth(int64_t want) {
     return 1;
 }
 
+// Rows the launch schedule (depth, exchange depth, words per lane) is derived
+// from: in a multi-rank ring every rank must pick the same values, so they
+// all use the ring's smallest strip.
+int sched_rows(golhip_t h) { return (h->comm && h->nranks > 1 && h->ring_rows > 0) ? h->ring_rows : h->rows; }
+
 // Relative rate of a (words per lane, waves per workgroup) choice for the
 // persistent torus kernel: stored fraction of the computed tile words x band
 // efficiency S / (S + 1.75 D) (pipeline fill, see stream_band) x occupancy /
@@ -204,7 +211,7 @@ int largest_depth(int64_t want) {
 double plan_rate(golhip_t h, int wpl, int nw, int depth) {
     const int tiles = golk::tb_tiles(h->Ww, wpl);
     const double util = (double)h->Ww / (tiles * 62.0 * wpl);
-    const double S = (double)h->rows * tiles / std::max(1.0, (double)h->cu_count * nw);
+    const double S = (double)sched_rows(h) * tiles / std::max(1.0, (double)h->cu_count * nw);
     const double occ = nw >= 16 ? 1.0 : 0.95;
     return util * S / (S + 1.75 * depth) * occ / (wpl == 2 ? 13.0 : 17.0);
 }
@@ -256,7 +263,7 @@ int loaded_canonical(golhip_t h) {
 int next_depth(golhip_t h, int64_t remaining, bool halo) {
     if (h->W % 32 != 0) return 1;  // generic kernel: one turn per launch
     int64_t cap = std::min<int64_t>(std::min(h->tb_depth, golk::max_depth_for(wpl_for(h))), remaining);
-    if (halo) cap = std::min<int64_t>(cap, h->rows);
+    if (halo) cap = std::min<int64_t>(cap, sched_rows(h));
     return largest_depth(cap);
 }
 
@@ -341,22 +348,75 @@ void plan(int strip_rows, int nranks, int rank, int depth, int Ww, golhip_halo_p
     p->bytes = (int64_t)depth * Ww * 4;
 }
 
-// RCCL halo exchange for a launch of `depth` turns.  Posting order pairs
-// correctly even when prev == next (2 ranks): on every A->B channel the
-// first message is A's top rows (B's bottom halo), the second A's bottom rows.
-int exchange_rccl(golhip_t h, int depth) {
+// RCCL halo exchange for a launch of `depth` turns on stream `st`.  Posting
+// order pairs correctly even when prev == next (2 ranks) or both are this
+// rank (one-rank ring, option "force_halo"): on every A->B channel the first
+// message is A's top rows (B's bottom halo), the second A's bottom rows.
+int exchange_rccl(golhip_t h, int depth, hipStream_t st) {
     golhip_halo_plan_t p;
     plan(h->rows, h->nranks, h->rank, depth, h->Ww, &p);
     uint32_t *b = h->buf[h->cur];
     const size_t n = (size_t)depth * h->Ww;
     NCCL_OR_FAIL(ncclGroupStart());
-    NCCL_OR_FAIL(ncclSend(b + (int64_t)p.send_up_row * h->Ww, n, ncclUint32, p.prev_rank, h->comm, h->stream));
-    NCCL_OR_FAIL(ncclRecv(b + (int64_t)p.recv_bottom_row * h->Ww, n, ncclUint32, p.next_rank, h->comm, h->stream));
-    NCCL_OR_FAIL(ncclSend(b + (int64_t)p.send_down_row * h->Ww, n, ncclUint32, p.next_rank, h->comm, h->stream));
-    NCCL_OR_FAIL(ncclRecv(b + (int64_t)p.recv_top_row * h->Ww, n, ncclUint32, p.prev_rank, h->comm, h->stream));
+    NCCL_OR_FAIL(ncclSend(b + (int64_t)p.send_up_row * h->Ww, n, ncclUint32, p.prev_rank, h->comm, st));
+    NCCL_OR_FAIL(ncclRecv(b + (int64_t)p.recv_bottom_row * h->Ww, n, ncclUint32, p.next_rank, h->comm, st));
+    NCCL_OR_FAIL(ncclSend(b + (int64_t)p.send_down_row * h->Ww, n, ncclUint32, p.next_rank, h->comm, st));
+    NCCL_OR_FAIL(ncclRecv(b + (int64_t)p.recv_top_row * h->Ww, n, ncclUint32, p.prev_rank, h->comm, st));
     NCCL_OR_FAIL(ncclGroupEnd());
     h->halo_bytes += 2 * (int64_t)n * 4;
     return GOLHIP_OK;
+}
+
+// Launch the step kernel for output rows [lo, hi) of this handle (halos, if
+// used, already in place); `alive` (nullable) accumulates their popcount.
+// No bookkeeping: see finish_launch.
+int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int lo, int hi) {
+    const hipStream_t st = h->stream;
+    golk::StepArgs a = step_args(h, alive, halo);
+    if (lo != 0 || hi != h->rows) {  // other row range (halo mode only): shift the row maps
+        a.rows_out = hi - lo;
+        a.dst_base = kHalo + lo;
+        a.in.off = kHalo + lo;
+    }
+    const int wpl = wpl_for(h);
+    if (a.rows_out == h->rows) {
+        a.rows_per_wave = rows_per_wave_for(h, depth);
+    } else if (h->rows_per_wave > 0) {
+        a.rows_per_wave = h->rows_per_wave;
+    } else {
+        const int slots = h->cu_count * golk::tb_blocks_per_cu(depth, wpl) * 4;
+        a.rows_per_wave = golk::auto_rows_per_wave(h->Ww, a.rows_out, depth, std::max(slots, 1), h->fill_skip, wpl);
+    }
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (h->flags & GOLHIP_FLAG_TIMING) {
+        e0 = take_event(h);
+        e1 = take_event(h);
+        if (!e0 || !e1) return fail(GOLHIP_EHIP, "hipEventCreate failed");
+        HIP_OR_FAIL(hipEventRecord(e0, st));
+    }
+    hipError_t e;
+    if (h->W % 32 == 0)
+        e = golk::launch_step_tb(a, depth, st, h->fill_skip, wpl);
+    else
+        e = golk::launch_step_generic(a, st);
+    if (e != hipSuccess) return fail(GOLHIP_EHIP, "step launch: %s", hipGetErrorString(e));
+    if (e1) {
+        HIP_OR_FAIL(hipEventRecord(e1, st));
+        h->ev_pending.push_back({e0, e1, false});
+        if (h->ev_pending.size() >= 4096) {
+            int rc = drain_events(h);
+            if (rc) return rc;
+        }
+    }
+    h->step_launches++;
+    return GOLHIP_OK;
+}
+
+void finish_launch(golhip_t h, int depth, bool count) {
+    h->cur ^= 1;
+    h->turns += depth;
+    h->step_turns += depth;
+    if (count) h->alive_turn = h->turns;
 }
 
 // One step launch of `depth` turns (halos already in place).
@@ -366,34 +426,30 @@ int launch_depth(golhip_t h, int depth, bool count, bool halo) {
         alive = h->d_scalars;
         HIP_OR_FAIL(hipMemsetAsync(alive, 0, sizeof(unsigned long long), h->stream));
     }
-    golk::StepArgs a = step_args(h, alive, halo);
-    a.rows_per_wave = rows_per_wave_for(h, depth);
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (h->flags & GOLHIP_FLAG_TIMING) {
-        e0 = take_event(h);
-        e1 = take_event(h);
-        if (!e0 || !e1) return fail(GOLHIP_EHIP, "hipEventCreate failed");
-        HIP_OR_FAIL(hipEventRecord(e0, h->stream));
+    if (int rc = launch_rows(h, depth, alive, halo, 0, h->rows)) return rc;
+    finish_launch(h, depth, count);
+    return GOLHIP_OK;
+}
+
+// Halo mode with deep halos: one exchange of k * depth rows feeds k launches
+// of `depth` turns.  Launch i (0-based) steps rows [-ext, rows + ext) with
+// ext = (k - 1 - i) * depth, so it also rebuilds the next launch's halo rows
+// from the wider halo (the trapezoid: output row -ext needs input rows
+// -ext - depth .. , all inside the k * depth received rows).  The extension
+// costs 2 * ext extra rows per launch; it saves k - 1 of every k exchanges.
+int halo_launches(int rows, int depth, int64_t left) {
+    const int64_t k = std::min<int64_t>({(int64_t)kHalo / depth, left / depth, (int64_t)rows / depth});
+    return (int)std::max<int64_t>(1, k);
+}
+
+int launch_ext(golhip_t h, int depth, bool count, int ext) {
+    unsigned long long *alive = nullptr;
+    if (count) {
+        alive = h->d_scalars;
+        HIP_OR_FAIL(hipMemsetAsync(alive, 0, sizeof(unsigned long long), h->stream));
     }
-    hipError_t e;
-    if (h->W % 32 == 0)
-        e = golk::launch_step_tb(a, depth, h->stream, h->fill_skip, wpl_for(h));
-    else
-        e = golk::launch_step_generic(a, h->stream);
-    if (e != hipSuccess) return fail(GOLHIP_EHIP, "step launch: %s", hipGetErrorString(e));
-    if (e1) {
-        HIP_OR_FAIL(hipEventRecord(e1, h->stream));
-        h->ev_pending.push_back({e0, e1, false});
-        if (h->ev_pending.size() >= 4096) {
-            int rc = drain_events(h);
-            if (rc) return rc;
-        }
-    }
-    h->cur ^= 1;
-    h->turns += depth;
-    h->step_launches++;
-    h->step_turns += depth;
-    if (count) h->alive_turn = h->turns;
+    if (int rc = launch_rows(h, depth, alive, true, -ext, h->rows + ext)) return rc;
+    finish_launch(h, depth, count);
     return GOLHIP_OK;
 }
 
@@ -675,6 +731,10 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         }
         return GOLHIP_OK;
     }
+    if (!strcmp(key, "force_halo")) {
+        h->force_halo = value != 0;
+        return GOLHIP_OK;
+    }
     if (!strcmp(key, "fill_skip")) {
         h->fill_skip = value != 0;
         for (int &c : h->auto_rpw) c = 0;
@@ -704,13 +764,35 @@ int golhip_comm_init(golhip_t h, const uint8_t id[GOLHIP_UNIQUE_ID_BYTES], int32
     NCCL_OR_FAIL(ncclCommInitRank(&h->comm, nranks, u, rank));
     h->nranks = nranks;
     h->rank = rank;
+    // agree on the schedule: the smallest strip of the ring
+    int32_t *d_rows = nullptr;
+    HIP_OR_FAIL(hipMalloc(&d_rows, sizeof(int32_t)));
+    int32_t rows = h->rows;
+    hipError_t e = hipMemcpy(d_rows, &rows, sizeof rows, hipMemcpyHostToDevice);
+    ncclResult_t nr = e == hipSuccess ? ncclAllReduce(d_rows, d_rows, 1, ncclInt32, ncclMin, h->comm, h->stream) : ncclSuccess;
+    if (e == hipSuccess && nr == ncclSuccess) e = hipStreamSynchronize(h->stream);
+    if (e == hipSuccess && nr == ncclSuccess) e = hipMemcpy(&rows, d_rows, sizeof rows, hipMemcpyDeviceToHost);
+    (void)hipFree(d_rows);
+    if (nr != ncclSuccess) return fail(GOLHIP_ERCCL, "ncclAllReduce(strip rows): %s", ncclGetErrorString(nr));
+    if (e != hipSuccess) return fail(GOLHIP_EHIP, "strip rows: %s", hipGetErrorString(e));
+    h->ring_rows = rows;
+    return GOLHIP_OK;
+}
+
+int golhip_halo_schedule(int32_t strip_rows, int32_t tb_depth, int64_t turns_left, int32_t *depth,
+                         int32_t *launches) {
+    if (!depth || !launches || strip_rows <= 0 || tb_depth < 1 || tb_depth > GOLHIP_MAX_TB_DEPTH || turns_left < 1)
+        return fail(GOLHIP_EINVAL, "bad halo schedule request");
+    const int d = largest_depth(std::min<int64_t>({(int64_t)tb_depth, turns_left, (int64_t)strip_rows}));
+    *depth = d;
+    *launches = halo_launches(strip_rows, d, turns_left);
     return GOLHIP_OK;
 }
 
 int golhip_halo_plan(int32_t width, int32_t strip_rows, int32_t nranks, int32_t rank, int32_t depth,
                      golhip_halo_plan_t *out) {
     if (!out || width <= 0 || strip_rows <= 0 || nranks < 1 || rank < 0 || rank >= nranks || depth < 1 ||
-        depth > GOLHIP_MAX_TB_DEPTH || depth > strip_rows)
+        depth > GOLHIP_HALO_ROWS || depth > strip_rows)
         return fail(GOLHIP_EINVAL, "bad halo plan request");
     plan(strip_rows, nranks, rank, depth, (width + 31) / 32, out);
     return GOLHIP_OK;
@@ -774,7 +856,9 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     h->flips_valid = false;
     int64_t left = nturns;
     const int64_t tail = want_flips ? 1 : 0;
-    const bool halo = h->nranks > 1;
+    // halo mode: row strips of a multi-rank ring, or (option force_halo) a
+    // whole board run as a one-rank RCCL ring
+    const bool halo = h->comm && (h->nranks > 1 || h->force_halo);
     if (!halo) {
         int rc = GOLHIP_OK;
         left -= try_persist(h, left - tail, tail == 0, &rc);
@@ -782,14 +866,21 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     }
     while (left > tail) {
         const int d = next_depth(h, left - tail, halo);
-        if (halo)
-            if (int rc = exchange_rccl(h, d)) return rc;
-        if (int rc = launch_depth(h, d, left - d == 0, halo)) return rc;
-        left -= d;
+        if (!halo) {
+            if (int rc = launch_depth(h, d, left - d == 0, false)) return rc;
+            left -= d;
+            continue;
+        }
+        const int k = halo_launches(sched_rows(h), d, left - tail);
+        if (int rc = exchange_rccl(h, k * d, h->stream)) return rc;
+        for (int i = 0; i < k; ++i) {
+            if (int rc = launch_ext(h, d, left - d == 0, (k - 1 - i) * d)) return rc;
+            left -= d;
+        }
     }
     if (want_flips && nturns > 0) {
         if (halo)
-            if (int rc = exchange_rccl(h, 1)) return rc;
+            if (int rc = exchange_rccl(h, 1, h->stream)) return rc;
         if (int rc = launch_depth(h, 1, true, halo)) return rc;
         if (int rc = start_flips(h)) return rc;
     }
@@ -823,7 +914,11 @@ int golhip_group_step(golhip_t *hs, int32_t n, int64_t nturns) {
         int d = GOLHIP_MAX_TB_DEPTH;
         for (int i = 0; i < n; ++i) d = std::min(d, next_depth(hs[i], left, n > 1));
         d = largest_depth(d);
+        int k = 1;
         if (n > 1) {
+            k = kHalo / d;
+            for (int i = 0; i < n; ++i) k = std::min(k, halo_launches(hs[i]->rows, d, left));
+            const int x = k * d;  // rows exchanged
             for (int i = 0; i < n && !rc; ++i) {
                 HIP_RC(hipSetDevice(hs[i]->device));
                 HIP_RC(hipEventRecord(ready[i], hs[i]->stream));
@@ -831,14 +926,14 @@ int golhip_group_step(golhip_t *hs, int32_t n, int64_t nturns) {
             for (int i = 0; i < n && !rc; ++i) {
                 golhip *me = hs[i], *prev = hs[(i - 1 + n) % n], *next = hs[(i + 1) % n];
                 golhip_halo_plan_t p;
-                plan(me->rows, n, i, d, me->Ww, &p);
+                plan(me->rows, n, i, x, me->Ww, &p);
                 HIP_RC(hipSetDevice(me->device));
                 HIP_RC(hipStreamWaitEvent(me->stream, ready[(i - 1 + n) % n], 0));
                 HIP_RC(hipStreamWaitEvent(me->stream, ready[(i + 1) % n], 0));
                 const size_t bytes = (size_t)p.bytes;
-                // top halo <- prev's last d rows; bottom halo <- next's first d rows
+                // top halo <- prev's last x rows; bottom halo <- next's first x rows
                 uint32_t *mb = me->buf[me->cur];
-                const uint32_t *pb = prev->buf[prev->cur] + (int64_t)(kHalo + prev->rows - d) * prev->Ww;
+                const uint32_t *pb = prev->buf[prev->cur] + (int64_t)(kHalo + prev->rows - x) * prev->Ww;
                 const uint32_t *nb = next->buf[next->cur] + (int64_t)kHalo * next->Ww;
                 HIP_RC(hipMemcpyPeerAsync(mb + (int64_t)p.recv_top_row * me->Ww, me->device, pb, prev->device, bytes,
                                           me->stream));
@@ -846,12 +941,27 @@ int golhip_group_step(golhip_t *hs, int32_t n, int64_t nturns) {
                                           bytes, me->stream));
                 me->halo_bytes += 2 * (int64_t)bytes;
             }
+            // a strip's second launch rewrites the buffer its neighbours copied
+            // from: every stream waits for its neighbours' copies first
+            for (int i = 0; i < n && !rc; ++i) {
+                HIP_RC(hipSetDevice(hs[i]->device));
+                HIP_RC(hipEventRecord(ready[i], hs[i]->stream));
+            }
+            for (int i = 0; i < n && !rc; ++i) {
+                HIP_RC(hipSetDevice(hs[i]->device));
+                HIP_RC(hipStreamWaitEvent(hs[i]->stream, ready[(i - 1 + n) % n], 0));
+                HIP_RC(hipStreamWaitEvent(hs[i]->stream, ready[(i + 1) % n], 0));
+            }
         }
-        for (int i = 0; i < n && !rc; ++i) {
-            HIP_RC(hipSetDevice(hs[i]->device));
-            if (!rc) rc = launch_depth(hs[i], d, left - d == 0, n > 1);
+        for (int j = 0; j < k && rc == GOLHIP_OK; ++j) {
+            for (int i = 0; i < n && !rc; ++i) {
+                HIP_RC(hipSetDevice(hs[i]->device));
+                if (rc) break;
+                rc = n > 1 ? launch_ext(hs[i], d, left - d == 0, (k - 1 - j) * d)
+                           : launch_depth(hs[i], d, left - d == 0, false);
+            }
+            left -= d;
         }
-        left -= d;
     }
     for (int i = 0; i < n; ++i) {
         HIP_RC(hipSetDevice(hs[i]->device));

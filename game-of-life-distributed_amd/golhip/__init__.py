@@ -21,6 +21,7 @@ GOLHIP_ERANGE = -4
 FLAG_TIMING = 0x1
 UNIQUE_ID_BYTES = 128
 MAX_TB_DEPTH = 32
+HALO_ROWS = 64  # GOLHIP_HALO_ROWS
 
 
 class GolHipError(RuntimeError):
@@ -97,6 +98,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "golhip_comm_init": ([H, ctypes.c_char_p, i32, i32], ctypes.c_int),
         "golhip_group_step": ([P(H), i32, i64], ctypes.c_int),
         "golhip_halo_plan": ([i32, i32, i32, i32, i32, P(HaloPlan)], ctypes.c_int),
+        "golhip_halo_schedule": ([i32, i32, i64, P(i32), P(i32)], ctypes.c_int),
         "golhip_load_bytes": ([H, ctypes.c_void_p], ctypes.c_int),
         "golhip_load_bits": ([H, ctypes.c_void_p], ctypes.c_int),
         "golhip_fill_random": ([H, u64], ctypes.c_int),
@@ -138,6 +140,13 @@ def halo_plan(width: int, strip_rows: int, nranks: int, rank: int, depth: int) -
     p = HaloPlan()
     _check(load().golhip_halo_plan(width, strip_rows, nranks, rank, depth, ctypes.byref(p)))
     return {k: getattr(p, k) for k, _ in p._fields_}
+
+
+def halo_schedule(strip_rows: int, tb_depth: int, turns_left: int) -> tuple[int, int]:
+    """(depth, launches) of the next halo exchange (golhip_halo_schedule)."""
+    d, k = ctypes.c_int32(), ctypes.c_int32()
+    _check(load().golhip_halo_schedule(strip_rows, tb_depth, turns_left, ctypes.byref(d), ctypes.byref(k)))
+    return d.value, k.value
 
 
 def unique_id() -> bytes:

@@ -50,6 +50,7 @@ extern "C" {
 
 #define GOLHIP_UNIQUE_ID_BYTES 128 /* == sizeof(ncclUniqueId)                 */
 #define GOLHIP_MAX_TB_DEPTH 32     /* max turns fused in one step launch      */
+#define GOLHIP_HALO_ROWS 64        /* halo rows above/below a strip buffer    */
 
 typedef struct golhip golhip;
 typedef golhip *golhip_t;
@@ -100,9 +101,14 @@ int golhip_set_tb_depth(golhip_t h, int32_t turns);
 int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
 /* Named engine options (kernel variants for A/B measurement); results never
  * depend on them.  "fill_skip" (default 1): skip pipeline-fill stage-rows;
- * "wpl" (default 0 = auto): words per lane, 1 or 2; "persistent" (default 1):
- * resident multi-super-step kernel for long runs on a whole torus;
- * "persist_depth" (default 0 = tb_depth): turns per super-step. */
+ * "wpl" (default 0 = auto): words per lane, 1 or 2 (2 runs on the
+ * interleaved pair layout, converted at the I/O boundary); "persistent"
+ * (default 1): resident multi-super-step kernel for long runs on a whole
+ * torus; "persist_depth" (default 0 = tb_depth): turns per super-step;
+ * "persist_waves" (0 = auto, 8 or 16): waves per persistent workgroup;
+ * "trace" (0): persistent-kernel diagnostics (golhip_persist_trace);
+ * "force_halo" (0): after golhip_comm_init with one rank, run a whole board
+ * through the multi-GPU path as a one-rank RCCL ring (tests, measurement). */
 int golhip_set_option(golhip_t h, const char *key, int64_t value);
 
 /* ---- multi-GPU -------------------------------------------------------- */
@@ -117,7 +123,8 @@ int golhip_comm_init(golhip_t h, const uint8_t id[GOLHIP_UNIQUE_ID_BYTES], int32
 int golhip_group_step(golhip_t *hs, int32_t n, int64_t nturns);
 
 /* Halo plan used by both transports (exposed for tests): rows this strip
- * sends up/down and receives for a launch of `depth` turns. */
+ * sends up/down and receives for an exchange of `depth` rows
+ * (1 <= depth <= min(GOLHIP_HALO_ROWS, strip_rows)). */
 typedef struct golhip_halo_plan {
     int32_t prev_rank, next_rank;   /* ring neighbours                       */
     int32_t send_up_row, recv_top_row;     /* physical buffer rows             */
@@ -127,6 +134,13 @@ typedef struct golhip_halo_plan {
 } golhip_halo_plan_t;
 int golhip_halo_plan(int32_t width, int32_t strip_rows, int32_t nranks, int32_t rank, int32_t depth,
                      golhip_halo_plan_t *out);
+/* Exchange schedule of a strip: each exchange moves launches * depth halo
+ * rows, then `launches` step launches of `depth` turns follow; launch i
+ * (0-based) steps rows [-e, strip_rows + e), e = (launches - 1 - i) * depth,
+ * so it rebuilds the next launch's halos from the deeper exchanged ones
+ * (kernel-side rows, W % 32 == 0; other widths run one turn per launch). */
+int golhip_halo_schedule(int32_t strip_rows, int32_t tb_depth, int64_t turns_left, int32_t *depth,
+                         int32_t *launches);
 
 /* ---- board I/O -------------------------------------------------------- */
 /* Load this handle's rows (height x width bytes, or its strip's rows). */

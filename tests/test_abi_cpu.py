@@ -43,11 +43,11 @@ def test_no_device_fails_loudly():
 
 
 @pytest.mark.parametrize("nranks", [1, 2, 3, 8])
-@pytest.mark.parametrize("depth", [1, 4, 32])
+@pytest.mark.parametrize("depth", [1, 4, 32, 64])
 def test_halo_plan_pairs_up(nranks, depth):
-    rows = 40
+    rows = 80
     plans = [golhip.halo_plan(2048, rows, nranks, r, depth) for r in range(nranks)]
-    halo = 32
+    halo = golhip.HALO_ROWS
     for r, p in enumerate(plans):
         assert p["prev_rank"] == (r - 1) % nranks and p["next_rank"] == (r + 1) % nranks
         assert p["rows"] == depth and p["bytes"] == depth * 2048 // 8
@@ -61,4 +61,15 @@ def test_halo_plan_rejects_depth_above_strip():
     with pytest.raises(golhip.GolHipError):
         golhip.halo_plan(64, 3, 2, 0, 4)
     with pytest.raises(golhip.GolHipError):
-        golhip.halo_plan(64, 64, 2, 0, 33)
+        golhip.halo_plan(64, 128, 2, 0, golhip.HALO_ROWS + 1)
+
+
+@pytest.mark.parametrize("rows,tb,left,want", [(16384, 16, 1000, (16, 4)), (16384, 16, 40, (16, 2)),
+                                               (16384, 32, 1000, (32, 2)), (40, 16, 1000, (16, 2)),
+                                               (10, 16, 1000, (8, 1)), (16384, 16, 7, (4, 1)),
+                                               (16384, 1, 100, (1, 64))])
+def test_halo_schedule(rows, tb, left, want):
+    """k launches of d turns per exchange of k * d <= GOLHIP_HALO_ROWS rows, k * d <= strip rows."""
+    d, k = golhip.halo_schedule(rows, tb, left)
+    assert (d, k) == want
+    assert d * k <= min(golhip.HALO_ROWS, max(rows, d)) and d * k <= left

@@ -1,11 +1,14 @@
 """Row-strip decomposition over torch.distributed (gloo, CPU): the N > 1 path.
 
-Each rank owns a strip of the 64x64 fixture torus and, before every fused
-launch of `depth` turns, exchanges `depth` halo rows with its ring neighbours
-exactly as libgolhip's RCCL path does (golhip.hip exchange_rccl): the rows to
-send / receive come from the library's own golhip_halo_plan, and the four p2p
-operations are posted in the same order (send up, recv bottom, send down,
-recv top), which is what makes 2 ranks (prev == next) pair correctly.  The
+Each rank owns a strip of the 64x64 fixture torus and follows libgolhip's
+RCCL path (golhip.hip golhip_step / exchange_rccl): the library's own
+golhip_halo_schedule says how deep the next exchange is (k launches of
+`depth` turns per exchange of k * depth rows), golhip_halo_plan which rows to
+send / receive, and the four p2p operations are posted in the same order
+(send up, recv bottom, send down, recv top), which is what makes 2 ranks
+(prev == next) pair correctly.  Launch i of an exchange steps the strip
+extended by (k - 1 - i) * depth rows on each side, rebuilding the next
+launch's halos from the deeper exchanged ones.  The
 turn computation uses the numpy oracle (test infrastructure), so the test
 checks the decomposition protocol, not the kernel; the GPU kernel's halo mode
 is covered by tests/test_gpu_parity.py::test_group_strips_*.
@@ -21,25 +24,13 @@ import torch.multiprocessing as mp
 
 golhip = pytest.importorskip("golhip")
 
-HALO = 32  # golk::kHalo
+HALO = golhip.HALO_ROWS  # golk::kHalo
 
 
 def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
-
-
-def _depth_schedule(nturns: int, tb: int, rows: int):
-    """golhip.hip next_depth(): largest power of two <= min(tb, left, rows)."""
-    left = nturns
-    while left > 0:
-        cap = min(tb, left, rows)
-        d = 1
-        while d * 2 <= cap:
-            d *= 2
-        yield d
-        left -= d
 
 
 def _worker(rank, world, port, splits, turns, tb, q):
@@ -58,24 +49,32 @@ def _worker(rank, world, port, splits, turns, tb, q):
     # physical strip buffer with HALO rows above and below, like the device buffer
     buf = np.zeros((rows + 2 * HALO, 64), dtype=np.uint8)
     buf[HALO:HALO + rows] = board[row0:row0 + rows]
-    for d in _depth_schedule(turns, tb, min(splits)):
-        p = g.halo_plan(64, rows, world, rank, d)
-        up = torch.from_numpy(buf[p["send_up_row"]:p["send_up_row"] + d].copy())
-        down = torch.from_numpy(buf[p["send_down_row"]:p["send_down_row"] + d].copy())
+    left = turns
+    while left > 0:
+        # every rank derives the same schedule from the smallest strip
+        d, k = g.halo_schedule(min(splits), tb, left)
+        x = k * d
+        p = g.halo_plan(64, rows, world, rank, x)
+        up = torch.from_numpy(buf[p["send_up_row"]:p["send_up_row"] + x].copy())
+        down = torch.from_numpy(buf[p["send_down_row"]:p["send_down_row"] + x].copy())
         bot = torch.empty_like(up)
         top = torch.empty_like(up)
         ops = [dist.P2POp(dist.isend, up, p["prev_rank"]), dist.P2POp(dist.irecv, bot, p["next_rank"]),
                dist.P2POp(dist.isend, down, p["next_rank"]), dist.P2POp(dist.irecv, top, p["prev_rank"])]
         for w in dist.batch_isend_irecv(ops):
             w.wait()
-        buf[p["recv_bottom_row"]:p["recv_bottom_row"] + d] = bot.numpy()
-        buf[p["recv_top_row"]:p["recv_top_row"] + d] = top.numpy()
-        # d turns on strip + halos; rows within d of the extended edge become
-        # garbage, exactly the halo rows (the device kernel's cone argument)
-        ext = buf[HALO - d:HALO + rows + d].copy()
-        for _ in range(d):
-            ext = step_np(ext)
-        buf[HALO:HALO + rows] = ext[d:d + rows]
+        buf[p["recv_bottom_row"]:p["recv_bottom_row"] + x] = bot.numpy()
+        buf[p["recv_top_row"]:p["recv_top_row"] + x] = top.numpy()
+        for i in range(k):
+            e = (k - 1 - i) * d
+            # d turns on the strip extended by e rows, from input extended by
+            # e + d rows: rows within d of the input's edge become garbage,
+            # the kernel's cone argument
+            ext = buf[HALO - e - d:HALO + rows + e + d].copy()
+            for _ in range(d):
+                ext = step_np(ext)
+            buf[HALO - e:HALO + rows + e] = ext[d:d + rows + 2 * e]
+            left -= d
     gathered = [None] * world
     dist.all_gather_object(gathered, (row0, buf[HALO:HALO + rows]))
     if rank == 0:
