@@ -34,6 +34,7 @@ struct StepArgs {
     int dst_base;     // physical row of logical output row 0
     RowMap in;
     int rows_per_wave;
+    int dummy_rows;   // >= 1 leading physical rows of dst usable as store dummies
     unsigned long long *alive;  // nullable: += popcount of the output
 };
 
@@ -71,7 +72,8 @@ int persist_waves_for(int depth, int wpl);
 int persist_blocks_per_cu(int depth, int wpl, int nw);
 // Workgroup shape / band height for `cus` resident workgroups of `units`
 // (tile, strip) units each; false if none fits.  Caller sets p->nw.
-bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, int units, PersistArgs *p);
+// force_tx > 0: only workgroups of that many tiles across.
+bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, int units, PersistArgs *p, int force_tx = 0);
 hipError_t launch_persist(const PersistArgs &p, int depth, int wpl, hipStream_t s);
 
 hipError_t launch_pack(const uint8_t *bytes, uint32_t *words, int W, int Ww, int rows, hipStream_t s);

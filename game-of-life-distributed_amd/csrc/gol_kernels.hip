@@ -241,7 +241,7 @@ __device__ __forceinline__ Lanes<WPL> vmov(const Lanes<WPL> &v) {
 // first stored word is t0, D turns ahead; returns the popcount of its stored
 // output words.  Shared by the per-launch and the persistent kernel.
 template <int D, bool SKIP, int WPL>
-__device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int rows_here, int t0) {
+__device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int rows_here, int t0, int wave_id) {
     const int lane = threadIdx.x & 63;
     const int Ww = a.Ww;
     int col = (t0 + WPL * (lane - 1)) % Ww;  // WPL = 2 needs Ww even: a pair never wraps
@@ -273,9 +273,12 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
     // Output rows are stored unconditionally so the whole 3-row group is one
     // basic block (the scheduler can then overlap stage t of row i+1 with
     // stage t+1 of row i): pipeline-fill rows and halo lanes write to a dummy
-    // address in physical row 0, a halo row that is never an output.
+    // address in one of the first `dummy_rows` physical rows (halo rows that
+    // are no output of this launch and not read before they are rewritten),
+    // spread over waves: one shared dummy line written by every wave of a
+    // tile column serialises in L2.
     uint32_t *const dst_row0 = a.dst + (size_t)(a.dst_base + r0) * Ww + col;
-    uint32_t *const dummy = a.dst + col;
+    uint32_t *const dummy = a.dst + (size_t)(wave_id % a.dummy_rows) * Ww + col;
     uint32_t cnt = 0;
     auto emit = [&](const Lanes<WPL> &y, int out_idx) {
         const bool ok = keep && (unsigned)out_idx < (unsigned)rows_here;
@@ -357,7 +360,7 @@ __global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
     const int tile = wave - strip * tiles_x;
     const int r0 = strip * S;
     if (r0 >= a.rows_out) return;  // wave-uniform
-    const uint32_t cnt = stream_band<D, SKIP, WPL>(a, r0, min(S, a.rows_out - r0), tile * tile_words(WPL));
+    const uint32_t cnt = stream_band<D, SKIP, WPL>(a, r0, min(S, a.rows_out - r0), tile * tile_words(WPL), wave);
     if (a.alive) {
         const uint32_t tot = wave_sum_u32(cnt);
         if ((threadIdx.x & 63) == 0) atomicAdd(a.alive, (unsigned long long)tot);
@@ -410,7 +413,7 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
     for (int j = 0; j < p.J; ++j) {
         const long long tr_w0 = (long long)__builtin_amdgcn_s_memrealtime();
         if (j > 0) {
-            if (w == 0) {
+            if (w == NW - 1) {  // the last wave polls (SIMD balance)
                 const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
                 for (;;) {
                     const unsigned v = __hip_atomic_load(&p.progress[nb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -437,7 +440,7 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
         const bool odd = ((p.first + j) & 1) != 0;
         a.src = odd ? p.buf1 : p.buf0;
         a.dst = odd ? p.buf0 : p.buf1;
-        cnt = rows_here > 0 ? stream_band<D, true, WPL>(a, r0, rows_here, tile * tile_words(WPL)) : 0u;
+        cnt = rows_here > 0 ? stream_band<D, true, WPL>(a, r0, rows_here, tile * tile_words(WPL), b * NW + w) : 0u;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         {
             const long long tr_e = (long long)__builtin_amdgcn_s_memrealtime();
@@ -450,7 +453,7 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
             }
         }
         __syncthreads();
-        if (threadIdx.x == 0) {
+        if (threadIdx.x == (NW - 1) * 64) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(&p.progress[b], (unsigned)(j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -555,12 +558,13 @@ int persist_blocks_per_cu(int depth, int wpl, int nw) {
     return e == hipSuccess ? b : 0;
 }
 
-bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, int units, PersistArgs *p) {
+bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, int units, PersistArgs *p, int force_tx) {
     const int NW = units;
     const int tiles_x = tb_tiles(Ww, wpl);
     bool found = false;
     long best_s = 0;
     for (int wg_tx = 1; wg_tx <= NW; wg_tx *= 2) {
+        if (force_tx > 0 && wg_tx != force_tx) continue;
         const int wg_sy = NW / wg_tx;
         const int cols = (tiles_x + wg_tx - 1) / wg_tx;
         // as many workgroup rows as CUs allow, but bands of >= depth rows

@@ -90,6 +90,8 @@ struct golhip {
     int wpl_opt = 0;            // option "wpl": words per lane (0 = auto, 1, 2)
     int persist_depth = 0;      // option "persist_depth" (0: tb_depth)
     int persist_waves = 0;      // option "persist_waves": waves per workgroup (0: default)
+    int dummy_rows = 0;         // option "dummy_rows": halo rows taking the kernels' dummy stores (0: all)
+    int persist_wg_tx = 0;      // option "persist_wg_tx": tiles across a persistent workgroup (0: plan)
     unsigned long long *d_trace = nullptr;  // option "trace": persistent-kernel diagnostics
     unsigned *d_sync = nullptr; // persistent kernel: [0] error, [1..] progress per workgroup
     unsigned *h_err = nullptr;  // pinned copy of the error word
@@ -233,6 +235,15 @@ int persist_nw_for(golhip_t h, int depth, int wpl) {
 int wpl_for(golhip_t h) {
     if (h->W % 64 != 0) return 1;
     if (h->wpl_opt == 1 || h->wpl_opt == 2) return h->wpl_opt;
+    if ((h->comm && (h->nranks > 1 || h->force_halo)) || !h->persistent) {
+        // per-launch kernels (row strips): the hardware refills freed wave
+        // slots, so band height matters less; stored fraction / slots per word
+        // (16384-wide strips: 55.6 vs 51.2 TCUPS for wpl 2 vs 1, profiles/r1e)
+        auto rate = [&](int wpl) {
+            return (double)h->Ww / (golk::tb_tiles(h->Ww, wpl) * 62.0 * wpl) / (wpl == 2 ? 13.0 : 17.0);
+        };
+        return rate(2) >= rate(1) ? 2 : 1;
+    }
     auto best = [&](int wpl) {
         const int d = default_depth(h, wpl);
         const int def = golk::persist_waves_for(d, wpl);
@@ -289,6 +300,7 @@ golk::StepArgs step_args(golhip_t h, unsigned long long *alive, bool halo) {
         a.in.rmax = (int)h->phys_rows - 1;
     }
     a.rows_per_wave = h->rows_per_wave;
+    a.dummy_rows = h->dummy_rows > 0 ? h->dummy_rows : kHalo;
     a.alive = alive;
     return a;
 }
@@ -377,6 +389,7 @@ int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int
         a.rows_out = hi - lo;
         a.dst_base = kHalo + lo;
         a.in.off = kHalo + lo;
+        a.dummy_rows = std::max(1, std::min(a.dummy_rows, kHalo + std::min(lo, 0)));  // rows above the outputs
     }
     const int wpl = wpl_for(h);
     if (a.rows_out == h->rows) {
@@ -486,7 +499,7 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     const int nw = persist_nw_for(h, depth, wpl);
     if (golk::persist_blocks_per_cu(depth, wpl, nw) < 1) return 0;
     golk::PersistArgs p{};
-    if (!golk::plan_persist(h->Ww, h->rows, depth, h->cu_count, wpl, nw, &p)) return 0;
+    if (!golk::plan_persist(h->Ww, h->rows, depth, h->cu_count, wpl, nw, &p, h->persist_wg_tx)) return 0;
     p.nw = nw;
     if (!h->d_sync) {
         if (hipMalloc(&h->d_sync, (size_t)(h->cu_count + 2) * sizeof(unsigned)) != hipSuccess ||
@@ -720,6 +733,16 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         if (value != 0 && value != 4 && value != 8 && value != 16)
             return fail(GOLHIP_EINVAL, "persist_waves %lld not in {0,4,8,16}", (long long)value);
         h->persist_waves = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "dummy_rows")) {
+        if (value < 0 || value > kHalo) return fail(GOLHIP_EINVAL, "dummy_rows %lld", (long long)value);
+        h->dummy_rows = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "persist_wg_tx")) {
+        if (value < 0 || value > 16) return fail(GOLHIP_EINVAL, "persist_wg_tx %lld", (long long)value);
+        h->persist_wg_tx = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "trace")) {
