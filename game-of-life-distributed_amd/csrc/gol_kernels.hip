@@ -413,7 +413,7 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
     for (int j = 0; j < p.J; ++j) {
         const long long tr_w0 = (long long)__builtin_amdgcn_s_memrealtime();
         if (j > 0) {
-            if (w == NW - 1) {  // the last wave polls (SIMD balance)
+            if (w == NW - 1) {  // the last wave polls: wave 0 polling cost 16 % at 65536^2 wpl 2 (r1e)
                 const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
                 for (;;) {
                     const unsigned v = __hip_atomic_load(&p.progress[nb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
