@@ -173,3 +173,32 @@ def test_ref_quirks_mode(root, fixtures):
     first = [e["Cell"] for e in evs if e["type"] == "CellFlipped" and e["CompletedTurns"] == 0]
     rows, cols = np.nonzero(b0 == 255)
     assert first[: len(rows)] == list(zip(rows.tolist(), cols.tolist()))   # Cell{X: row, Y: col}
+
+
+# ---------------------------------------------------------------- the command line (main.go)
+CLI = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "game-of-life-distributed_amd",
+                   "golhip", "golrun")
+
+
+@pytest.mark.parametrize("n,turns", [(512, 100), (64, 1), (16, 0)])
+def test_cli_headless(root, manifest, n, turns):
+    """golrun -noVis (main.go's flags and headless drain loop): same stdout
+    header, and out/<n>x<n>x<turns>.pgm byte-identical to check/images."""
+    import subprocess
+
+    res = subprocess.run([CLI, "-noVis", "-t", "4", "-w", str(n), "-h", str(n), "-turns", str(turns),
+                          "-root", str(root)], capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0, res.stderr
+    assert res.stdout.startswith(f"Threads: 4\nWidth: {n}\nHeight: {n}\n")
+    data = (root / "out" / f"{n}x{n}x{turns}.pgm").read_bytes()
+    assert hashlib.sha256(data).hexdigest() == manifest[f"check_{n}x{turns}"]["sha256"]
+
+
+def test_cli_quit_key(root):
+    """Without -noVis, a `q` line on stdin quits the (endless by default) run."""
+    import subprocess
+
+    res = subprocess.run([CLI, "-w", "64", "-h", "64", "-root", str(root)], input="q\n", capture_output=True,
+                         text=True, timeout=120)
+    assert res.returncode == 0, res.stderr
+    assert any(p.name.startswith("64x64x") for p in (root / "out").iterdir())

@@ -45,3 +45,20 @@ def test_no_device_fails_loudly(tmp_path):
         pass
     evs, err = run_err(tmp_path, b"P5\n64 64\n255\n" + bytes(4096))
     assert evs == [] and "golhip" in err
+
+
+def test_cli_flags_without_gpu(tmp_path):
+    """golrun parses main.go's flags and prints its header; without a HIP
+    device (or image) it fails loudly instead of falling back to the CPU."""
+    import subprocess
+
+    cli = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "game-of-life-distributed_amd",
+                       "golhip", "golrun")
+    if not os.path.exists(cli):
+        pytest.skip("golrun not built")
+    res = subprocess.run([cli, "-noVis", "-t=3", "--w", "32", "-h", "16", "-turns", "5", "-root", str(tmp_path)],
+                         capture_output=True, text=True, timeout=60)
+    assert res.stdout.startswith("Threads: 3\nWidth: 32\nHeight: 16\n")
+    assert res.returncode == 1 and "golrun:" in res.stderr
+    bad = subprocess.run([cli, "-bogus"], capture_output=True, text=True, timeout=60)
+    assert bad.returncode == 2 and "flag provided but not defined" in bad.stderr
