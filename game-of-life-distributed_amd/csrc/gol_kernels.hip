@@ -392,9 +392,21 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
     const int b = blockIdx.x;
     const int wx = b % p.cols, wy = b / p.cols;
     const int tile = wx * p.wg_tx + w % p.wg_tx;
-    const int strip = wy * p.wg_sy + w / p.wg_tx;
-    const int r0 = strip * p.S;
-    const int rows_here = (tile < p.tiles_x && r0 < p.base.rows_out) ? min(p.S, p.base.rows_out - r0) : 0;
+    int r0, band;
+    if (p.S_old > 0) {
+        // one tile column per workgroup, unequal bands: the SIMD arbiter serves
+        // the oldest wave first, so waves 0 .. NW/2-1 (the first on each SIMD)
+        // take taller bands than their younger SIMD mates (see plan_persist)
+        constexpr int half = NW / 2;
+        const int base = wy * p.wg_sy * p.S;
+        r0 = base + (w < half ? w * p.S_old : half * p.S_old + (w - half) * p.S_young);
+        band = w < half ? p.S_old : p.S_young;
+        if (w == NW - 1) band = base + p.wg_sy * p.S - r0;  // the last band takes the rounding
+    } else {
+        r0 = (wy * p.wg_sy + w / p.wg_tx) * p.S;
+        band = p.S;
+    }
+    const int rows_here = (tile < p.tiles_x && r0 < p.base.rows_out) ? min(band, p.base.rows_out - r0) : 0;
 
     // neighbour workgroup polled by lane k < 9
     int nb = b;

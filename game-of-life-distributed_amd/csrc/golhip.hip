@@ -90,6 +90,7 @@ struct golhip {
     int wpl_opt = 0;            // option "wpl": words per lane (0 = auto, 1, 2)
     int persist_depth = 0;      // option "persist_depth" (0: tb_depth)
     int persist_waves = 0;      // option "persist_waves": waves per workgroup (0: default)
+    int age_split = -1;         // option "age_split": % of a workgroup's rows for its oldest waves (0: equal, -1: auto)
     int dummy_rows = 0;         // option "dummy_rows": halo rows taking the kernels' dummy stores (0: all)
     int persist_wg_tx = 0;      // option "persist_wg_tx": tiles across a persistent workgroup (0: plan)
     unsigned long long *d_trace = nullptr;  // option "trace": persistent-kernel diagnostics
@@ -499,7 +500,19 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     const int nw = persist_nw_for(h, depth, wpl);
     if (golk::persist_blocks_per_cu(depth, wpl, nw) < 1) return 0;
     golk::PersistArgs p{};
-    if (!golk::plan_persist(h->Ww, h->rows, depth, h->cu_count, wpl, nw, &p, h->persist_wg_tx)) return 0;
+    // With two waves per SIMD the older one is served first and finishes its
+    // band early; giving the older half of the waves 65 % of the rows lets
+    // both finish together (16384^2: 59 -> 64 TCUPS, profiles/r1f).
+    const int age_split = h->age_split >= 0 ? h->age_split : (nw == 8 ? 65 : 0);
+    const bool split = age_split > 0 && age_split < 100;
+    if (!golk::plan_persist(h->Ww, h->rows, depth, h->cu_count, wpl, nw, &p, split ? 1 : h->persist_wg_tx)) return 0;
+    if (split) {
+        // rows of a workgroup stack: age_split % to the NW/2 oldest waves
+        const int R = p.wg_sy * p.S, half = nw / 2;
+        p.S_old = std::max(1, (int)((int64_t)R * age_split / 100 / half));
+        p.S_young = std::max(1, (R - half * p.S_old) / half);
+        if (half * p.S_old >= R) p.S_old = p.S_young = 0;
+    }
     p.nw = nw;
     if (!h->d_sync) {
         if (hipMalloc(&h->d_sync, (size_t)(h->cu_count + 2) * sizeof(unsigned)) != hipSuccess ||
@@ -733,6 +746,11 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         if (value != 0 && value != 4 && value != 8 && value != 16)
             return fail(GOLHIP_EINVAL, "persist_waves %lld not in {0,4,8,16}", (long long)value);
         h->persist_waves = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "age_split")) {
+        if (value < -1 || value >= 100) return fail(GOLHIP_EINVAL, "age_split %lld", (long long)value);
+        h->age_split = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "dummy_rows")) {

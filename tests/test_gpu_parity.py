@@ -439,3 +439,22 @@ def test_rccl_halo_ring_full_size():
             b.step(200)
             res.append((b.board_hash(), b.alive_count()))
     assert res[0] == res[1]
+
+
+@pytest.mark.parametrize("N,depth,wpl,nw,split", [(2048, 16, 1, 8, 70), (4096, 16, 2, 8, 80), (2048, 8, 1, 16, 65),
+                                                  (3968, 16, 1, 8, 75)])
+def test_persistent_unequal_bands(coracle, N, depth, wpl, nw, split):
+    """Persistent kernel with taller bands for the oldest waves (age_split) vs the C oracle."""
+    board = coracle.fill_random(N, N // 2, 0x5EED000F)
+    turns = 4 * depth + 1
+    want = coracle.run(board, turns)
+    with golhip.Board(N, N // 2) as b:
+        b.set_option("wpl", wpl)
+        b.set_option("persist_waves", nw)
+        b.set_option("age_split", split)
+        b.set_tb_depth(depth)
+        b.load_bytes(board)
+        b.step(turns)
+        assert b.perf()["persist_launches"] == 1
+        assert np.array_equal(b.snapshot_bytes(), want)
+        assert b.alive_count() == (int((want == 255).sum()), turns)
