@@ -59,7 +59,8 @@ struct PersistArgs {
     int first;                // buffer holding generation 0 (0 -> buf0)
     int J;                    // super-steps of `depth` turns
     int S;                    // rows per wavefront
-    int S_old, S_young;       // > 0: unequal bands (wg_tx == 1), first / second half of the waves
+    int S_old, S_young;       // > 0: unequal bands, first / second half of the band rows (wg_sy even)
+    int paired;               // 1: waves w, w + NW/2 share two bands, met from both ends (wg_sy even)
     int wg_tx, wg_sy;         // workgroup block of (tiles, strips)
     int cols, wg_y;           // workgroup grid
     int tiles_x;

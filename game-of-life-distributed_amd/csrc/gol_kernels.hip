@@ -240,8 +240,14 @@ __device__ __forceinline__ Lanes<WPL> vmov(const Lanes<WPL> &v) {
 // One wavefront streams output rows [r0, r0 + rows_here) of the tile whose
 // first stored word is t0, D turns ahead; returns the popcount of its stored
 // output words.  Shared by the per-launch and the persistent kernel.
+// dir = -1 streams the band bottom to top (the rule is symmetric in y).
+// With `claim` (an LDS counter shared with the wave streaming the same band
+// from the other end) the wave takes its output rows three at a time from the
+// counter and stops when the two fronts meet, so the band splits wherever the
+// SIMD arbiter's service left the two waves.
 template <int D, bool SKIP, int WPL>
-__device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int rows_here, int t0, int wave_id) {
+__device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int rows_here, int t0, int wave_id,
+                                                int dir = 1, int *claim = nullptr) {
     const int lane = threadIdx.x & 63;
     const int Ww = a.Ww;
     int col = (t0 + WPL * (lane - 1)) % Ww;  // WPL = 2 needs Ww even: a pair never wraps
@@ -249,7 +255,7 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
     const bool keep = lane >= 1 && lane <= kTileValid && (t0 + WPL * (lane - 1)) < Ww;
 
     // input row cursor (wave-uniform)
-    int r = r0 - D + a.in.off;
+    int r = (dir > 0 ? r0 - D : r0 + rows_here - 1 + D) + a.in.off;
     const int wrap = a.in.wrap > 0 ? a.in.wrap : INT_MAX;
     if (a.in.wrap > 0) {
         r %= a.in.wrap;
@@ -266,7 +272,10 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
             v.w[0] = q.x;
             v.w[1] = q.y;
         }
-        r = (r + 1 == wrap) ? 0 : r + 1;
+        if (dir > 0)
+            r = (r + 1 == wrap) ? 0 : r + 1;
+        else
+            r = (r == 0) ? wrap - 1 : r - 1;  // no wrap: only prefetched rows past the band go below 0
         return v;
     };
 
@@ -277,12 +286,14 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
     // are no output of this launch and not read before they are rewritten),
     // spread over waves: one shared dummy line written by every wave of a
     // tile column serialises in L2.
-    uint32_t *const dst_row0 = a.dst + (size_t)(a.dst_base + r0) * Ww + col;
+    uint32_t *const dst_row0 = a.dst + (size_t)(a.dst_base + (dir > 0 ? r0 : r0 + rows_here - 1)) * Ww + col;
+    const ptrdiff_t dst_step = dir > 0 ? (ptrdiff_t)Ww : -(ptrdiff_t)Ww;
+    int lim = claim ? 0 : rows_here;  // output rows [0, lim) of this wave's order are its own
     uint32_t *const dummy = a.dst + (size_t)(wave_id % a.dummy_rows) * Ww + col;
     uint32_t cnt = 0;
     auto emit = [&](const Lanes<WPL> &y, int out_idx) {
-        const bool ok = keep && (unsigned)out_idx < (unsigned)rows_here;
-        uint32_t *p = ok ? dst_row0 + (ptrdiff_t)out_idx * Ww : dummy;
+        const bool ok = keep && (unsigned)out_idx < (unsigned)lim;
+        uint32_t *p = ok ? dst_row0 + (ptrdiff_t)out_idx * dst_step : dummy;
         uint32_t pc = 0;
         if constexpr (WPL == 1) {
             *p = y.w[0];
@@ -333,11 +344,24 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
     fill(std::integral_constant<int, D / 4>());
     fill(std::integral_constant<int, D / 2>());
     fill(std::integral_constant<int, 3 * D / 4>());
-    for (; oi < rows_here; oi += 3) {
+    bool more = true;
+    for (; claim ? more : oi < rows_here; oi += 3) {
         const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
+        // claim this group's rows >= 0 (the LDS round trip hides under the group)
+        const int need = claim ? min(3, max(0, oi + 3)) : 0;
+        int old = 0;
+        if (need > 0) {
+            int o = 0;
+            if (lane == 0) o = __hip_atomic_fetch_add(claim, -need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            old = __builtin_amdgcn_readfirstlane(o);
+        }
         __builtin_amdgcn_sched_barrier(0);
         Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
         push_group<D, D, WPL>(y0, y1, y2, h0, h1, cc);
+        if (need > 0) {
+            lim = max(oi, 0) + min(need, max(0, old));
+            more = old > need;
+        }
         emit(y0, oi);
         emit(y1, oi + 1);
         emit(y2, oi + 2);
@@ -392,18 +416,28 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
     const int b = blockIdx.x;
     const int wx = b % p.cols, wy = b / p.cols;
     const int tile = wx * p.wg_tx + w % p.wg_tx;
-    int r0, band;
-    if (p.S_old > 0) {
-        // one tile column per workgroup, unequal bands: the SIMD arbiter serves
-        // the oldest wave first, so waves 0 .. NW/2-1 (the first on each SIMD)
-        // take taller bands than their younger SIMD mates (see plan_persist)
-        constexpr int half = NW / 2;
+    int r0, band, dir = 1;
+    const int ry = w / p.wg_tx;  // band row within the workgroup stack
+    // paired bands: wave w (band row ry < wg_sy/2) and wave w + NW/2 (the
+    // younger wave on the same SIMD) share the two-band region of pair
+    // ry % (wg_sy/2), streaming it from the top and from the bottom
+    const bool paired = p.paired != 0;
+    if (paired) {
+        const int hr = p.wg_sy / 2;
+        r0 = wy * p.wg_sy * p.S + 2 * (ry % hr) * p.S;
+        band = 2 * p.S;
+        dir = ry < hr ? 1 : -1;
+    } else if (p.S_old > 0) {
+        // unequal bands: the SIMD arbiter serves the oldest wave first, so the
+        // band rows of waves 0 .. NW/2-1 (the first on each SIMD) are taller
+        // than those of their younger SIMD mates (see try_persist)
+        const int hr = p.wg_sy / 2;
         const int base = wy * p.wg_sy * p.S;
-        r0 = base + (w < half ? w * p.S_old : half * p.S_old + (w - half) * p.S_young);
-        band = w < half ? p.S_old : p.S_young;
-        if (w == NW - 1) band = base + p.wg_sy * p.S - r0;  // the last band takes the rounding
+        r0 = base + (ry < hr ? ry * p.S_old : hr * p.S_old + (ry - hr) * p.S_young);
+        band = ry < hr ? p.S_old : p.S_young;
+        if (ry == p.wg_sy - 1) band = base + p.wg_sy * p.S - r0;  // the last band row takes the rounding
     } else {
-        r0 = (wy * p.wg_sy + w / p.wg_tx) * p.S;
+        r0 = (wy * p.wg_sy + ry) * p.S;
         band = p.S;
     }
     const int rows_here = (tile < p.tiles_x && r0 < p.base.rows_out) ? min(band, p.base.rows_out - r0) : 0;
@@ -416,7 +450,9 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
         nb = ny * p.cols + nx;
     }
     __shared__ int s_abort;
+    __shared__ int s_claim[2][NW / 2];  // per pair, double-buffered over super-steps
     if (threadIdx.x == 0) s_abort = 0;
+    if (paired && w < NW / 2 && lane == 0) s_claim[0][w] = rows_here;
     __syncthreads();
 
     uint32_t cnt = 0;
@@ -452,7 +488,14 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
         const bool odd = ((p.first + j) & 1) != 0;
         a.src = odd ? p.buf1 : p.buf0;
         a.dst = odd ? p.buf0 : p.buf1;
-        cnt = rows_here > 0 ? stream_band<D, true, WPL>(a, r0, rows_here, tile * tile_words(WPL), b * NW + w) : 0u;
+        int *claim = nullptr;
+        if (paired) {
+            claim = &s_claim[j & 1][w % (NW / 2)];
+            // every claim of super-step j-1 is done (barrier above): re-arm its counter for j+1
+            if (w < NW / 2 && lane == 0) s_claim[(j + 1) & 1][w] = rows_here;
+        }
+        cnt = rows_here > 0 ? stream_band<D, true, WPL>(a, r0, rows_here, tile * tile_words(WPL), b * NW + w, dir, claim)
+                            : 0u;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         {
             const long long tr_e = (long long)__builtin_amdgcn_s_memrealtime();
@@ -580,11 +623,12 @@ bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, int units, Pers
         const int wg_sy = NW / wg_tx;
         const int cols = (tiles_x + wg_tx - 1) / wg_tx;
         // as many workgroup rows as CUs allow, but bands of >= depth rows
-        const int wg_y = std::min(cus / cols, rows / (wg_sy * depth));
+        int wg_y = std::min(cus / cols, rows / (wg_sy * depth));
         if (wg_y < 1) continue;
         const int strips = wg_y * wg_sy;
         const int S = (rows + strips - 1) / strips;
         if (S < depth) continue;                         // halo rows from the adjacent strip only
+        wg_y = (rows + wg_sy * S - 1) / (wg_sy * S);     // rounding S up can leave trailing rows empty
         // every workgroup row must hold >= depth real rows (its neighbours' halos)
         const int last_rows = rows - (wg_y - 1) * wg_sy * S;
         if (last_rows < depth) continue;

@@ -91,6 +91,7 @@ struct golhip {
     int persist_depth = 0;      // option "persist_depth" (0: tb_depth)
     int persist_waves = 0;      // option "persist_waves": waves per workgroup (0: default)
     int age_split = -1;         // option "age_split": % of a workgroup's rows for its oldest waves (0: equal, -1: auto)
+    int paired_bands = 1;       // option "paired_bands": SIMD mates share two bands from both ends (persistent)
     int dummy_rows = 0;         // option "dummy_rows": halo rows taking the kernels' dummy stores (0: all)
     int persist_wg_tx = 0;      // option "persist_wg_tx": tiles across a persistent workgroup (0: plan)
     unsigned long long *d_trace = nullptr;  // option "trace": persistent-kernel diagnostics
@@ -505,13 +506,18 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     // both finish together (16384^2: 59 -> 64 TCUPS, profiles/r1f).
     const int age_split = h->age_split >= 0 ? h->age_split : (nw == 8 ? 65 : 0);
     const bool split = age_split > 0 && age_split < 100;
-    if (!golk::plan_persist(h->Ww, h->rows, depth, h->cu_count, wpl, nw, &p, split ? 1 : h->persist_wg_tx)) return 0;
-    if (split) {
-        // rows of a workgroup stack: age_split % to the NW/2 oldest waves
-        const int R = p.wg_sy * p.S, half = nw / 2;
-        p.S_old = std::max(1, (int)((int64_t)R * age_split / 100 / half));
-        p.S_young = std::max(1, (R - half * p.S_old) / half);
-        if (half * p.S_old >= R) p.S_old = p.S_young = 0;
+    if (!golk::plan_persist(h->Ww, h->rows, depth, h->cu_count, wpl, nw, &p, h->persist_wg_tx)) return 0;
+    if (h->paired_bands && p.wg_sy >= 2 && p.wg_sy % 2 == 0) {
+        // the older and the younger wave of a SIMD stream a shared two-band
+        // region from both ends and meet where the arbiter's service put them
+        p.paired = 1;
+    } else if (split && p.wg_sy >= 2 && p.wg_sy % 2 == 0) {
+        // rows of a workgroup stack: age_split % to the band rows of the
+        // NW/2 oldest waves (w < NW/2 <=> band row < wg_sy/2)
+        const int R = p.wg_sy * p.S, hr = p.wg_sy / 2;
+        p.S_old = std::max(1, (int)((int64_t)R * age_split / 100 / hr));
+        p.S_young = std::max(1, (R - hr * p.S_old) / (p.wg_sy - hr));
+        if (hr * p.S_old >= R) p.S_old = p.S_young = 0;
     }
     p.nw = nw;
     if (!h->d_sync) {
@@ -756,6 +762,11 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     if (!strcmp(key, "dummy_rows")) {
         if (value < 0 || value > kHalo) return fail(GOLHIP_EINVAL, "dummy_rows %lld", (long long)value);
         h->dummy_rows = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "paired_bands")) {
+        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "paired_bands %lld", (long long)value);
+        h->paired_bands = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "persist_wg_tx")) {

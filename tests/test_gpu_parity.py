@@ -441,17 +441,43 @@ def test_rccl_halo_ring_full_size():
     assert res[0] == res[1]
 
 
-@pytest.mark.parametrize("N,depth,wpl,nw,split", [(2048, 16, 1, 8, 70), (4096, 16, 2, 8, 80), (2048, 8, 1, 16, 65),
-                                                  (3968, 16, 1, 8, 75)])
-def test_persistent_unequal_bands(coracle, N, depth, wpl, nw, split):
-    """Persistent kernel with taller bands for the oldest waves (age_split) vs the C oracle."""
+@pytest.mark.parametrize("N,depth,wpl,nw,split,tx", [(2048, 16, 1, 8, 70, 1), (4096, 16, 2, 8, 80, 1),
+                                                     (2048, 8, 1, 16, 65, 1), (3968, 16, 1, 8, 75, 1),
+                                                     (4096, 16, 1, 8, 65, 2), (4096, 16, 2, 8, 60, 4),
+                                                     (3968, 8, 1, 16, 65, 4), (2048, 16, 1, 8, 65, 8)])
+def test_persistent_unequal_bands(coracle, N, depth, wpl, nw, split, tx):
+    """Persistent kernel with static taller bands for the oldest waves (age_split) vs the C oracle."""
     board = coracle.fill_random(N, N // 2, 0x5EED000F)
     turns = 4 * depth + 1
     want = coracle.run(board, turns)
     with golhip.Board(N, N // 2) as b:
         b.set_option("wpl", wpl)
         b.set_option("persist_waves", nw)
+        b.set_option("paired_bands", 0)
         b.set_option("age_split", split)
+        b.set_option("persist_wg_tx", tx)
+        b.set_tb_depth(depth)
+        b.load_bytes(board)
+        b.step(turns)
+        assert b.perf()["persist_launches"] == 1
+        assert np.array_equal(b.snapshot_bytes(), want)
+        assert b.alive_count() == (int((want == 255).sum()), turns)
+
+
+@pytest.mark.parametrize("N,rows,depth,wpl,nw,tx", [(2048, 1024, 16, 1, 8, 1), (4096, 2048, 16, 2, 8, 1),
+                                                    (2048, 1024, 8, 1, 16, 1), (3968, 1984, 16, 1, 8, 2),
+                                                    (4096, 2048, 16, 2, 8, 4), (3968, 1001, 8, 1, 16, 4),
+                                                    (2048, 1024, 16, 1, 8, 8), (1984, 999, 4, 2, 16, 2)])
+def test_persistent_paired_bands(coracle, N, rows, depth, wpl, nw, tx):
+    """SIMD mates streaming a shared two-band region from both ends (dynamic meeting row) vs the C oracle."""
+    board = coracle.fill_random(N, rows, 0x5EED0010)
+    turns = 5 * depth + 3
+    want = coracle.run(board, turns)
+    with golhip.Board(N, rows) as b:
+        b.set_option("wpl", wpl)
+        b.set_option("persist_waves", nw)
+        b.set_option("persist_wg_tx", tx)
+        b.set_option("paired_bands", 1)
         b.set_tb_depth(depth)
         b.load_bytes(board)
         b.step(turns)
