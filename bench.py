@@ -18,7 +18,8 @@ neighbours over RCCL every fused launch (the only collective on the path).
 
 Rank 0 prints ONE JSON line; `roofline` is measured on the step kernel with
 HIP events on the engine's stream; `cpu_baseline` times the oracle's port of
-the reference worker pool on a bounded sample (rank 0, N = 1 only).
+the reference worker pool on a bounded sample (rank 0, N = 1 only), with the
+bit-packed OpenMP CPU comparator beside it (`cpu_baseline.fast_cpu`).
 """
 from __future__ import annotations
 
@@ -27,6 +28,8 @@ import json
 import os
 import sys
 import time
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 for _p in (ROOT, os.path.join(ROOT, "game-of-life-distributed_amd")):
@@ -61,16 +64,37 @@ def parse():
     return ap.parse_args()
 
 
+def host_info() -> dict:
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count()}
+
+
+def cpu_threads() -> int:
+    # the box's CPU share is 16 threads (nproc shows the whole machine)
+    return max(1, min(16, os.cpu_count() or 1))
+
+
 def cpu_baseline(W: int, target_s: float) -> dict:
     """Oracle port of the reference worker pool (distributor.go:116-173) on a
     bounded sample of the same synthetic board: a 4096-row band of the board,
-    as many turns as fit in ~target_s."""
+    as many turns as fit in ~target_s.  Beside it (`fast_cpu`), the bit-packed
+    OpenMP comparator (oracle/gol_fastcpu.c) on the whole board, ~target_s / 2."""
     from oracle.oracle import COracle
 
     o = COracle()
+    seed = WORKLOADS.get(W, WORKLOADS[16384])["seed"]
     rows = min(4096, W)
-    board = o.fill_random(W, rows, WORKLOADS.get(W, WORKLOADS[16384])["seed"])
-    threads = max(1, min(16, (os.cpu_count() or 2)) - 1)  # Threads; the pool runs Threads+1 workers
+    board = o.fill_random(W, rows, seed)
+    threads = cpu_threads() - 1  # Threads; the pool runs Threads+1 workers
+    threads = max(1, threads)
     t0 = time.perf_counter()
     o.run_workerpool(board, 1, threads)
     one = time.perf_counter() - t0
@@ -78,14 +102,36 @@ def cpu_baseline(W: int, target_s: float) -> dict:
     t0 = time.perf_counter()
     o.run_workerpool(board, turns, threads)
     dt = time.perf_counter() - t0
-    return {
+    out = {
         "value": W * rows * turns / dt / 1e9,
         "unit": "GCUPS",
         "cores": threads + 1,
         "kind": "port",
         "sample": f"{rows}x{W} band of the workload board (torus), {turns} turns, oracle/gol_oracle.c "
                   f"worker-pool port (Threads={threads}, Threads+1 workers), {dt:.1f} s",
+        "host": host_info(),
     }
+    # fast comparator: whole board if it fits in a few GB of host memory, else a band
+    fast_rows = W if W <= 65536 else 16384
+    words = o.pack64(o.fill_random(W, fast_rows, seed)) if W <= 16384 else \
+        np.ascontiguousarray(np.random.default_rng(seed).integers(0, 2**64, (fast_rows, W // 64), dtype=np.uint64))
+    nth = cpu_threads()
+    t0 = time.perf_counter()
+    o.run_fast_words(words, W, 4, nth)
+    one = (time.perf_counter() - t0) / 4
+    fturns = max(1, int(target_s / 2 / max(one, 1e-6)))
+    t0 = time.perf_counter()
+    o.run_fast_words(words, W, fturns, nth)
+    fdt = time.perf_counter() - t0
+    out["fast_cpu"] = {
+        "value": W * fast_rows * fturns / fdt / 1e9,
+        "unit": "GCUPS",
+        "cores": nth,
+        "kind": "bit-packed OpenMP comparator (not the reference algorithm)",
+        "sample": f"{fast_rows}x{W} torus, {fturns} turns, oracle/gol_fastcpu.c (64 cells/uint64, "
+                  f"{nth} OpenMP threads), {fdt:.1f} s",
+    }
+    return out
 
 
 def main():

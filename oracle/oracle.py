@@ -160,6 +160,10 @@ class COracle:
         lib.oracle_fill_random.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_uint64]
         lib.oracle_run_workerpool.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int]
         lib.oracle_run_workerpool.restype = ctypes.c_int64
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        lib.fastcpu_pack.argtypes = [u8p, ctypes.c_int, ctypes.c_int, u64p]
+        lib.fastcpu_unpack.argtypes = [u64p, ctypes.c_int, ctypes.c_int, u8p]
+        lib.fastcpu_run.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int]
         self.lib = lib
 
     @staticmethod
@@ -209,6 +213,35 @@ class COracle:
         if flips < 0:
             raise MemoryError("oracle_run_workerpool")
         return b, flips
+
+
+    # -- bit-packed OpenMP comparator (gol_fastcpu.c), W % 64 == 0
+    def pack64(self, board: np.ndarray) -> np.ndarray:
+        b = np.ascontiguousarray(board, dtype=np.uint8)
+        H, W = b.shape
+        w = np.zeros((H, W // 64), dtype=np.uint64)
+        if self.lib.fastcpu_pack(self._p(b), W, H, self._p(w, ctypes.c_uint64)) != 0:
+            raise ValueError("fastcpu_pack needs W % 64 == 0")
+        return w
+
+    def unpack64(self, words: np.ndarray, W: int) -> np.ndarray:
+        H = words.shape[0]
+        b = np.zeros((H, W), dtype=np.uint8)
+        if self.lib.fastcpu_unpack(self._p(np.ascontiguousarray(words), ctypes.c_uint64), W, H, self._p(b)) != 0:
+            raise ValueError("fastcpu_unpack needs W % 64 == 0")
+        return b
+
+    def run_fast_words(self, words: np.ndarray, W: int, turns: int, threads: int) -> None:
+        """In place on H x W/64 packed words."""
+        H = words.shape[0]
+        if self.lib.fastcpu_run(self._p(words, ctypes.c_uint64), W, H, turns, threads) != 0:
+            raise ValueError("fastcpu_run")
+
+    def run_fast(self, board: np.ndarray, turns: int, threads: int = 1) -> np.ndarray:
+        W = board.shape[1]
+        w = self.pack64(board)
+        self.run_fast_words(w, W, turns, threads)
+        return self.unpack64(w, W)
 
 
 def build() -> str:

@@ -117,3 +117,16 @@ def test_pack_unpack_roundtrip():
     for (H, W) in [(3, 16), (5, 33), (4, 64), (2, 100)]:
         b = np.where(rng.random((H, W)) < 0.4, 255, 0).astype(np.uint8)
         assert np.array_equal(unpack_bits(pack_bits(b), W), b)
+
+
+@pytest.mark.parametrize("n,t", [(64, 0), (64, 1), (64, 100), (512, 0), (512, 1), (512, 100)])
+def test_fastcpu_comparator_matches_golden_boards(fixtures, coracle, n, t):
+    """The bit-packed OpenMP CPU comparator (oracle/gol_fastcpu.c, timed by bench.py) is exact too."""
+    out = coracle.run_fast(board(fixtures, f"image_{n}", n), t, threads=3)
+    assert np.array_equal(pack_bits(out), fixtures[f"check_{n}x{t}"])
+
+
+@pytest.mark.parametrize("W,H,turns,threads", [(64, 3, 7, 1), (128, 37, 13, 4), (1024, 99, 20, 8), (192, 200, 33, 5)])
+def test_fastcpu_comparator_matches_oracle(coracle, W, H, turns, threads):
+    b = coracle.fill_random(W, H, 0x5EED0042 + W)
+    assert np.array_equal(coracle.run_fast(b, turns, threads), coracle.run(b, turns))
