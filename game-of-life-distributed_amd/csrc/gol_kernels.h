@@ -41,7 +41,7 @@ struct StepArgs {
 // Bit-sliced temporal-blocked step: `depth` in {1,2,4,8,16,32}; requires W % 32 == 0
 // (wpl = 2: W % 64 == 0, depth <= 16, board in the interleaved pair layout).  fill_skip: skip the pipeline-fill
 // stage-rows that only see padding.  wpl: words per lane (1 or 2).
-hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s, bool fill_skip, int wpl);
+hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s, bool fill_skip, int wpl, bool paired = false);
 int max_depth_for(int wpl);
 int tb_tiles(int Ww, int wpl);
 // One turn for any width (W % 32 != 0 boards such as 16x16).
@@ -49,8 +49,9 @@ hipError_t launch_step_generic(const StepArgs &a, hipStream_t s);
 int tb_waves(const StepArgs &a, int wpl);
 // Resident 256-thread blocks per CU of the depth-`depth` step kernel.
 int tb_blocks_per_cu(int depth, int wpl);
+int tb_wave_slots_per_cu(int depth, int wpl, bool paired);  // resident waves per CU
 // Rows per wavefront minimising (rounds of waves) x (rows streamed per wave).
-int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_skip, int wpl);
+int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_skip, int wpl, bool paired = false);
 
 // Persistent multi-super-step step kernel (torus mode); see gol_kernels.hip K1p.
 struct PersistArgs {

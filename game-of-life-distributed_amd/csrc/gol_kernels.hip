@@ -391,6 +391,36 @@ __global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
     }
 }
 
+// K1 with paired bands: a workgroup of 8 waves covers 4 consecutive (region,
+// tile) pairs in row-major order, a region being 2 S rows of one tile; the
+// two waves of each SIMD (w and w + 4, the older and the younger) stream
+// pair w & 3 from the top and from the bottom and claim output rows from a
+// shared LDS counter until they meet, so the SIMD arbiter's oldest-first
+// service no longer leaves the younger wave running alone at the end of the
+// launch.
+template <int D, int WPL>
+__global__ __launch_bounds__(512) void gol_tb_pair_kernel(StepArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int tiles_x = (a.Ww + tile_words(WPL) - 1) / tile_words(WPL);
+    const int S = a.rows_per_wave;
+    const int q = blockIdx.x * 4 + (w & 3);
+    const int region = q / tiles_x;
+    const int tile = q - region * tiles_x;
+    const int r0 = region * 2 * S;
+    const int len = r0 < a.rows_out ? min(2 * S, a.rows_out - r0) : 0;
+    __shared__ int s_claim[4];
+    if (w < 4 && lane == 0) s_claim[w] = len;
+    __syncthreads();
+    if (len == 0) return;  // wave-uniform, after the only barrier
+    const uint32_t cnt = stream_band<D, true, WPL>(a, r0, len, tile * tile_words(WPL), blockIdx.x * 8 + w,
+                                                   w < 4 ? 1 : -1, &s_claim[w & 3]);
+    if (a.alive) {
+        const uint32_t tot = wave_sum_u32(cnt);
+        if (lane == 0 && tot) atomicAdd(a.alive, (unsigned long long)tot);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // K1p: persistent multi-super-step kernel (torus mode, one device).
 //
@@ -553,7 +583,29 @@ int tb_waves(const StepArgs &a, int wpl) {
     return tb_tiles(a.Ww, wpl) * strips;
 }
 
-hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s, bool fill_skip, int wpl) {
+template <typename F>
+static hipError_t dispatch_pair(int depth, int wpl, F &&f) {
+#define GOL_QCASE(D, WP) \
+    if (depth == D && wpl == WP) return f(gol_tb_pair_kernel<D, WP>);
+    GOL_QCASE(1, 1) GOL_QCASE(2, 1) GOL_QCASE(4, 1) GOL_QCASE(8, 1) GOL_QCASE(16, 1) GOL_QCASE(32, 1)
+    GOL_QCASE(1, 2) GOL_QCASE(2, 2) GOL_QCASE(4, 2) GOL_QCASE(8, 2) GOL_QCASE(16, 2)
+#undef GOL_QCASE
+    return hipErrorInvalidValue;
+}
+
+int tb_pair_blocks(const StepArgs &a, int wpl) {
+    const int regions = (a.rows_out + 2 * a.rows_per_wave - 1) / (2 * a.rows_per_wave);
+    return (tb_tiles(a.Ww, wpl) * regions + 3) / 4;
+}
+
+hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s, bool fill_skip, int wpl, bool paired) {
+    if (paired && fill_skip) {
+        const dim3 grid(tb_pair_blocks(a, wpl)), block(512);
+        return dispatch_pair(depth, wpl, [&](auto kern) {
+            hipLaunchKernelGGL(kern, grid, block, 0, s, a);
+            return hipGetLastError();
+        });
+    }
     const int waves = tb_waves(a, wpl);
     const dim3 grid((waves + 3) / 4), block(256);
     return dispatch(depth, fill_skip, wpl, [&](auto kern) {
@@ -570,7 +622,16 @@ int tb_blocks_per_cu(int depth, int wpl) {
     return (e == hipSuccess && b > 0) ? b : 1;
 }
 
-int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_skip, int wpl) {
+int tb_wave_slots_per_cu(int depth, int wpl, bool paired) {
+    if (!paired) return 4 * tb_blocks_per_cu(depth, wpl);
+    int b = 0;
+    hipError_t e = dispatch_pair(depth, wpl, [&](auto kern) {
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 512, 0);
+    });
+    return 8 * ((e == hipSuccess && b > 0) ? b : 1);
+}
+
+int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_skip, int wpl, bool paired) {
     // Each wave streams S + 2*depth rows (~S + 1.25*depth row-equivalents of
     // work when the fill skips dead stages); waves run in ceil(waves / slots)
     // rounds.  Minimise rounds * work (fill overhead vs tail).
@@ -579,7 +640,8 @@ int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_sk
     double best = 1e300;
     for (int strips = 1; strips <= rows; ++strips) {
         const int S = (rows + strips - 1) / strips;
-        const long long waves = (long long)tiles_x * ((rows + S - 1) / S);
+        const long long waves = paired ? 2LL * tiles_x * ((rows + 2 * S - 1) / (2 * S))
+                                       : (long long)tiles_x * ((rows + S - 1) / S);
         const long long rounds = (waves + wave_slots - 1) / wave_slots;
         const double cost = (double)rounds * (S + (fill_skip ? 2 * depth - 0.75 * depth : 2 * depth));
         if (cost < best * 0.999) {

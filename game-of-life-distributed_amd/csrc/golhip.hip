@@ -86,7 +86,7 @@ struct golhip {
     int rows_per_wave = 0;      // 0 = automatic (per depth, from occupancy)
     int cu_count = 0;
     bool fill_skip = true;      // option "fill_skip"
-    bool persistent = true;     // option "persistent": K1p for long torus runs
+    int persistent = -1;        // option "persistent": K1p for long torus runs (1 on, 0 off, -1 auto)
     int wpl_opt = 0;            // option "wpl": words per lane (0 = auto, 1, 2)
     int persist_depth = 0;      // option "persist_depth" (0: tb_depth)
     int persist_waves = 0;      // option "persist_waves": waves per workgroup (0: default)
@@ -231,13 +231,24 @@ int persist_nw_for(golhip_t h, int depth, int wpl) {
     return def;
 }
 
+// The resident kernel wins on boards whose two buffers sit in the 256 MB
+// MALL (16384^2: 61 vs 58 TCUPS); on larger boards the per-launch kernel is
+// as fast or faster and far steadier from box to box (65536^2: 114-116 vs
+// 96-120 TCUPS over six boxes, 262144^2: 126 vs 105, profiles/r1f), so
+// "auto" keeps K1p for buffers of at most 64 MiB.
+constexpr int64_t kPersistAutoMaxBytes = 64ll << 20;
+bool persist_on(golhip_t h) {
+    if (h->persistent >= 0) return h->persistent != 0;
+    return h->local_words() * 4 <= kPersistAutoMaxBytes;
+}
+
 // Words per lane of the step kernels: 2 (interleaved pair layout) cuts the
 // shift work per word but quantises tiles at 124 words and halves the band
 // height; the option, or whichever plan_rate prefers.
 int wpl_for(golhip_t h) {
     if (h->W % 64 != 0) return 1;
     if (h->wpl_opt == 1 || h->wpl_opt == 2) return h->wpl_opt;
-    if ((h->comm && (h->nranks > 1 || h->force_halo)) || !h->persistent) {
+    if ((h->comm && (h->nranks > 1 || h->force_halo)) || !persist_on(h)) {
         // per-launch kernels (row strips): the hardware refills freed wave
         // slots, so band height matters less; stored fraction / slots per word
         // (16384-wide strips: 55.6 vs 51.2 TCUPS for wpl 2 vs 1, profiles/r1e)
@@ -313,6 +324,9 @@ int depth_index(int d) {
     return i;
 }
 
+// Per-launch kernel with paired bands (gol_tb_pair_kernel; needs the fill skip).
+bool tb_paired(golhip_t h) { return h->paired_bands && h->fill_skip; }
+
 // Rows per wave for a launch of `depth` turns: the user's value, or the
 // automatic choice (wave slots = CUs x resident waves per CU).
 int rows_per_wave_for(golhip_t h, int depth) {
@@ -320,8 +334,8 @@ int rows_per_wave_for(golhip_t h, int depth) {
     int &c = h->auto_rpw[depth_index(depth)];
     if (c == 0) {
         const int wpl = wpl_for(h);
-        const int slots = h->cu_count * golk::tb_blocks_per_cu(depth, wpl) * 4;
-        c = golk::auto_rows_per_wave(h->Ww, h->rows, depth, std::max(slots, 1), h->fill_skip, wpl);
+        const int slots = h->cu_count * golk::tb_wave_slots_per_cu(depth, wpl, tb_paired(h));
+        c = golk::auto_rows_per_wave(h->Ww, h->rows, depth, std::max(slots, 1), h->fill_skip, wpl, tb_paired(h));
     }
     return c;
 }
@@ -399,8 +413,9 @@ int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int
     } else if (h->rows_per_wave > 0) {
         a.rows_per_wave = h->rows_per_wave;
     } else {
-        const int slots = h->cu_count * golk::tb_blocks_per_cu(depth, wpl) * 4;
-        a.rows_per_wave = golk::auto_rows_per_wave(h->Ww, a.rows_out, depth, std::max(slots, 1), h->fill_skip, wpl);
+        const int slots = h->cu_count * golk::tb_wave_slots_per_cu(depth, wpl, tb_paired(h));
+        a.rows_per_wave = golk::auto_rows_per_wave(h->Ww, a.rows_out, depth, std::max(slots, 1), h->fill_skip, wpl,
+                                                     tb_paired(h));
     }
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->flags & GOLHIP_FLAG_TIMING) {
@@ -411,7 +426,7 @@ int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int
     }
     hipError_t e;
     if (h->W % 32 == 0)
-        e = golk::launch_step_tb(a, depth, st, h->fill_skip, wpl);
+        e = golk::launch_step_tb(a, depth, st, h->fill_skip, wpl, tb_paired(h));
     else
         e = golk::launch_step_generic(a, st);
     if (e != hipSuccess) return fail(GOLHIP_EHIP, "step launch: %s", hipGetErrorString(e));
@@ -475,7 +490,7 @@ int check_persist(golhip_t h) {
     h->persist_pending = false;
     if (*h->h_err) {
         *h->h_err = 0;
-        h->persistent = false;
+        h->persistent = 0;
         return fail(GOLHIP_EHIP, "persistent step kernel timed out waiting for a neighbour workgroup "
                                  "(not all workgroups resident?); board state is undefined, persistent mode disabled");
     }
@@ -491,7 +506,7 @@ int sync_stream(golhip_t h) {
 // run (0 if the persistent path does not apply).
 int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     *rc = GOLHIP_OK;
-    if (!h->persistent || h->W % 32 != 0 || !h->torus()) return 0;
+    if (!persist_on(h) || h->W % 32 != 0 || !h->torus()) return 0;
     const int wpl = wpl_for(h);
     const int depth = largest_depth(std::min(h->persist_depth > 0 ? h->persist_depth : h->tb_depth,
                                              golk::max_depth_for(wpl)));
@@ -740,7 +755,8 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         return GOLHIP_OK;
     }
     if (!strcmp(key, "persistent")) {
-        h->persistent = value != 0;
+        if (value < -1 || value > 1) return fail(GOLHIP_EINVAL, "persistent %lld", (long long)value);
+        h->persistent = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "persist_depth")) {
@@ -767,6 +783,7 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     if (!strcmp(key, "paired_bands")) {
         if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "paired_bands %lld", (long long)value);
         h->paired_bands = (int)value;
+        for (int &c : h->auto_rpw) c = 0;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "persist_wg_tx")) {

@@ -103,9 +103,15 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * depend on them.  "fill_skip" (default 1): skip pipeline-fill stage-rows;
  * "wpl" (default 0 = auto): words per lane, 1 or 2 (2 runs on the
  * interleaved pair layout, converted at the I/O boundary); "persistent"
- * (default 1): resident multi-super-step kernel for long runs on a whole
- * torus; "persist_depth" (default 0 = tb_depth): turns per super-step;
+ * (default -1 = auto: on for buffers of at most 64 MiB; 1 on, 0 off):
+ * resident multi-super-step kernel for long runs on a whole torus;
+ * "persist_depth" (default 0 = tb_depth): turns per super-step;
  * "persist_waves" (0 = auto, 8 or 16): waves per persistent workgroup;
+ * "paired_bands" (default 1): the two waves of a SIMD stream one two-band
+ * region from both ends and meet where they meet; "age_split" (-1 = auto,
+ * 0 = equal, else %): static taller bands for the older waves when pairing
+ * is off; "persist_wg_tx" (0 = plan): tiles across a persistent workgroup;
+ * "dummy_rows" (0 = all halo rows): rows that absorb masked stores;
  * "trace" (0): persistent-kernel diagnostics (golhip_persist_trace);
  * "force_halo" (0): after golhip_comm_init with one rank, run a whole board
  * through the multi-GPU path as a one-rank RCCL ring (tests, measurement). */

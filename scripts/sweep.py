@@ -21,7 +21,7 @@ ap.add_argument("--repeats", type=int, default=1)
 a = ap.parse_args()
 variants = [v for v in a.variants.split(";") if v] or [""]
 # engine options are sticky on a handle: every variant starts from the defaults
-DEFAULTS = {"wpl": 0, "persistent": 1, "persist_depth": 0, "persist_waves": 0, "persist_wg_tx": 0, "dummy_rows": 0, "age_split": -1,
+DEFAULTS = {"wpl": 0, "persistent": -1, "persist_depth": 0, "persist_waves": 0, "persist_wg_tx": 0, "dummy_rows": 0, "age_split": -1, "paired_bands": 1,
             "fill_skip": 1}
 for N in map(int, a.sizes.split(",")):
     b = golhip.Board(N, N, timing=True)

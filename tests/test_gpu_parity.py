@@ -484,3 +484,25 @@ def test_persistent_paired_bands(coracle, N, rows, depth, wpl, nw, tx):
         assert b.perf()["persist_launches"] == 1
         assert np.array_equal(b.snapshot_bytes(), want)
         assert b.alive_count() == (int((want == 255).sum()), turns)
+
+
+@pytest.mark.parametrize("N,rows,depth,wpl,rpw", [(2048, 1024, 16, 1, 0), (4096, 2048, 16, 2, 0), (1984, 999, 8, 2, 37),
+                                                  (3968, 1001, 4, 1, 5), (2048, 77, 2, 1, 3), (1024, 513, 32, 1, 50),
+                                                  (4096, 300, 1, 2, 7)])
+@pytest.mark.parametrize("paired", [1, 0])
+def test_per_launch_paired_bands(coracle, N, rows, depth, wpl, rpw, paired):
+    """Per-launch kernel with SIMD mates meeting inside a two-band region (gol_tb_pair_kernel) vs the C oracle."""
+    board = coracle.fill_random(N, rows, 0x5EED0011)
+    turns = 3 * depth + 1
+    want = coracle.run(board, turns)
+    with golhip.Board(N, rows) as b:
+        b.set_option("persistent", 0)
+        b.set_option("wpl", wpl)
+        b.set_option("paired_bands", paired)
+        b.set_tb_depth(depth)
+        b.set_rows_per_wave(rpw)
+        b.load_bytes(board)
+        b.step(turns)
+        assert b.perf()["persist_launches"] == 0
+        assert np.array_equal(b.snapshot_bytes(), want)
+        assert b.alive_count() == (int((want == 255).sum()), turns)
