@@ -201,7 +201,9 @@ def main():
         kname, launches, kms, kturns = "gol_persist_kernel", perf["persist_launches"], perf["persist_kernel_ms"], \
             perf["persist_turns"]
     else:
-        kname, launches, kms, kturns = "gol_tb_kernel", perf["step_launches"], perf["step_kernel_ms"], perf["step_turns"]
+        # per-launch K1: the paired-band kernel (engine default, paired_bands = fill_skip = 1)
+        kname, launches, kms, kturns = "gol_tb_pair_kernel", perf["step_launches"], perf["step_kernel_ms"], \
+            perf["step_turns"]
     launches = max(1, launches)
     avg_ms = kms / launches
     alg_bytes_per_launch = W * rows * (kturns / launches) * ALG_BYTES_PER_UPDATE
@@ -210,8 +212,8 @@ def main():
     try:
         with open(a.pmc) as f:
             rec = json.load(f).get(f"{N}:{kname}")
-        if rec:
-            traffic = rec["hbm_bytes_per_launch"]
+        if rec:  # measured per profiled launch; scaled to this run's turns per launch
+            traffic = rec["hbm_bytes_per_launch"] / rec.get("turns_per_launch", kturns / launches) * (kturns / launches)
     except (OSError, ValueError):
         pass
 
@@ -252,7 +254,8 @@ def main():
             "note": "achieved = 0.25 B/cell-update (SURVEY 8d) x cell-updates per launch / avg launch time; "
                     "a launch fuses many turns, so frac > 1 means temporal blocking beat the single-pass "
                     "HBM roofline (the kernel is VALU-bound, see DESIGN.md 5); traffic = measured HBM bytes "
-                    "per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE) from profiles/pmc_traffic.json",
+                    "per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per turn, profiles/pmc_traffic.json, "
+                    "times this run's turns per launch)",
         },
         "final_alive": alive,
         "final_turn": at_turn,

@@ -14,7 +14,7 @@ import sys
 src = sys.argv[1]
 dst = sys.argv[2]
 out = json.load(open(dst)) if os.path.exists(dst) else {}
-KERNELS = ("gol_persist_kernel", "gol_tb_kernel")
+KERNELS = ("gol_persist_kernel", "gol_tb_kernel", "gol_tb_pair_kernel")
 for size, kname in [(s, k) for s in (16384, 65536, 262144) for k in KERNELS]:
     vals = {}
     durs = []
@@ -31,6 +31,8 @@ for size, kname in [(s, k) for s in (16384, 65536, 262144) for k in KERNELS]:
     rec = {"fetch_size_bytes_raw": f, "fetch_bytes_corrected": 2 * f, "write_bytes": w,
            "hbm_bytes_per_launch": 2 * f + w, "board_bytes": size * size / 8, "launches": len(vals["FETCH_SIZE"]),
            "kernel": kname,
+           # prof_step.py: a persistent launch runs 4 super-steps of 16 turns, a per-launch one 16 turns
+           "turns_per_launch": 64 if kname == "gol_persist_kernel" else 16,
            "note": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes, scripts/prof_step.py; "
                    "Infinity-Cache hits are counted (a board <= 256 MiB is cache-resident)"}
     if "SQ_INSTS_VALU" in vals:
