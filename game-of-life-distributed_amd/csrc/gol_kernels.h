@@ -11,7 +11,7 @@ namespace golk {
 // exchange (strip mode) and unused in torus mode.
 // Halo rows above and below a strip buffer (== GOLHIP_HALO_ROWS): deeper than
 // one launch (GOLHIP_MAX_TB_DEPTH) so one exchange can feed several launches.
-constexpr int kHalo = 64;
+constexpr int kHalo = 128;
 constexpr int kWave = 64;
 constexpr int kTileValid = 62;   // lanes per wavefront tile that are stored (lanes 1..62)
 
@@ -35,7 +35,8 @@ struct StepArgs {
     RowMap in;
     int rows_per_wave;
     int dummy_rows;   // >= 1 leading physical rows of dst usable as store dummies
-    unsigned long long *alive;  // nullable: += popcount of the output
+    unsigned long long *alive;  // nullable: += popcount of the output rows [count_lo, count_hi)
+    int count_lo, count_hi;
 };
 
 // Bit-sliced temporal-blocked step: `depth` in {1,2,4,8,16,32}; requires W % 32 == 0
@@ -53,7 +54,8 @@ int tb_wave_slots_per_cu(int depth, int wpl, bool paired);  // resident waves pe
 // Rows per wavefront minimising (rounds of waves) x (rows streamed per wave).
 int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_skip, int wpl, bool paired = false);
 
-// Persistent multi-super-step step kernel (torus mode); see gol_kernels.hip K1p.
+// Persistent multi-super-step step kernel (torus, or a strip's extended rows
+// between two deep-halo exchanges); see gol_kernels.hip K1p.
 struct PersistArgs {
     StepArgs base;            // rows_out, in-map, dst_base, W/Ww, alive (last super-step)
     uint32_t *buf0, *buf1;    // the two physical boards

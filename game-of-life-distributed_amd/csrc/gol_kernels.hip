@@ -291,6 +291,9 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
     int lim = claim ? 0 : rows_here;  // output rows [0, lim) of this wave's order are its own
     uint32_t *const dummy = a.dst + (size_t)(wave_id % a.dummy_rows) * Ww + col;
     uint32_t cnt = 0;
+    // output rows counted into the popcount, in this wave's out_idx order
+    const int clo = dir > 0 ? a.count_lo - r0 : r0 + rows_here - a.count_hi;
+    const int chi = dir > 0 ? a.count_hi - r0 : r0 + rows_here - a.count_lo;
     auto emit = [&](const Lanes<WPL> &y, int out_idx) {
         const bool ok = keep && (unsigned)out_idx < (unsigned)lim;
         uint32_t *p = ok ? dst_row0 + (ptrdiff_t)out_idx * dst_step : dummy;
@@ -302,7 +305,7 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
             *reinterpret_cast<uint2 *>(p) = make_uint2(y.w[0], y.w[1]);
             pc = __builtin_popcount(y.w[0]) + __builtin_popcount(y.w[1]);
         }
-        cnt += ok ? pc : 0u;
+        cnt += (ok && out_idx >= clo && out_idx < chi) ? pc : 0u;
     };
 
     uint32_t h0[3][D][WPL], h1[3][D][WPL], cc[3][D][WPL];

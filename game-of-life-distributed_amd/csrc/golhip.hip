@@ -227,7 +227,9 @@ int default_depth(golhip_t h, int wpl) { return largest_depth(std::min(h->tb_dep
 int persist_nw_for(golhip_t h, int depth, int wpl) {
     if (h->persist_waves > 0) return h->persist_waves;
     const int def = golk::persist_waves_for(depth, wpl);
-    if (def == 16 && plan_rate(h, wpl, 8, depth) > plan_rate(h, wpl, 16, depth)) return 8;
+    if (def == 16 && plan_rate(h, wpl, 8, depth) > plan_rate(h, wpl, 16, depth) &&
+        golk::persist_blocks_per_cu(depth, wpl, 8) >= 1)  // (depth, wpl, 8) instantiated
+        return 8;
     return def;
 }
 
@@ -235,11 +237,13 @@ int persist_nw_for(golhip_t h, int depth, int wpl) {
 // MALL (16384^2: 61 vs 58 TCUPS); on larger boards the per-launch kernel is
 // as fast or faster and far steadier from box to box (65536^2: 114-116 vs
 // 96-120 TCUPS over six boxes, 262144^2: 126 vs 105, profiles/r1f), so
-// "auto" keeps K1p for buffers of at most 64 MiB.
+// "auto" keeps K1p for buffers of at most 64 MiB (sched_rows: every rank of
+// a ring decides alike, as the choice also fixes the word layout).  A row
+// strip runs K1p between two deep-halo exchanges (golhip_step).
 constexpr int64_t kPersistAutoMaxBytes = 64ll << 20;
 bool persist_on(golhip_t h) {
     if (h->persistent >= 0) return h->persistent != 0;
-    return h->local_words() * 4 <= kPersistAutoMaxBytes;
+    return (int64_t)sched_rows(h) * h->Ww * 4 <= kPersistAutoMaxBytes;
 }
 
 // Words per lane of the step kernels: 2 (interleaved pair layout) cuts the
@@ -248,8 +252,8 @@ bool persist_on(golhip_t h) {
 int wpl_for(golhip_t h) {
     if (h->W % 64 != 0) return 1;
     if (h->wpl_opt == 1 || h->wpl_opt == 2) return h->wpl_opt;
-    if ((h->comm && (h->nranks > 1 || h->force_halo)) || !persist_on(h)) {
-        // per-launch kernels (row strips): the hardware refills freed wave
+    if ((!h->torus() && !h->comm) || !persist_on(h)) {
+        // per-launch kernels (group strips, large boards): the hardware refills freed wave
         // slots, so band height matters less; stored fraction / slots per word
         // (16384-wide strips: 55.6 vs 51.2 TCUPS for wpl 2 vs 1, profiles/r1e)
         auto rate = [&](int wpl) {
@@ -315,6 +319,8 @@ golk::StepArgs step_args(golhip_t h, unsigned long long *alive, bool halo) {
     a.rows_per_wave = h->rows_per_wave;
     a.dummy_rows = h->dummy_rows > 0 ? h->dummy_rows : kHalo;
     a.alive = alive;
+    a.count_lo = 0;
+    a.count_hi = a.rows_out;
     return a;
 }
 
@@ -395,18 +401,25 @@ int exchange_rccl(golhip_t h, int depth, hipStream_t st) {
     return GOLHIP_OK;
 }
 
+// Halo mode: output rows [lo, hi) instead of [0, rows) (the deep-halo
+// extension), counting only [0, rows).
+void shift_rows(golk::StepArgs &a, int lo, int hi) {
+    const int rows = a.rows_out;  // the handle's rows (step_args)
+    a.rows_out = hi - lo;
+    a.dst_base = kHalo + lo;
+    a.in.off = kHalo + lo;
+    a.dummy_rows = std::max(1, std::min(a.dummy_rows, kHalo + std::min(lo, 0)));  // rows above the outputs
+    a.count_lo = -lo;
+    a.count_hi = -lo + rows;
+}
+
 // Launch the step kernel for output rows [lo, hi) of this handle (halos, if
 // used, already in place); `alive` (nullable) accumulates their popcount.
 // No bookkeeping: see finish_launch.
 int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int lo, int hi) {
     const hipStream_t st = h->stream;
     golk::StepArgs a = step_args(h, alive, halo);
-    if (lo != 0 || hi != h->rows) {  // other row range (halo mode only): shift the row maps
-        a.rows_out = hi - lo;
-        a.dst_base = kHalo + lo;
-        a.in.off = kHalo + lo;
-        a.dummy_rows = std::max(1, std::min(a.dummy_rows, kHalo + std::min(lo, 0)));  // rows above the outputs
-    }
+    if (lo != 0 || hi != h->rows) shift_rows(a, lo, hi);
     const int wpl = wpl_for(h);
     if (a.rows_out == h->rows) {
         a.rows_per_wave = rows_per_wave_for(h, depth);
@@ -502,26 +515,19 @@ int sync_stream(golhip_t h) {
     return check_persist(h);
 }
 
-// J super-steps of `depth` turns in one resident launch; returns the turns
-// run (0 if the persistent path does not apply).
-int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
+// One resident launch of J super-steps of `depth` turns over the rows of
+// `base` (count: the popcount of its last super-step goes to d_scalars);
+// returns false (with *rc == 0) when no workgroup plan fits.
+bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int wpl, bool count, int *rc) {
     *rc = GOLHIP_OK;
-    if (!persist_on(h) || h->W % 32 != 0 || !h->torus()) return 0;
-    const int wpl = wpl_for(h);
-    const int depth = largest_depth(std::min(h->persist_depth > 0 ? h->persist_depth : h->tb_depth,
-                                             golk::max_depth_for(wpl)));
-    if (depth < 4) return 0;
-    const int64_t J = left / depth;
-    if (J < 2) return 0;
     const int nw = persist_nw_for(h, depth, wpl);
-    if (golk::persist_blocks_per_cu(depth, wpl, nw) < 1) return 0;
+    if (golk::persist_blocks_per_cu(depth, wpl, nw) < 1) return false;
     golk::PersistArgs p{};
-    // With two waves per SIMD the older one is served first and finishes its
-    // band early; giving the older half of the waves 65 % of the rows lets
-    // both finish together (16384^2: 59 -> 64 TCUPS, profiles/r1f).
+    // Unpaired fallback: with two waves per SIMD the older one is served
+    // first, so the older half of the waves gets 65 % of the rows.
     const int age_split = h->age_split >= 0 ? h->age_split : (nw == 8 ? 65 : 0);
     const bool split = age_split > 0 && age_split < 100;
-    if (!golk::plan_persist(h->Ww, h->rows, depth, h->cu_count, wpl, nw, &p, h->persist_wg_tx)) return 0;
+    if (!golk::plan_persist(h->Ww, base.rows_out, depth, h->cu_count, wpl, nw, &p, h->persist_wg_tx)) return false;
     if (h->paired_bands && p.wg_sy >= 2 && p.wg_sy % 2 == 0) {
         // the older and the younger wave of a SIMD stream a shared two-band
         // region from both ends and meet where the arbiter's service put them
@@ -539,17 +545,17 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
         if (hipMalloc(&h->d_sync, (size_t)(h->cu_count + 2) * sizeof(unsigned)) != hipSuccess ||
             hipHostMalloc(&h->h_err, sizeof(unsigned), hipHostMallocDefault) != hipSuccess) {
             *rc = fail(GOLHIP_ENOMEM, "persistent sync words");
-            return 0;
+            return false;
         }
         *h->h_err = 0;
     }
-    const bool count = count_last && J * depth == left;
     if (count) {
         hipError_t e = hipMemsetAsync(h->d_scalars, 0, sizeof(unsigned long long), h->stream);
-        if (e != hipSuccess) { *rc = fail(GOLHIP_EHIP, "memset: %s", hipGetErrorString(e)); return 0; }
+        if (e != hipSuccess) { *rc = fail(GOLHIP_EHIP, "memset: %s", hipGetErrorString(e)); return false; }
     }
     hipError_t e = hipMemsetAsync(h->d_sync, 0, (size_t)(h->cu_count + 2) * sizeof(unsigned), h->stream);
-    p.base = step_args(h, count ? h->d_scalars : nullptr, false);
+    p.base = base;
+    p.base.alive = count ? h->d_scalars : nullptr;
     p.buf0 = h->buf[0];
     p.buf1 = h->buf[1];
     p.first = h->cur;
@@ -573,7 +579,7 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     if (e == hipSuccess) e = hipMemcpyAsync(h->h_err, h->d_sync, sizeof(unsigned), hipMemcpyDeviceToHost, h->stream);
     if (e != hipSuccess) {
         *rc = fail(GOLHIP_EHIP, "persistent launch: %s", hipGetErrorString(e));
-        return 0;
+        return false;
     }
     h->persist_pending = true;
     if (J & 1) h->cur ^= 1;
@@ -581,7 +587,41 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     h->persist_turns += J * depth;
     h->persist_launches++;
     if (count) h->alive_turn = h->turns;
+    return true;
+}
+
+int persist_depth_for(golhip_t h, int wpl) {
+    return largest_depth(std::min(h->persist_depth > 0 ? h->persist_depth : h->tb_depth, golk::max_depth_for(wpl)));
+}
+
+// Torus: J super-steps of `depth` turns in one resident launch; returns the
+// turns run (0 if the persistent path does not apply).
+int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
+    *rc = GOLHIP_OK;
+    if (!persist_on(h) || h->W % 32 != 0 || !h->torus()) return 0;
+    const int wpl = wpl_for(h);
+    const int depth = persist_depth_for(h, wpl);
+    if (depth < 4) return 0;
+    const int64_t J = left / depth;
+    if (J < 2) return 0;
+    const bool count = count_last && J * depth == left;
+    if (!persist_launch(h, step_args(h, nullptr, false), J, depth, wpl, count, rc)) return 0;
     return J * depth;
+}
+
+// Row strip between two deep-halo exchanges of k * d rows: the k launches of
+// d turns as one resident launch of k super-steps over the rows
+// [-(k-1) d, rows + (k-1) d) (the outer rows go stale one super-step at a
+// time, as in the per-launch trapezoid, and are never read by a kept row).
+bool try_persist_halo(golhip_t h, int d, int k, bool count, int *rc) {
+    *rc = GOLHIP_OK;
+    if (!persist_on(h) || h->W % 32 != 0 || k < 2 || d < 4) return false;
+    const int wpl = wpl_for(h);
+    if (d != persist_depth_for(h, wpl)) return false;
+    const int e = (k - 1) * d;
+    golk::StepArgs a = step_args(h, nullptr, true);
+    shift_rows(a, -e, h->rows + e);
+    return persist_launch(h, a, k, d, wpl, count, rc);
 }
 
 int start_flips(golhip_t h) {
@@ -942,6 +982,12 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
         }
         const int k = halo_launches(sched_rows(h), d, left - tail);
         if (int rc = exchange_rccl(h, k * d, h->stream)) return rc;
+        int prc = GOLHIP_OK;
+        if (try_persist_halo(h, d, k, left - k * d == 0, &prc)) {
+            left -= (int64_t)k * d;
+            continue;
+        }
+        if (prc) return prc;
         for (int i = 0; i < k; ++i) {
             if (int rc = launch_ext(h, d, left - d == 0, (k - 1 - i) * d)) return rc;
             left -= d;

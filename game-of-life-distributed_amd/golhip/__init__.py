@@ -21,7 +21,7 @@ GOLHIP_ERANGE = -4
 FLAG_TIMING = 0x1
 UNIQUE_ID_BYTES = 128
 MAX_TB_DEPTH = 32
-HALO_ROWS = 64  # GOLHIP_HALO_ROWS
+HALO_ROWS = 128  # GOLHIP_HALO_ROWS
 
 
 class GolHipError(RuntimeError):

@@ -50,7 +50,7 @@ extern "C" {
 
 #define GOLHIP_UNIQUE_ID_BYTES 128 /* == sizeof(ncclUniqueId)                 */
 #define GOLHIP_MAX_TB_DEPTH 32     /* max turns fused in one step launch      */
-#define GOLHIP_HALO_ROWS 64        /* halo rows above/below a strip buffer    */
+#define GOLHIP_HALO_ROWS 128       /* halo rows above/below a strip buffer    */
 
 typedef struct golhip golhip;
 typedef golhip *golhip_t;
@@ -104,7 +104,8 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * "wpl" (default 0 = auto): words per lane, 1 or 2 (2 runs on the
  * interleaved pair layout, converted at the I/O boundary); "persistent"
  * (default -1 = auto: on for buffers of at most 64 MiB; 1 on, 0 off):
- * resident multi-super-step kernel for long runs on a whole torus;
+ * resident multi-super-step kernel for long runs on a whole torus and,
+ * in a ring, for the launches between two deep-halo exchanges;
  * "persist_depth" (default 0 = tb_depth): turns per super-step;
  * "persist_waves" (0 = auto, 8 or 16): waves per persistent workgroup;
  * "paired_bands" (default 1): the two waves of a SIMD stream one two-band

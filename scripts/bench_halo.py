@@ -14,6 +14,7 @@ sys.path.insert(0, os.path.join(ROOT, "game-of-life-distributed_amd"))
 import golhip  # noqa: E402
 
 VARIANTS = (("persistent_torus", {}), ("per_launch_torus", {"persistent": 0}), ("rccl_ring", {"force_halo": 1}),
+            ("rccl_ring_launch", {"force_halo": 1, "persistent": 0}),
             ("rccl_ring_wpl1", {"force_halo": 1, "wpl": 1}), ("rccl_ring_wpl2", {"force_halo": 1, "wpl": 2}))
 
 

@@ -64,10 +64,11 @@ def test_halo_plan_rejects_depth_above_strip():
         golhip.halo_plan(64, 128, 2, 0, golhip.HALO_ROWS + 1)
 
 
-@pytest.mark.parametrize("rows,tb,left,want", [(16384, 16, 1000, (16, 4)), (16384, 16, 40, (16, 2)),
-                                               (16384, 32, 1000, (32, 2)), (40, 16, 1000, (16, 2)),
+@pytest.mark.parametrize("rows,tb,left,want", [(16384, 16, 1000, (16, 8)), (16384, 16, 40, (16, 2)),
+                                               (16384, 32, 1000, (32, 4)), (40, 16, 1000, (16, 2)),
                                                (10, 16, 1000, (8, 1)), (16384, 16, 7, (4, 1)),
-                                               (16384, 1, 100, (1, 64))])
+                                               (16384, 1, 100, (1, 100)), (16384, 1, 1000, (1, 128)),
+                                               (100, 16, 1000, (16, 6))])
 def test_halo_schedule(rows, tb, left, want):
     """k launches of d turns per exchange of k * d <= GOLHIP_HALO_ROWS rows, k * d <= strip rows."""
     d, k = golhip.halo_schedule(rows, tb, left)

@@ -404,22 +404,30 @@ def test_interleaved_fill_random_and_strips(coracle):
 
 # ---------------------------------------------------------------- RCCL halo path on one GPU
 @pytest.mark.parametrize("W,H,depth", [(512, 512, 16), (512, 512, 4), (1024, 768, 8), (2048, 1024, 32),
-                                       (640, 200, 16), (4096, 96, 16), (4096, 40, 16), (1000, 300, 4)])
-def test_rccl_halo_ring_one_rank(coracle, W, H, depth):
-    """The multi-GPU path (RCCL send/recv of deep halo rows, per-launch kernels
-    on extended row ranges) run as a one-rank ring over the whole board
-    (option force_halo) vs the C oracle."""
+                                       (640, 200, 16), (4096, 96, 16), (4096, 40, 16), (1000, 300, 4),
+                                       (2048, 2048, 16), (1984, 1500, 8)])
+@pytest.mark.parametrize("persistent", [-1, 0])
+def test_rccl_halo_ring_one_rank(coracle, W, H, depth, persistent):
+    """The multi-GPU path (RCCL send/recv of deep halo rows, then the resident
+    kernel over the extended rows or per-launch kernels on shrinking ranges)
+    run as a one-rank ring over the whole board (option force_halo) vs the C
+    oracle."""
     board = coracle.fill_random(W, H, 0x5EED000E)
-    turns = 3 * depth + 5
+    turns = 5 * depth + 5
     want = coracle.run(board, turns)
     with golhip.Board(W, H) as b:
         b.comm_init(golhip.unique_id(), 1, 0)
         b.set_option("force_halo", 1)
+        b.set_option("persistent", persistent)
         b.set_tb_depth(depth)
         b.load_bytes(board)
         b.step(turns)
         p = b.perf()
-        assert p["persist_launches"] == 0 and p["halo_bytes"] > 0
+        assert p["halo_bytes"] > 0
+        if persistent == 0:
+            assert p["persist_launches"] == 0
+        elif W % 32 == 0 and depth >= 4 and H >= 4 * depth:
+            assert p["persist_launches"] > 0
         assert np.array_equal(b.snapshot_bytes(), want)
         assert b.alive_count() == (int((want == 255).sum()), turns)
         b.step(1, want_flips=True)
@@ -428,17 +436,18 @@ def test_rccl_halo_ring_one_rank(coracle, W, H, depth):
 
 
 def test_rccl_halo_ring_full_size():
-    """16384^2 through the one-rank RCCL ring (deep halos) == the persistent torus kernel."""
+    """16384^2 through the one-rank RCCL ring (deep halos; resident and per-launch kernels) == the torus kernel."""
     res = []
-    for halo in (1, 0):
+    for halo in (1, 2, 0):
         with golhip.Board(16384, 16384) as b:
             if halo:
                 b.comm_init(golhip.unique_id(), 1, 0)
                 b.set_option("force_halo", 1)
+                b.set_option("persistent", 1 if halo == 1 else 0)
             b.fill_random(0x5EED0001)
             b.step(200)
             res.append((b.board_hash(), b.alive_count()))
-    assert res[0] == res[1]
+    assert res[0] == res[1] == res[2]
 
 
 @pytest.mark.parametrize("N,depth,wpl,nw,split,tx", [(2048, 16, 1, 8, 70, 1), (4096, 16, 2, 8, 80, 1),
