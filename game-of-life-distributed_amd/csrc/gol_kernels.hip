@@ -245,7 +245,18 @@ __device__ __forceinline__ Lanes<WPL> vmov(const Lanes<WPL> &v) {
 // from the other end) the wave takes its output rows three at a time from the
 // counter and stops when the two fronts meet, so the band splits wherever the
 // SIMD arbiter's service left the two waves.
-template <int D, bool SKIP, int WPL>
+// Output stores (STORE): kStoreDeferred = masked, one group late (K1);
+// kStoreMasked = masked, right after the group; kStoreDummy = unconditional,
+// masked rows to a dummy row (wave_id % dummy_rows of dst).
+[[maybe_unused]] constexpr int kStoreDeferred = 0, kStoreMasked = 1, kStoreDummy = 2;
+#ifndef GOL_PERSIST_STORE
+#define GOL_PERSIST_STORE 2
+#endif
+#ifndef GOL_PAIR_STORE
+#define GOL_PAIR_STORE 0
+#endif
+
+template <int D, bool SKIP, int WPL, int STORE = kStoreDeferred, bool LATE_CLAIM = true>
 __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int rows_here, int t0, int wave_id,
                                                 int dir = 1, int *claim = nullptr) {
     const int lane = threadIdx.x & 63;
@@ -279,13 +290,17 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
         return v;
     };
 
-    // Output rows are stored unconditionally so the whole 3-row group is one
-    // basic block (the scheduler can then overlap stage t of row i+1 with
-    // stage t+1 of row i): pipeline-fill rows and halo lanes write to a dummy
-    // address in one of the first `dummy_rows` physical rows (halo rows that
-    // are no output of this launch and not read before they are rewritten),
-    // spread over waves: one shared dummy line written by every wave of a
-    // tile column serialises in L2.
+    // Output stores, by STORE: kStoreDeferred stores under the lane mask
+    // (halo lanes, pipeline-fill rows and rows past the band or the meeting
+    // row store nothing) and one group late: a group's stores are issued at
+    // the top of the next body, just before its prefetch loads, so the
+    // in-order vmcnt wait for those loads at the bottom of that body also
+    // covers the stores, a whole group after they were issued (stores issued
+    // right after the group are followed straight away by that wait, which
+    // then stalls on their acks: 97 -> 115 TCUPS for K1 at 65536^2 on the
+    // boxes where it did).  kStoreMasked stores right away under the mask;
+    // kStoreDummy stores unconditionally, masked rows/lanes to a dummy row
+    // (one of the first `dummy_rows` physical rows of dst, spread over waves).
     uint32_t *const dst_row0 = a.dst + (size_t)(a.dst_base + (dir > 0 ? r0 : r0 + rows_here - 1)) * Ww + col;
     const ptrdiff_t dst_step = dir > 0 ? (ptrdiff_t)Ww : -(ptrdiff_t)Ww;
     int lim = claim ? 0 : rows_here;  // output rows [0, lim) of this wave's order are its own
@@ -296,15 +311,24 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
     const int chi = dir > 0 ? a.count_hi - r0 : r0 + rows_here - a.count_lo;
     auto emit = [&](const Lanes<WPL> &y, int out_idx) {
         const bool ok = keep && (unsigned)out_idx < (unsigned)lim;
-        uint32_t *p = ok ? dst_row0 + (ptrdiff_t)out_idx * dst_step : dummy;
         uint32_t pc = 0;
-        if constexpr (WPL == 1) {
-            *p = y.w[0];
-            pc = __builtin_popcount(y.w[0]);
-        } else {
-            *reinterpret_cast<uint2 *>(p) = make_uint2(y.w[0], y.w[1]);
-            pc = __builtin_popcount(y.w[0]) + __builtin_popcount(y.w[1]);
+        if constexpr (STORE == kStoreDummy) {
+            uint32_t *p = ok ? dst_row0 + (ptrdiff_t)out_idx * dst_step : dummy;
+            if constexpr (WPL == 1)
+                *p = y.w[0];
+            else
+                *reinterpret_cast<uint2 *>(p) = make_uint2(y.w[0], y.w[1]);
+        } else if (ok) {
+            uint32_t *p = dst_row0 + (ptrdiff_t)out_idx * dst_step;
+            if constexpr (WPL == 1)
+                *p = y.w[0];
+            else
+                *reinterpret_cast<uint2 *>(p) = make_uint2(y.w[0], y.w[1]);
         }
+        if constexpr (WPL == 1)
+            pc = __builtin_popcount(y.w[0]);
+        else
+            pc = __builtin_popcount(y.w[0]) + __builtin_popcount(y.w[1]);
         cnt += (ok && out_idx >= clo && out_idx < chi) ? pc : 0u;
     };
 
@@ -344,17 +368,42 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
             }
         }
     };
-    fill(std::integral_constant<int, D / 4>());
-    fill(std::integral_constant<int, D / 2>());
-    fill(std::integral_constant<int, 3 * D / 4>());
-    bool more = true;
+#if GOL_FILL_PHASES == 8
+    if constexpr (D >= 8) {  // eighths: closer to the exact triangle, more code
+        fill(std::integral_constant<int, D / 8>());
+        fill(std::integral_constant<int, 2 * D / 8>());
+        fill(std::integral_constant<int, 3 * D / 8>());
+        fill(std::integral_constant<int, 4 * D / 8>());
+        fill(std::integral_constant<int, 5 * D / 8>());
+        fill(std::integral_constant<int, 6 * D / 8>());
+        fill(std::integral_constant<int, 7 * D / 8>());
+    } else
+#endif
+    {
+        fill(std::integral_constant<int, D / 4>());
+        fill(std::integral_constant<int, D / 2>());
+        fill(std::integral_constant<int, 3 * D / 4>());
+    }
+    bool more = true, pend = false;
+    Lanes<WPL> q0, q1, q2;  // the previous group's output rows (stored one body late)
+    int qoi = 0;
     for (; claim ? more : oi < rows_here; oi += 3) {
+        if (STORE == kStoreDeferred && pend) {
+            emit(q0, qoi);
+            emit(q1, qoi + 1);
+            emit(q2, qoi + 2);
+        }
         const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
-        // claim this group's rows >= 0 (the LDS round trip hides under the group)
+        // claim this group's rows >= 0; the LDS round trip hides under the group
         const int need = claim ? min(3, max(0, oi + 3)) : 0;
-        int old = 0;
-        if (need > 0) {
-            int o = 0;
+        // LATE_CLAIM: wait for the LDS round trip after the group rather than
+        // before it.  Measured per kernel (profiles/r1g): K1 65536^2 115 (late)
+        // vs 96 TCUPS (early); K1p 16384^2 54 (late) vs 59 (early).
+        int old = 0, o = 0;
+        if constexpr (LATE_CLAIM) {
+            if (need > 0 && lane == 0)
+                o = __hip_atomic_fetch_add(claim, -need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if (need > 0) {
             if (lane == 0) o = __hip_atomic_fetch_add(claim, -need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             old = __builtin_amdgcn_readfirstlane(o);
         }
@@ -362,16 +411,33 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
         Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
         push_group<D, D, WPL>(y0, y1, y2, h0, h1, cc);
         if (need > 0) {
+            if constexpr (LATE_CLAIM) {
+                asm volatile("" : "+v"(o));  // keep the LDS wait here, after the group
+                old = __builtin_amdgcn_readfirstlane(o);
+            }
             lim = max(oi, 0) + min(need, max(0, old));
             more = old > need;
         }
-        emit(y0, oi);
-        emit(y1, oi + 1);
-        emit(y2, oi + 2);
+        if constexpr (STORE == kStoreDeferred) {
+            q0 = y0;
+            q1 = y1;
+            q2 = y2;
+            qoi = oi;
+            pend = true;
+        } else {
+            emit(y0, oi);
+            emit(y1, oi + 1);
+            emit(y2, oi + 2);
+        }
         __builtin_amdgcn_sched_barrier(0);
         x0 = vmov(n0);
         x1 = vmov(n1);
         x2 = vmov(n2);
+    }
+    if (STORE == kStoreDeferred && pend) {
+        emit(q0, qoi);
+        emit(q1, qoi + 1);
+        emit(q2, qoi + 2);
     }
     return cnt;
 }
@@ -416,7 +482,7 @@ __global__ __launch_bounds__(512) void gol_tb_pair_kernel(StepArgs a) {
     if (w < 4 && lane == 0) s_claim[w] = len;
     __syncthreads();
     if (len == 0) return;  // wave-uniform, after the only barrier
-    const uint32_t cnt = stream_band<D, true, WPL>(a, r0, len, tile * tile_words(WPL), blockIdx.x * 8 + w,
+    const uint32_t cnt = stream_band<D, true, WPL, GOL_PAIR_STORE, true>(a, r0, len, tile * tile_words(WPL), blockIdx.x * 8 + w,
                                                    w < 4 ? 1 : -1, &s_claim[w & 3]);
     if (a.alive) {
         const uint32_t tot = wave_sum_u32(cnt);
@@ -527,7 +593,8 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
             // every claim of super-step j-1 is done (barrier above): re-arm its counter for j+1
             if (w < NW / 2 && lane == 0) s_claim[(j + 1) & 1][w] = rows_here;
         }
-        cnt = rows_here > 0 ? stream_band<D, true, WPL>(a, r0, rows_here, tile * tile_words(WPL), b * NW + w, dir, claim)
+        cnt = rows_here > 0 ? stream_band<D, true, WPL, GOL_PERSIST_STORE, false>(a, r0, rows_here, tile * tile_words(WPL), b * NW + w,
+                                                                            dir, claim)
                             : 0u;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         {

@@ -13,7 +13,7 @@ import re
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgolhip.so")
+LIB_PATH = os.environ.get("GOLHIP_LIB") or os.path.join(HERE, "libgolhip.so")  # override: A/B builds
 HEADER = os.path.join(HERE, "..", "..", "include", "golhip.h")
 
 GOLHIP_OK = 0
