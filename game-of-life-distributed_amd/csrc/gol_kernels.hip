@@ -630,7 +630,8 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
 }
 
 // ---- host-side dispatch over (depth, fill skip, words per lane) ----------
-// WPL = 2 is instantiated up to depth 16 (depth 32 would exceed 256 VGPRs).
+// Depths 1, 2, 4, 8, 12, 16 (and 24, 32 for WPL = 1: depth 32 at WPL = 2 would
+// exceed 256 VGPRs); the host's depth_plan picks among them.
 template <typename F>
 static hipError_t dispatch(int depth, bool skip, int wpl, F &&f) {
 #define GOL_CASE(D, SK, WP) \
@@ -638,6 +639,8 @@ static hipError_t dispatch(int depth, bool skip, int wpl, F &&f) {
     GOL_CASE(1, true, 1) GOL_CASE(2, true, 1) GOL_CASE(4, true, 1) GOL_CASE(8, true, 1) GOL_CASE(16, true, 1)
     GOL_CASE(32, true, 1) GOL_CASE(1, false, 1) GOL_CASE(2, false, 1) GOL_CASE(4, false, 1) GOL_CASE(8, false, 1)
     GOL_CASE(16, false, 1) GOL_CASE(32, false, 1)
+    GOL_CASE(12, true, 1) GOL_CASE(24, true, 1) GOL_CASE(12, false, 1) GOL_CASE(24, false, 1)
+    GOL_CASE(12, true, 2) GOL_CASE(12, false, 2)
     GOL_CASE(1, true, 2) GOL_CASE(2, true, 2) GOL_CASE(4, true, 2) GOL_CASE(8, true, 2) GOL_CASE(16, true, 2)
     GOL_CASE(1, false, 2) GOL_CASE(2, false, 2) GOL_CASE(4, false, 2) GOL_CASE(8, false, 2) GOL_CASE(16, false, 2)
 #undef GOL_CASE
@@ -659,6 +662,7 @@ static hipError_t dispatch_pair(int depth, int wpl, F &&f) {
     if (depth == D && wpl == WP) return f(gol_tb_pair_kernel<D, WP>);
     GOL_QCASE(1, 1) GOL_QCASE(2, 1) GOL_QCASE(4, 1) GOL_QCASE(8, 1) GOL_QCASE(16, 1) GOL_QCASE(32, 1)
     GOL_QCASE(1, 2) GOL_QCASE(2, 2) GOL_QCASE(4, 2) GOL_QCASE(8, 2) GOL_QCASE(16, 2)
+    GOL_QCASE(12, 1) GOL_QCASE(24, 1) GOL_QCASE(12, 2)
 #undef GOL_QCASE
     return hipErrorInvalidValue;
 }

@@ -16,6 +16,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <climits>
+#include <functional>
 #include <atomic>
 #include <cstdarg>
 #include <cstdio>
@@ -63,7 +65,10 @@ int fail(int code, const char *fmt, ...) {
         if (r_ != ncclSuccess) return fail(GOLHIP_ERCCL, "%s: %s", #expr, ncclGetErrorString(r_)); \
     } while (0)
 
-constexpr int kDepths[] = {32, 16, 8, 4, 2, 1};
+// Turns per launch with an instantiated step kernel (24: one word per lane
+// only, as 32; see max_depth_for).
+constexpr int kDepths[] = {32, 24, 16, 12, 8, 4, 2, 1};
+constexpr int kNumDepths = sizeof(kDepths) / sizeof(kDepths[0]);
 // trace buffer: 8 totals + (start, end) per (workgroup < 1024, wave < 64)
 constexpr int64_t kTraceWords = 8 + 2 * 1024 * 64;
 
@@ -99,7 +104,7 @@ struct golhip {
     unsigned *h_err = nullptr;  // pinned copy of the error word
     bool persist_pending = false;
     int64_t persist_launches = 0;
-    int auto_rpw[6] = {0, 0, 0, 0, 0, 0};  // cache per depth index
+    int auto_rpw[kNumDepths] = {};  // cache per depth index
     bool loaded = false;
     bool il = false;            // board words in the interleaved pair layout (wpl = 2 kernels)
     std::atomic<int64_t> turns{0};
@@ -200,6 +205,45 @@ int largest_depth(int64_t want) {
     return 1;
 }
 
+// The next run of launches for `left` turns of at most `cap` turns each:
+// depth d and how many launches of d come next.  The schedule has the fewest
+// launches and, among those, the largest smallest launch, in descending
+// order: 100 turns at cap 16 run as 4 x 16 + 3 x 12, not 6 x 16 + 4 (a
+// 4-turn launch costs about as much as a 16-turn one on a large board:
+// 65536^2 x 100 turns ran at 108 vs 122 TCUPS kernel-only).  Far from the
+// end the run is `cap` turns; the last 3-4 caps are planned exactly.
+struct DepthRun {
+    int d;
+    int64_t n;
+};
+DepthRun depth_plan(int cap, int64_t left) {
+    const int M = largest_depth(std::max(1, cap));
+    if (left <= 0) return {M, 0};
+    const int64_t head = std::max<int64_t>(0, left / M - 3);  // launches of M before the planned tail
+    const int t = (int)(left - head * M);                     // < 4 M <= 128
+    // best[v] = (launches, -smallest launch) for v turns; pick[v] = first depth
+    std::vector<int> nl(t + 1, INT_MAX), mn(t + 1, 0), pick(t + 1, 0);
+    nl[0] = 0;
+    mn[0] = INT_MAX;
+    for (int v = 1; v <= t; ++v)
+        for (int d : kDepths) {  // descending: ties keep the larger depth
+            if (d > M || d > v || nl[v - d] == INT_MAX) continue;
+            const int n = nl[v - d] + 1, m = std::min(mn[v - d], d);
+            if (n < nl[v] || (n == nl[v] && m > mn[v])) {
+                nl[v] = n;
+                mn[v] = m;
+                pick[v] = d;
+            }
+        }
+    std::vector<int> seq;
+    for (int v = t; v > 0; v -= pick[v]) seq.push_back(pick[v]);
+    std::sort(seq.begin(), seq.end(), std::greater<int>());
+    const int d = head > 0 ? M : seq[0];
+    int64_t n = head;
+    for (int x : seq) n += (x == d);
+    return {d, n};
+}
+
 // Rows the launch schedule (depth, exchange depth, words per lane) is derived
 // from: in a multi-rank ring every rank must pick the same values, so they
 // all use the ring's smallest strip.
@@ -286,14 +330,17 @@ int loaded_canonical(golhip_t h) {
     return set_layout(h, want_il(h));
 }
 
-// How many turns the next launch fuses.  In halo mode the `depth` halo rows
-// must all come from one neighbour strip, so depth <= strip rows.
-int next_depth(golhip_t h, int64_t remaining, bool halo) {
+// Most turns one launch may fuse.  In halo mode the `depth` halo rows must
+// all come from one neighbour strip, so depth <= strip rows.
+int depth_cap(golhip_t h, bool halo) {
     if (h->W % 32 != 0) return 1;  // generic kernel: one turn per launch
-    int64_t cap = std::min<int64_t>(std::min(h->tb_depth, golk::max_depth_for(wpl_for(h))), remaining);
-    if (halo) cap = std::min<int64_t>(cap, sched_rows(h));
-    return largest_depth(cap);
+    int cap = std::min(h->tb_depth, golk::max_depth_for(wpl_for(h)));
+    if (halo) cap = std::min(cap, sched_rows(h));
+    return cap;
 }
+
+// How many turns the next launch fuses (depth_plan).
+int next_depth(golhip_t h, int64_t remaining, bool halo) { return depth_plan(depth_cap(h, halo), remaining).d; }
 
 // torus mode: the handle holds the whole board and wraps rows itself;
 // halo mode: rows outside the strip come from the halo rows.
@@ -325,9 +372,9 @@ golk::StepArgs step_args(golhip_t h, unsigned long long *alive, bool halo) {
 }
 
 int depth_index(int d) {
-    int i = 0;
-    while ((1 << i) < d) ++i;
-    return i;
+    for (int i = 0; i < kNumDepths; ++i)
+        if (kDepths[i] == d) return i;
+    return kNumDepths - 1;
 }
 
 // Per-launch kernel with paired bands (gol_tb_pair_kernel; needs the fill skip).
@@ -480,8 +527,8 @@ int launch_depth(golhip_t h, int depth, bool count, bool halo) {
 // from the wider halo (the trapezoid: output row -ext needs input rows
 // -ext - depth .. , all inside the k * depth received rows).  The extension
 // costs 2 * ext extra rows per launch; it saves k - 1 of every k exchanges.
-int halo_launches(int rows, int depth, int64_t left) {
-    const int64_t k = std::min<int64_t>({(int64_t)kHalo / depth, left / depth, (int64_t)rows / depth});
+int halo_launches(int rows, int depth, int64_t run) {
+    const int64_t k = std::min<int64_t>({(int64_t)kHalo / depth, run, (int64_t)rows / depth});
     return (int)std::max<int64_t>(1, k);
 }
 
@@ -892,9 +939,9 @@ int golhip_halo_schedule(int32_t strip_rows, int32_t tb_depth, int64_t turns_lef
                          int32_t *launches) {
     if (!depth || !launches || strip_rows <= 0 || tb_depth < 1 || tb_depth > GOLHIP_MAX_TB_DEPTH || turns_left < 1)
         return fail(GOLHIP_EINVAL, "bad halo schedule request");
-    const int d = largest_depth(std::min<int64_t>({(int64_t)tb_depth, turns_left, (int64_t)strip_rows}));
-    *depth = d;
-    *launches = halo_launches(strip_rows, d, turns_left);
+    const DepthRun run = depth_plan(std::min(tb_depth, strip_rows), turns_left);
+    *depth = run.d;
+    *launches = halo_launches(strip_rows, run.d, run.n);
     return GOLHIP_OK;
 }
 
@@ -974,13 +1021,14 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
         if (rc) return rc;
     }
     while (left > tail) {
-        const int d = next_depth(h, left - tail, halo);
+        const DepthRun run = depth_plan(depth_cap(h, halo), left - tail);
+        const int d = run.d;
         if (!halo) {
             if (int rc = launch_depth(h, d, left - d == 0, false)) return rc;
             left -= d;
             continue;
         }
-        const int k = halo_launches(sched_rows(h), d, left - tail);
+        const int k = halo_launches(sched_rows(h), d, run.n);
         if (int rc = exchange_rccl(h, k * d, h->stream)) return rc;
         int prc = GOLHIP_OK;
         if (try_persist_halo(h, d, k, left - k * d == 0, &prc)) {
@@ -1026,13 +1074,14 @@ int golhip_group_step(golhip_t *hs, int32_t n, int64_t nturns) {
     }
     int64_t left = nturns;
     while (left > 0 && rc == GOLHIP_OK) {
-        int d = GOLHIP_MAX_TB_DEPTH;
-        for (int i = 0; i < n; ++i) d = std::min(d, next_depth(hs[i], left, n > 1));
-        d = largest_depth(d);
+        int cap = GOLHIP_MAX_TB_DEPTH;
+        for (int i = 0; i < n; ++i) cap = std::min(cap, depth_cap(hs[i], n > 1));
+        const DepthRun run = depth_plan(cap, left);
+        const int d = run.d;
         int k = 1;
         if (n > 1) {
             k = kHalo / d;
-            for (int i = 0; i < n; ++i) k = std::min(k, halo_launches(hs[i]->rows, d, left));
+            for (int i = 0; i < n; ++i) k = std::min(k, halo_launches(hs[i]->rows, d, run.n));
             const int x = k * d;  // rows exchanged
             for (int i = 0; i < n && !rc; ++i) {
                 HIP_RC(hipSetDevice(hs[i]->device));

@@ -64,7 +64,7 @@ def test_halo_plan_rejects_depth_above_strip():
         golhip.halo_plan(64, 128, 2, 0, golhip.HALO_ROWS + 1)
 
 
-@pytest.mark.parametrize("rows,tb,left,want", [(16384, 16, 1000, (16, 8)), (16384, 16, 40, (16, 2)),
+@pytest.mark.parametrize("rows,tb,left,want", [(16384, 16, 1000, (16, 8)), (16384, 16, 40, (16, 1)),
                                                (16384, 32, 1000, (32, 4)), (40, 16, 1000, (16, 2)),
                                                (10, 16, 1000, (8, 1)), (16384, 16, 7, (4, 1)),
                                                (16384, 1, 100, (1, 100)), (16384, 1, 1000, (1, 128)),
@@ -74,3 +74,41 @@ def test_halo_schedule(rows, tb, left, want):
     d, k = golhip.halo_schedule(rows, tb, left)
     assert (d, k) == want
     assert d * k <= min(golhip.HALO_ROWS, max(rows, d)) and d * k <= left
+
+
+@pytest.mark.parametrize("rows,tb,left,want", [
+    (65536, 16, 100, [(16, 4), (12, 3)]),          # not 6 x 16 + 4: no short tail launch
+    (16384, 16, 40, [(16, 1), (12, 2)]),
+    (16384, 32, 100, [(32, 2), (24, 1), (12, 1)]),
+    (16384, 16, 20, [(12, 1), (8, 1)]),
+    (16384, 16, 7, [(4, 1), (2, 1), (1, 1)]),
+    (16384, 16, 36, [(12, 3)]),
+])
+def test_halo_schedule_sequence(rows, tb, left, want):
+    """The whole schedule (golhip.hip depth_plan): fewest launches, then the
+    largest smallest launch, in descending depth order."""
+    seq, l = [], left
+    while l > 0:
+        d, k = golhip.halo_schedule(rows, tb, l)
+        seq.append((d, k))
+        l -= d * k
+    assert seq == want
+
+
+@pytest.mark.parametrize("tb", [1, 4, 12, 16, 32])
+def test_halo_schedule_covers_turns(tb):
+    for left in list(range(1, 200)) + [999, 1000, 10000]:
+        seq, l = [], left
+        while l > 0:
+            d, k = golhip.halo_schedule(1 << 20, tb, l)
+            assert 1 <= d <= tb and 1 <= k and d * k <= min(golhip.HALO_ROWS, l)
+            seq += [d] * k
+            l -= d * k
+        assert sum(seq) == left and seq == sorted(seq, reverse=True)
+        # never more launches than the greedy power-of-two schedule
+        g, r = 0, left
+        while r > 0:
+            d = 1 << (min(r, tb).bit_length() - 1)
+            r -= d
+            g += 1
+        assert len(seq) <= g

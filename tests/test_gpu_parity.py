@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 golhip = pytest.importorskip("golhip")
 
 CHECKS = [(16, 0), (16, 1), (16, 100), (64, 0), (64, 1), (64, 100), (512, 0), (512, 1), (512, 100)]
-DEPTHS = [1, 2, 4, 8, 16, 32]
+DEPTHS = [1, 2, 4, 8, 12, 16, 24, 32]
 
 
 @pytest.fixture(scope="module")
@@ -167,7 +167,7 @@ def test_depth_and_strip_height_invariance(fixtures, depth, rpw, fill_skip, wpl)
 
 @pytest.mark.parametrize("W,H", [(32, 1), (32, 3), (64, 2), (96, 7), (2016, 9), (1984, 33), (4000 - 4000 % 32, 40),
                                  (8192, 5), (320, 1000), (6272, 70), (7936, 20), (8064, 12), (128, 64)])
-@pytest.mark.parametrize("depth", [1, 8, 32])
+@pytest.mark.parametrize("depth", [1, 8, 12, 32])
 @pytest.mark.parametrize("wpl", [1, 2])
 def test_random_shapes(W, H, depth, wpl):
     """Widths that are 1..many tiles (62 x wpl stored words/tile), heights below the depth."""
@@ -270,9 +270,10 @@ def test_group_strips_large_random_hash():
 
 
 # ---------------------------------------------------------------- full-size properties
-@pytest.mark.parametrize("N,turns", [(16384, 256), (65536, 32)])
+@pytest.mark.parametrize("N,turns", [(16384, 256), (65536, 32), (65536, 100)])
 def test_full_size_depth_invariance(N, turns):
-    """BASELINE configs 2/3 at full size: fused depths 32 / 16 / 1 agree (digest + count)."""
+    """BASELINE configs 2/3 at full size: fused depths 32 / 16 / 1 agree (digest + count);
+    65536^2 x 100 turns is the bench step (launches of 16, 16, 16, 16, 12, 12, 12 turns)."""
     res = []
     for depth in (32, 16, 1):
         with golhip.Board(N, N) as b:
