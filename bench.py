@@ -246,7 +246,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
             "traffic": traffic,
-            "kernel": f"{kname}<{perf['tb_depth']}>",
+            "kernel": f"{kname}<{perf['tb_depth']}, {perf['words_per_lane']}>",
             "avg_launch_ms": round(avg_ms, 5),
             "launches": launches,
             "turns_per_launch": kturns / launches,

@@ -85,12 +85,12 @@ hipError_t launch_pack(const uint8_t *bytes, uint32_t *words, int W, int Ww, int
 // il: the words are in the interleaved pair layout of the wpl = 2 step kernels
 // (W % 64 == 0); pack / fill_random / load write canonical words, which the
 // engine converts in place with launch_convert_layout.
-hipError_t launch_unpack(const uint32_t *words, uint8_t *bytes, int W, int Ww, int rows, bool il, hipStream_t s);
-hipError_t launch_convert_layout(uint32_t *words, int64_t nwords, bool to_il, hipStream_t s);
+hipError_t launch_unpack(const uint32_t *words, uint8_t *bytes, int W, int Ww, int rows, int il, hipStream_t s);
+hipError_t launch_convert_layout(uint32_t *words, int64_t nwords, int from, int to, hipStream_t s);
 hipError_t launch_fill_random(uint32_t *words, int W, int Ww, int rows, int64_t row0, uint64_t seed,
                               hipStream_t s);
 hipError_t launch_popcount(const uint32_t *words, int64_t nwords, unsigned long long *out, hipStream_t s);
-hipError_t launch_hash(const uint32_t *words, int64_t nwords, int64_t word0, unsigned long long *out, bool il,
+hipError_t launch_hash(const uint32_t *words, int64_t nwords, int64_t word0, unsigned long long *out, int il,
                        hipStream_t s);
 
 // Row-major compaction of set bits of (a ^ b) (b nullable -> a alone) into
@@ -101,7 +101,7 @@ hipError_t launch_compact_count(const uint32_t *a, const uint32_t *b, int64_t nw
                                 hipStream_t s);
 hipError_t launch_compact_scan(unsigned long long *blk, int64_t nblk, unsigned long long *total, hipStream_t s);
 hipError_t launch_compact_scatter(const uint32_t *a, const uint32_t *b, int64_t nwords, int Ww,
-                                  int64_t row0, const unsigned long long *blk_off, int32_t *xy, bool il,
+                                  int64_t row0, const unsigned long long *blk_off, int32_t *xy, int il,
                                   hipStream_t s);
 
 }  // namespace golk

@@ -113,31 +113,79 @@ __host__ __device__ __forceinline__ void il_decode(uint32_t e, uint32_t o, uint3
     a = shuffle32((e & 0xFFFFu) | (o << 16));
     b = shuffle32((e >> 16) | (o & 0xFFFF0000u));
 }
-// Canonical word i of a board stored in layout `il`.
-__device__ __forceinline__ uint32_t canon_word(const uint32_t *w, int64_t i, bool il) {
-    if (!il) return w[i];
-    uint32_t a, b;
-    il_decode(w[i & ~(int64_t)1], w[i | 1], a, b);
-    return (i & 1) ? b : a;
+// Interleaved quad layout (four words per lane, W % 128 == 0): word 4q + j of
+// a row holds the cells 128q + 4k + j in bit k.  It is the pair layout applied
+// twice: the pair encoding of (a, b) and (c, d) gives the even and odd cells
+// of each 64-cell half; pairing the two even-cell words (e1, e2) again splits
+// them into cells 4k (j = 0) and 4k + 2 (j = 2), the odd-cell words into
+// 4k + 1 (j = 1) and 4k + 3 (j = 3).
+__host__ __device__ __forceinline__ void il4_encode(const uint32_t (&c)[4], uint32_t (&w)[4]) {
+    uint32_t e1, o1, e2, o2;
+    il_encode(c[0], c[1], e1, o1);
+    il_encode(c[2], c[3], e2, o2);
+    il_encode(e1, e2, w[0], w[2]);
+    il_encode(o1, o2, w[1], w[3]);
+}
+__host__ __device__ __forceinline__ void il4_decode(const uint32_t (&w)[4], uint32_t (&c)[4]) {
+    uint32_t e1, o1, e2, o2;
+    il_decode(w[0], w[2], e1, e2);
+    il_decode(w[1], w[3], o1, o2);
+    il_decode(e1, o1, c[0], c[1]);
+    il_decode(e2, o2, c[2], c[3]);
+}
+// Canonical word i of a board stored in layout `il` (0 canonical, 2 pairs, 4 quads).
+__device__ __forceinline__ uint32_t canon_word(const uint32_t *w, int64_t i, int il) {
+    if (il == 0) return w[i];
+    if (il == 2) {
+        uint32_t a, b;
+        il_decode(w[i & ~(int64_t)1], w[i | 1], a, b);
+        return (i & 1) ? b : a;
+    }
+    const uint4 q = *reinterpret_cast<const uint4 *>(w + (i & ~(int64_t)3));
+    uint32_t c[4];
+    il4_decode({q.x, q.y, q.z, q.w}, c);
+    return c[i & 3];
 }
 
-__global__ __launch_bounds__(256) void convert_layout_kernel(uint32_t *__restrict__ w, int64_t npairs, int to_il) {
+// In place, one quad of words per thread: layout `from` -> canonical -> `to`.
+// Layout 4 implies W % 128 == 0 (whole quads); layout 2 only W % 64 == 0, so
+// the last "quad" of the buffer may be a single pair.
+__global__ __launch_bounds__(256) void convert_layout_kernel(uint32_t *__restrict__ w, int64_t nwords, int from, int to) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= npairs) return;
-    uint2 v = reinterpret_cast<uint2 *>(w)[i];
-    uint32_t p, q;
-    if (to_il)
-        il_encode(v.x, v.y, p, q);
-    else
-        il_decode(v.x, v.y, p, q);
-    reinterpret_cast<uint2 *>(w)[i] = make_uint2(p, q);
+    if (4 * i >= nwords) return;
+    if (4 * i + 4 > nwords) {  // a trailing pair: layouts 0 and 2 only
+        uint32_t *p = w + 4 * i, a = p[0], b = p[1];
+        if (from == 2) il_decode(p[0], p[1], a, b);
+        if (to == 2) il_encode(a, b, p[0], p[1]);
+        else p[0] = a, p[1] = b;
+        return;
+    }
+    const uint4 v = reinterpret_cast<uint4 *>(w)[i];
+    uint32_t x[4] = {v.x, v.y, v.z, v.w}, c[4];
+    if (from == 4) {
+        il4_decode(x, c);
+    } else if (from == 2) {
+        il_decode(x[0], x[1], c[0], c[1]);
+        il_decode(x[2], x[3], c[2], c[3]);
+    } else {
+        for (int k = 0; k < 4; ++k) c[k] = x[k];
+    }
+    if (to == 4) {
+        il4_encode(c, x);
+    } else if (to == 2) {
+        il_encode(c[0], c[1], x[0], x[1]);
+        il_encode(c[2], c[3], x[2], x[3]);
+    } else {
+        for (int k = 0; k < 4; ++k) x[k] = c[k];
+    }
+    reinterpret_cast<uint4 *>(w)[i] = make_uint4(x[0], x[1], x[2], x[3]);
 }
 
-hipError_t launch_convert_layout(uint32_t *words, int64_t nwords, bool to_il, hipStream_t s) {
-    const int64_t np = nwords / 2;
-    if (np == 0) return hipSuccess;
-    hipLaunchKernelGGL(convert_layout_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, words, np,
-                       to_il ? 1 : 0);
+hipError_t launch_convert_layout(uint32_t *words, int64_t nwords, int from, int to, hipStream_t s) {
+    if (from == to) return hipSuccess;
+    const int64_t nq = (nwords + 3) / 4;
+    if (nq == 0) return hipSuccess;
+    hipLaunchKernelGGL(convert_layout_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s, words, nwords, from, to);
     return hipGetLastError();
 }
 
@@ -183,6 +231,19 @@ __device__ __forceinline__ void stage(int t, Lanes<WPL> &x, uint32_t (&h0)[3][D]
         const uint32_t r = from_right_lane(x.w[0]);
         west[0] = __builtin_amdgcn_alignbit(x.w[0], l, 31);  // bit b = cell b-1
         east[0] = __builtin_amdgcn_alignbit(r, x.w[0], 1);   // bit b = cell b+1
+    } else if constexpr (WPL == 4) {
+        // interleaved quads: word j holds cells 4k + j, so every neighbour
+        // word but two is another word of the lane as is
+        const uint32_t l3 = from_left_lane(x.w[3]);   // left chunk's cells 4k + 3 (bit 31 = its cell 127)
+        const uint32_t r0 = from_right_lane(x.w[0]);  // right chunk's cells 4k (bit 0 = its cell 0)
+        west[0] = __builtin_amdgcn_alignbit(x.w[3], l3, 31);  // cell 4k - 1
+        west[1] = x.w[0];
+        west[2] = x.w[1];
+        west[3] = x.w[2];
+        east[0] = x.w[1];
+        east[1] = x.w[2];
+        east[2] = x.w[3];
+        east[3] = __builtin_amdgcn_alignbit(r0, x.w[0], 1);   // cell 4k + 4
     } else {
         const uint32_t l1 = from_left_lane(x.w[1]);   // left chunk's odd cells (bit 31 = its cell 63)
         const uint32_t r0 = from_right_lane(x.w[0]);  // right chunk's even cells (bit 0 = its cell 0)
@@ -261,7 +322,7 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
                                                 int dir = 1, int *claim = nullptr) {
     const int lane = threadIdx.x & 63;
     const int Ww = a.Ww;
-    int col = (t0 + WPL * (lane - 1)) % Ww;  // WPL = 2 needs Ww even: a pair never wraps
+    int col = (t0 + WPL * (lane - 1)) % Ww;  // WPL = 2 (4) needs Ww % 2 (4) == 0: a pair (quad) never wraps
     if (col < 0) col += Ww;
     const bool keep = lane >= 1 && lane <= kTileValid && (t0 + WPL * (lane - 1)) < Ww;
 
@@ -278,6 +339,12 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
         Lanes<WPL> v;
         if constexpr (WPL == 1) {
             v.w[0] = src[(size_t)pr * Ww];
+        } else if constexpr (WPL == 4) {
+            const uint4 q = *reinterpret_cast<const uint4 *>(src + (size_t)pr * Ww);
+            v.w[0] = q.x;
+            v.w[1] = q.y;
+            v.w[2] = q.z;
+            v.w[3] = q.w;
         } else {
             const uint2 q = *reinterpret_cast<const uint2 *>(src + (size_t)pr * Ww);
             v.w[0] = q.x;
@@ -312,23 +379,20 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
     auto emit = [&](const Lanes<WPL> &y, int out_idx) {
         const bool ok = keep && (unsigned)out_idx < (unsigned)lim;
         uint32_t pc = 0;
-        if constexpr (STORE == kStoreDummy) {
-            uint32_t *p = ok ? dst_row0 + (ptrdiff_t)out_idx * dst_step : dummy;
+        auto put = [&](uint32_t *p) {
             if constexpr (WPL == 1)
                 *p = y.w[0];
+            else if constexpr (WPL == 4)
+                *reinterpret_cast<uint4 *>(p) = make_uint4(y.w[0], y.w[1], y.w[2], y.w[3]);
             else
                 *reinterpret_cast<uint2 *>(p) = make_uint2(y.w[0], y.w[1]);
-        } else if (ok) {
-            uint32_t *p = dst_row0 + (ptrdiff_t)out_idx * dst_step;
-            if constexpr (WPL == 1)
-                *p = y.w[0];
-            else
-                *reinterpret_cast<uint2 *>(p) = make_uint2(y.w[0], y.w[1]);
-        }
-        if constexpr (WPL == 1)
-            pc = __builtin_popcount(y.w[0]);
-        else
-            pc = __builtin_popcount(y.w[0]) + __builtin_popcount(y.w[1]);
+        };
+        if constexpr (STORE == kStoreDummy)
+            put(ok ? dst_row0 + (ptrdiff_t)out_idx * dst_step : dummy);
+        else if (ok)
+            put(dst_row0 + (ptrdiff_t)out_idx * dst_step);
+#pragma unroll
+        for (int k = 0; k < WPL; ++k) pc += __builtin_popcount(y.w[k]);
         cnt += (ok && out_idx >= clo && out_idx < chi) ? pc : 0u;
     };
 
@@ -641,13 +705,15 @@ static hipError_t dispatch(int depth, bool skip, int wpl, F &&f) {
     GOL_CASE(16, false, 1) GOL_CASE(32, false, 1)
     GOL_CASE(12, true, 1) GOL_CASE(24, true, 1) GOL_CASE(12, false, 1) GOL_CASE(24, false, 1)
     GOL_CASE(12, true, 2) GOL_CASE(12, false, 2)
+    GOL_CASE(1, true, 4) GOL_CASE(2, true, 4) GOL_CASE(4, true, 4) GOL_CASE(8, true, 4)
+    GOL_CASE(1, false, 4) GOL_CASE(2, false, 4) GOL_CASE(4, false, 4) GOL_CASE(8, false, 4)
     GOL_CASE(1, true, 2) GOL_CASE(2, true, 2) GOL_CASE(4, true, 2) GOL_CASE(8, true, 2) GOL_CASE(16, true, 2)
     GOL_CASE(1, false, 2) GOL_CASE(2, false, 2) GOL_CASE(4, false, 2) GOL_CASE(8, false, 2) GOL_CASE(16, false, 2)
 #undef GOL_CASE
     return hipErrorInvalidValue;
 }
 
-int max_depth_for(int wpl) { return wpl == 2 ? 16 : 32; }
+int max_depth_for(int wpl) { return wpl == 4 ? 8 : wpl == 2 ? 16 : 32; }
 
 int tb_tiles(int Ww, int wpl) { return (Ww + tile_words(wpl) - 1) / tile_words(wpl); }
 
@@ -662,7 +728,7 @@ static hipError_t dispatch_pair(int depth, int wpl, F &&f) {
     if (depth == D && wpl == WP) return f(gol_tb_pair_kernel<D, WP>);
     GOL_QCASE(1, 1) GOL_QCASE(2, 1) GOL_QCASE(4, 1) GOL_QCASE(8, 1) GOL_QCASE(16, 1) GOL_QCASE(32, 1)
     GOL_QCASE(1, 2) GOL_QCASE(2, 2) GOL_QCASE(4, 2) GOL_QCASE(8, 2) GOL_QCASE(16, 2)
-    GOL_QCASE(12, 1) GOL_QCASE(24, 1) GOL_QCASE(12, 2)
+    GOL_QCASE(12, 1) GOL_QCASE(24, 1) GOL_QCASE(12, 2) GOL_QCASE(1, 4) GOL_QCASE(2, 4) GOL_QCASE(4, 4) GOL_QCASE(8, 4)
 #undef GOL_QCASE
     return hipErrorInvalidValue;
 }
@@ -869,7 +935,7 @@ __global__ __launch_bounds__(256) void pack_kernel(const uint8_t *__restrict__ b
 }
 
 __global__ __launch_bounds__(256) void unpack_kernel(const uint32_t *__restrict__ words, uint8_t *__restrict__ bytes,
-                                                      int W, int Ww, int rows, bool il) {
+                                                      int W, int Ww, int rows, int il) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (int64_t)rows * Ww) return;
     const int row = (int)(idx / Ww);
@@ -901,7 +967,7 @@ hipError_t launch_pack(const uint8_t *bytes, uint32_t *words, int W, int Ww, int
     return hipGetLastError();
 }
 
-hipError_t launch_unpack(const uint32_t *words, uint8_t *bytes, int W, int Ww, int rows, bool il, hipStream_t s) {
+hipError_t launch_unpack(const uint32_t *words, uint8_t *bytes, int W, int Ww, int rows, int il, hipStream_t s) {
     const int64_t n = (int64_t)rows * Ww;
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, words, bytes, W, Ww,
@@ -956,7 +1022,7 @@ hipError_t launch_popcount(const uint32_t *words, int64_t nwords, unsigned long 
 }
 
 __global__ __launch_bounds__(256) void hash_kernel(const uint32_t *__restrict__ w, int64_t n, int64_t word0,
-                                                    unsigned long long *out, bool il) {
+                                                    unsigned long long *out, int il) {
     unsigned long long h = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
@@ -965,7 +1031,7 @@ __global__ __launch_bounds__(256) void hash_kernel(const uint32_t *__restrict__ 
     if ((threadIdx.x & 63) == 0) atomicAdd(out, h);
 }
 
-hipError_t launch_hash(const uint32_t *words, int64_t nwords, int64_t word0, unsigned long long *out, bool il,
+hipError_t launch_hash(const uint32_t *words, int64_t nwords, int64_t word0, unsigned long long *out, int il,
                        hipStream_t s) {
     if (nwords == 0) return hipSuccess;
     const int64_t blocks = std::min<int64_t>((nwords + 255) / 256, 4096);
@@ -989,10 +1055,10 @@ __device__ __forceinline__ uint32_t cword(const uint32_t *a, const uint32_t *b, 
 }
 // Canonical (row-major cell order) word i of a ^ b.  Per block and per
 // thread chunk (kWpt even) the set-bit count is the same in either layout.
-__device__ __forceinline__ uint32_t cword_canon(const uint32_t *a, const uint32_t *b, int64_t i, bool il) {
+__device__ __forceinline__ uint32_t cword_canon(const uint32_t *a, const uint32_t *b, int64_t i, int il) {
     return b ? (canon_word(a, i, il) ^ canon_word(b, i, il)) : canon_word(a, i, il);
 }
-static_assert(kWpt % 2 == 0, "pairs must not straddle compaction chunks");
+static_assert(kWpt % 4 == 0, "pairs and quads must not straddle compaction chunks");
 
 __device__ uint32_t block_excl_scan(uint32_t v, uint32_t *total) {
     __shared__ uint32_t wsum[4];
@@ -1058,7 +1124,7 @@ __global__ __launch_bounds__(1024) void compact_scan_kernel(unsigned long long *
 __global__ __launch_bounds__(256) void compact_scatter_kernel(const uint32_t *__restrict__ a,
                                                                const uint32_t *__restrict__ b, int64_t n, int Ww,
                                                                int64_t row0, const unsigned long long *blk_off,
-                                                               int32_t *__restrict__ xy, bool il) {
+                                                               int32_t *__restrict__ xy, int il) {
     const int64_t base = (int64_t)blockIdx.x * kBlkWords + (int64_t)threadIdx.x * kWpt;
     uint32_t c = 0;
     for (int k = 0; k < kWpt; ++k)
@@ -1096,7 +1162,7 @@ hipError_t launch_compact_scan(unsigned long long *blk, int64_t nblk, unsigned l
 }
 
 hipError_t launch_compact_scatter(const uint32_t *a, const uint32_t *b, int64_t nwords, int Ww, int64_t row0,
-                                  const unsigned long long *blk_off, int32_t *xy, bool il, hipStream_t s) {
+                                  const unsigned long long *blk_off, int32_t *xy, int il, hipStream_t s) {
     const int64_t nb = compact_blocks(nwords);
     if (nb == 0) return hipSuccess;
     hipLaunchKernelGGL(compact_scatter_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, b, nwords, Ww, row0, blk_off,

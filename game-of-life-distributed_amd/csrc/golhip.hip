@@ -92,7 +92,7 @@ struct golhip {
     int cu_count = 0;
     bool fill_skip = true;      // option "fill_skip"
     int persistent = -1;        // option "persistent": K1p for long torus runs (1 on, 0 off, -1 auto)
-    int wpl_opt = 0;            // option "wpl": words per lane (0 = auto, 1, 2)
+    int wpl_opt = 0;            // option "wpl": words per lane (0 = auto, 1, 2, 4)
     int persist_depth = 0;      // option "persist_depth" (0: tb_depth)
     int persist_waves = 0;      // option "persist_waves": waves per workgroup (0: default)
     int age_split = -1;         // option "age_split": % of a workgroup's rows for its oldest waves (0: equal, -1: auto)
@@ -106,7 +106,7 @@ struct golhip {
     int64_t persist_launches = 0;
     int auto_rpw[kNumDepths] = {};  // cache per depth index
     bool loaded = false;
-    bool il = false;            // board words in the interleaved pair layout (wpl = 2 kernels)
+    int il = 0;                 // word layout of the board: 0 canonical, 2 interleaved pairs, 4 quads (= wpl)
     std::atomic<int64_t> turns{0};
 
     // side-channel scratch
@@ -256,12 +256,16 @@ int sched_rows(golhip_t h) { return (h->comm && h->nranks > 1 && h->ring_rows > 
 // DPP = 17 slots; wpl 2 interleaved: 9 + 1 + 1 half-rate = 13).  Fitted to
 // the round-1c sweeps (profiles/r1c): 16384^2 -> wpl 1 with 8 waves,
 // 65536^2 -> wpl 2.
+// VALU slots per word-turn: 9 LUTs + 2 half-rate DPP moves and 2 half-rate
+// funnel shifts per WPL words (interleaved layouts for WPL 2 and 4).
+double slots_per_word(int wpl) { return 9.0 + 8.0 / wpl; }
+
 double plan_rate(golhip_t h, int wpl, int nw, int depth) {
     const int tiles = golk::tb_tiles(h->Ww, wpl);
     const double util = (double)h->Ww / (tiles * 62.0 * wpl);
     const double S = (double)sched_rows(h) * tiles / std::max(1.0, (double)h->cu_count * nw);
     const double occ = nw >= 16 ? 1.0 : 0.95;
-    return util * S / (S + 1.75 * depth) * occ / (wpl == 2 ? 13.0 : 17.0);
+    return util * S / (S + 1.75 * depth) * occ / slots_per_word(wpl);
 }
 
 int default_depth(golhip_t h, int wpl) { return largest_depth(std::min(h->tb_depth, golk::max_depth_for(wpl))); }
@@ -296,14 +300,24 @@ bool persist_on(golhip_t h) {
 int wpl_for(golhip_t h) {
     if (h->W % 64 != 0) return 1;
     if (h->wpl_opt == 1 || h->wpl_opt == 2) return h->wpl_opt;
+    if (h->wpl_opt == 4) return h->W % 128 == 0 ? 4 : 2;
     if ((!h->torus() && !h->comm) || !persist_on(h)) {
         // per-launch kernels (group strips, large boards): the hardware refills freed wave
         // slots, so band height matters less; stored fraction / slots per word
         // (16384-wide strips: 55.6 vs 51.2 TCUPS for wpl 2 vs 1, profiles/r1e)
+        // Four words per lane (interleaved quads, 11 slots) run at most 8
+        // turns a launch (226 VGPRs); 8- vs 16-turn launches cost ~10 % per
+        // turn (fill, twice the HBM passes).  Measured, four vs two words per
+        // lane: 131072^2 127.6 vs 120.1 TCUPS, 262144^2 130.8 vs 122.4,
+        // 262144 x 32768 (an 8-GPU strip) 124.6 vs 118.5, but 65536^2 107.1
+        // vs 115.1 (9 tiles of 248 words for 2048), profiles/r1k; the model
+        // gives 65536^2 +0.5 %, hence the 3 % margin.
         auto rate = [&](int wpl) {
-            return (double)h->Ww / (golk::tb_tiles(h->Ww, wpl) * 62.0 * wpl) / (wpl == 2 ? 13.0 : 17.0);
+            const double deep = (wpl == 4 && h->tb_depth > golk::max_depth_for(4)) ? 0.9 : 1.0;
+            return (double)h->Ww / (golk::tb_tiles(h->Ww, wpl) * 62.0 * wpl) / slots_per_word(wpl) * deep;
         };
-        return rate(2) >= rate(1) ? 2 : 1;
+        const int two = rate(2) >= rate(1) ? 2 : 1;
+        return (h->W % 128 == 0 && rate(4) > 1.03 * rate(two)) ? 4 : two;
     }
     auto best = [&](int wpl) {
         const int d = default_depth(h, wpl);
@@ -316,16 +330,16 @@ int wpl_for(golhip_t h) {
 // The wpl = 2 step kernels run on the interleaved pair layout; every other
 // kernel reads canonical words (or is layout-agnostic: popcount, row halos).
 // Converts the current board in place when the wanted layout changes.
-int set_layout(golhip_t h, bool il) {
+int set_layout(golhip_t h, int il) {
     if (h->il == il) return GOLHIP_OK;
-    if (h->loaded) HIP_OR_FAIL(golk::launch_convert_layout(h->cur_rows(), h->local_words(), il, h->stream));
+    if (h->loaded) HIP_OR_FAIL(golk::launch_convert_layout(h->cur_rows(), h->local_words(), h->il, il, h->stream));
     h->il = il;
     return GOLHIP_OK;
 }
-bool want_il(golhip_t h) { return wpl_for(h) == 2; }
+int want_il(golhip_t h) { return wpl_for(h) >= 2 ? wpl_for(h) : 0; }
 // After canonical words were written into the current buffer.
 int loaded_canonical(golhip_t h) {
-    h->il = false;
+    h->il = 0;
     h->loaded = true;
     return set_layout(h, want_il(h));
 }
@@ -733,8 +747,12 @@ int create_common(int32_t width, int32_t height, int32_t row0, int32_t rows, int
     if (e == hipSuccess) h->own_stream = true;
     if (e == hipSuccess) e = hipMalloc(&h->buf[0], bytes);
     if (e == hipSuccess) e = hipMalloc(&h->buf[1], bytes);
-    if (e == hipSuccess) e = hipMemset(h->buf[0], 0, bytes);
-    if (e == hipSuccess) e = hipMemset(h->buf[1], 0, bytes);
+    // zeroed on the handle's own stream: it is non-blocking, so a plain
+    // hipMemset (null stream, asynchronous for device memory) could still be
+    // running when the first load / fill_random on `stream` writes the board
+    if (e == hipSuccess) e = hipMemsetAsync(h->buf[0], 0, bytes, h->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(h->buf[1], 0, bytes, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     if (e == hipSuccess) e = hipMalloc(&h->d_scalars, 4 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipHostMalloc(&h->h_scalars, 4 * sizeof(unsigned long long), hipHostMallocDefault);
     if (e != hipSuccess) {
@@ -836,7 +854,8 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     if (!key) return fail(GOLHIP_EINVAL, "null option");
     std::lock_guard<std::mutex> g(h->mu);
     if (!strcmp(key, "wpl")) {
-        if (value != 0 && value != 1 && value != 2) return fail(GOLHIP_EINVAL, "wpl %lld not in {0,1,2}", (long long)value);
+        if (value != 0 && value != 1 && value != 2 && value != 4)
+            return fail(GOLHIP_EINVAL, "wpl %lld not in {0,1,2,4}", (long long)value);
         h->wpl_opt = (int)value;
         for (int &c : h->auto_rpw) c = 0;
         return GOLHIP_OK;
@@ -882,7 +901,8 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         if (value && !h->d_trace) {
             if (hipMalloc(&h->d_trace, kTraceWords * sizeof(unsigned long long)) != hipSuccess)
                 return fail(GOLHIP_ENOMEM, "trace buffer");
-            if (hipMemset(h->d_trace, 0, kTraceWords * sizeof(unsigned long long)) != hipSuccess)
+            if (hipMemsetAsync(h->d_trace, 0, kTraceWords * sizeof(unsigned long long), h->stream) != hipSuccess ||
+                hipStreamSynchronize(h->stream) != hipSuccess)
                 return fail(GOLHIP_EHIP, "trace buffer memset");
         }
         return GOLHIP_OK;
@@ -924,7 +944,7 @@ int golhip_comm_init(golhip_t h, const uint8_t id[GOLHIP_UNIQUE_ID_BYTES], int32
     int32_t *d_rows = nullptr;
     HIP_OR_FAIL(hipMalloc(&d_rows, sizeof(int32_t)));
     int32_t rows = h->rows;
-    hipError_t e = hipMemcpy(d_rows, &rows, sizeof rows, hipMemcpyHostToDevice);
+    hipError_t e = hipMemcpyAsync(d_rows, &rows, sizeof rows, hipMemcpyHostToDevice, h->stream);
     ncclResult_t nr = e == hipSuccess ? ncclAllReduce(d_rows, d_rows, 1, ncclInt32, ncclMin, h->comm, h->stream) : ncclSuccess;
     if (e == hipSuccess && nr == ncclSuccess) e = hipStreamSynchronize(h->stream);
     if (e == hipSuccess && nr == ncclSuccess) e = hipMemcpy(&rows, d_rows, sizeof rows, hipMemcpyDeviceToHost);
@@ -1228,10 +1248,10 @@ int golhip_snapshot_bits(golhip_t h, uint32_t *out) {
     if (!out) return fail(GOLHIP_EINVAL, "out is null");
     std::lock_guard<std::mutex> g(h->mu);
     if (int rc = set_dev(h)) return rc;
-    const bool il = h->il;
-    if (il) HIP_OR_FAIL(golk::launch_convert_layout(h->cur_rows(), h->local_words(), false, h->stream));
+    const int il = h->il;
+    HIP_OR_FAIL(golk::launch_convert_layout(h->cur_rows(), h->local_words(), il, 0, h->stream));
     HIP_OR_FAIL(hipMemcpyAsync(out, h->cur_rows(), (size_t)h->local_words() * 4, hipMemcpyDeviceToHost, h->stream));
-    if (il) HIP_OR_FAIL(golk::launch_convert_layout(h->cur_rows(), h->local_words(), true, h->stream));
+    HIP_OR_FAIL(golk::launch_convert_layout(h->cur_rows(), h->local_words(), 0, il, h->stream));
     if (int rc_ = sync_stream(h)) return rc_;
     return GOLHIP_OK;
 }
@@ -1269,9 +1289,11 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     out->cell_updates = (int64_t)h->W * h->rows * (h->step_turns + h->persist_turns);
     out->alg_bytes = out->cell_updates / 4;
     out->halo_bytes = h->halo_bytes;
-    out->tb_depth = h->tb_depth;
-    out->rows_per_wave = rows_per_wave_for(h, next_depth(h, h->tb_depth, h->nranks > 1));
+    const bool halo = h->comm && (h->nranks > 1 || h->force_halo);
+    out->tb_depth = depth_cap(h, halo);
+    out->rows_per_wave = rows_per_wave_for(h, next_depth(h, h->tb_depth, halo));
     out->kernel_variant = h->W % 32 == 0 ? 1 : 0;
+    out->words_per_lane = h->W % 32 == 0 ? wpl_for(h) : 0;
     return GOLHIP_OK;
 }
 
@@ -1294,7 +1316,8 @@ int golhip_persist_trace(golhip_t h, uint64_t out[5]) {
     if (int rc = set_dev(h)) return rc;
     if (int rc = sync_stream(h)) return rc;
     HIP_OR_FAIL(hipMemcpy(out, h->d_trace, 5 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-    HIP_OR_FAIL(hipMemset(h->d_trace, 0, 8 * sizeof(unsigned long long)));
+    HIP_OR_FAIL(hipMemsetAsync(h->d_trace, 0, 8 * sizeof(unsigned long long), h->stream));
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
     return GOLHIP_OK;
 }
 

@@ -45,11 +45,11 @@ class Perf(ctypes.Structure):
         ("tb_depth", ctypes.c_int32),
         ("rows_per_wave", ctypes.c_int32),
         ("kernel_variant", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("words_per_lane", ctypes.c_int32),
     ]
 
     def as_dict(self) -> dict:
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class HaloPlan(ctypes.Structure):

@@ -66,10 +66,11 @@ typedef struct golhip_perf {
     int64_t cell_updates;     /* width * local rows * all stepped turns       */
     int64_t alg_bytes;        /* 0.25 B per cell-update (1 bit in + 1 bit out)*/
     int64_t halo_bytes;       /* bytes sent to neighbour ranks                */
-    int32_t tb_depth;         /* turns fused per step launch                  */
+    int32_t tb_depth;         /* most turns one step launch fuses (the setting,
+                                 capped by the kernel's words per lane)       */
     int32_t rows_per_wave;    /* rows streamed per wavefront (full-depth launch)*/
     int32_t kernel_variant;   /* 0 = generic (width % 32 != 0), 1 = bit-sliced*/
-    int32_t reserved;
+    int32_t words_per_lane;   /* 1, 2 (interleaved pairs) or 4 (quads); 0 generic */
 } golhip_perf_t;
 
 /* ---- library ---------------------------------------------------------- */

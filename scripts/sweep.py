@@ -18,13 +18,15 @@ ap.add_argument("--rpw", default="0,32,64,128,256,512,1024")
 ap.add_argument("--variants", default="", help="semicolon-separated option sets, e.g. 'fill_skip=0;fill_skip=1'")
 ap.add_argument("--turns", type=int, default=256)
 ap.add_argument("--repeats", type=int, default=1)
+ap.add_argument("--rows", type=int, default=0, help="board height (0 = square)")
 a = ap.parse_args()
 variants = [v for v in a.variants.split(";") if v] or [""]
 # engine options are sticky on a handle: every variant starts from the defaults
 DEFAULTS = {"wpl": 0, "persistent": -1, "persist_depth": 0, "persist_waves": 0, "persist_wg_tx": 0, "dummy_rows": 0, "age_split": -1, "paired_bands": 1,
             "fill_skip": 1}
 for N in map(int, a.sizes.split(",")):
-    b = golhip.Board(N, N, timing=True)
+    H = a.rows or N
+    b = golhip.Board(N, H, timing=True)
     b.fill_random(0x5EED0001)
     for d in map(int, a.depths.split(",")):
         for s in map(int, a.rpw.split(",")):
@@ -47,9 +49,9 @@ for N in map(int, a.sizes.split(",")):
                     p = b.perf()
                     kms = p["step_kernel_ms"] + p["persist_kernel_ms"]
                     kern = kms / max(1, p["step_launches"] + p["persist_launches"])
-                    rec = dict(N=N, depth=d, rpw=s, variant=v, rpw_used=p["rows_per_wave"], persist=p["persist_launches"],
-                               wall_gcups=N * N * a.turns / dt / 1e9,
-                               kernel_gcups=N * N * a.turns / (kms * 1e-3) / 1e9, launch_ms=kern)
+                    rec = dict(N=N, H=H, depth=d, rpw=s, variant=v, rpw_used=p["rows_per_wave"], persist=p["persist_launches"],
+                               wall_gcups=N * H * a.turns / dt / 1e9,
+                               kernel_gcups=N * H * a.turns / (kms * 1e-3) / 1e9, launch_ms=kern)
                     if rec["wall_gcups"] > best.get(v, {"wall_gcups": 0})["wall_gcups"]:
                         best[v] = rec
             for v in variants:

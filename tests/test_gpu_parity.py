@@ -159,7 +159,7 @@ def test_flips_after_multi_turn_step(fixtures):
 @pytest.mark.parametrize("depth", DEPTHS)
 @pytest.mark.parametrize("rpw", [0, 1, 2, 5, 37, 512])
 @pytest.mark.parametrize("fill_skip", [0, 1])
-@pytest.mark.parametrize("wpl", [1, 2])
+@pytest.mark.parametrize("wpl", [1, 2, 4])
 def test_depth_and_strip_height_invariance(fixtures, depth, rpw, fill_skip, wpl):
     board = img(fixtures, 256)
     assert np.array_equal(run_gpu(board, 70, depth, rpw, fill_skip=fill_skip, wpl=wpl), run_np(board, 70))
@@ -168,7 +168,7 @@ def test_depth_and_strip_height_invariance(fixtures, depth, rpw, fill_skip, wpl)
 @pytest.mark.parametrize("W,H", [(32, 1), (32, 3), (64, 2), (96, 7), (2016, 9), (1984, 33), (4000 - 4000 % 32, 40),
                                  (8192, 5), (320, 1000), (6272, 70), (7936, 20), (8064, 12), (128, 64)])
 @pytest.mark.parametrize("depth", [1, 8, 12, 32])
-@pytest.mark.parametrize("wpl", [1, 2])
+@pytest.mark.parametrize("wpl", [1, 2, 4])
 def test_random_shapes(W, H, depth, wpl):
     """Widths that are 1..many tiles (62 x wpl stored words/tile), heights below the depth."""
     rng = np.random.default_rng(W * 7 + H)
@@ -347,15 +347,18 @@ def test_persistent_waves_per_workgroup(coracle, N, depth, wpl, nw):
         assert b.alive_count() == (int((want == 255).sum()), turns)
 
 
-# ---------------------------------------------------------------- interleaved pair layout (wpl = 2)
-@pytest.mark.parametrize("W,H", [(1024, 96), (640, 128), (4096, 64)])
-def test_interleaved_layout_side_channels(coracle, W, H):
-    """wpl = 2 boards live in the interleaved pair layout: every canonical view
-    (bytes, bits, hash, flips, alive list) must be unaffected, including after
-    switching the layout mid-run and after load_bits."""
+# ------------------------------------------------ interleaved pair / quad layouts (wpl = 2, 4)
+@pytest.mark.parametrize("W,H", [(1024, 96), (640, 128), (4096, 64), (320, 33)])
+@pytest.mark.parametrize("wpl", [2, 4])
+def test_interleaved_layout_side_channels(coracle, W, H, wpl):
+    """wpl = 2 (4) boards live in the interleaved pair (quad) layout: every
+    canonical view (bytes, bits, hash, flips, alive list) must be unaffected,
+    including after switching the layout mid-run and after load_bits.  W = 320
+    (10 words a row, 33 rows) ends the buffer in half a quad; W % 128 != 0
+    runs wpl 4 as wpl 2."""
     board = coracle.fill_random(W, H, 0x5EED000B)
     with golhip.Board(W, H) as b:
-        b.set_option("wpl", 2)
+        b.set_option("wpl", wpl)
         b.load_bytes(board)
         assert np.array_equal(b.snapshot_bytes(), board)
         assert np.array_equal(b.snapshot_bits(), pack_bits(board))
@@ -371,8 +374,10 @@ def test_interleaved_layout_side_channels(coracle, W, H):
         b.step(7)
         want13 = coracle.run(board, 13)
         assert np.array_equal(b.snapshot_bits(), pack_bits(want13))
-        b.set_option("wpl", 2)
-        b.step(9, want_flips=True)
+        b.set_option("wpl", wpl)
+        b.step(4)
+        b.set_option("wpl", 6 - wpl)  # 2 <-> 4 directly
+        b.step(5, want_flips=True)
         want21, want22 = coracle.run(board, 21), coracle.run(board, 22)
         assert np.array_equal(b.flips(), flips_np(want21, want22))
         assert np.array_equal(b.snapshot_bytes(), want22)
@@ -383,15 +388,16 @@ def test_interleaved_layout_side_channels(coracle, W, H):
         assert b.alive_count() == (int((want22 == 255).sum()), 22)
 
 
-def test_interleaved_fill_random_and_strips(coracle):
-    """fill_random + in-process strips on a wpl = 2 board vs the C oracle."""
+@pytest.mark.parametrize("wpl", [2, 4])
+def test_interleaved_fill_random_and_strips(coracle, wpl):
+    """fill_random + in-process strips on a wpl = 2 / 4 board vs the C oracle."""
     W, H = 2048, 256
     want = coracle.run(coracle.fill_random(W, H, 0x5EED000C), 40)
     hs = []
     try:
         for r0, rows in ((0, 100), (100, 60), (160, 96)):
             h = golhip.Board(W, H, row0=r0, rows=rows)
-            h.set_option("wpl", 2)
+            h.set_option("wpl", wpl)
             h.fill_random(0x5EED000C)
             hs.append(h)
         golhip.group_step(hs, 40)
@@ -434,6 +440,44 @@ def test_rccl_halo_ring_one_rank(coracle, W, H, depth, persistent):
         b.step(1, want_flips=True)
         nxt = coracle.run(want, 1)
         assert np.array_equal(b.flips(), flips_np(want, nxt))
+
+
+@pytest.mark.parametrize("W,H,depth", [(2048, 1024, 16), (4096, 96, 8), (1024, 300, 4)])
+def test_rccl_halo_ring_quads(coracle, W, H, depth):
+    """The one-rank RCCL ring with four words per lane (interleaved quads,
+    launches of at most 8 turns, 16 launches per 128-row exchange)."""
+    board = coracle.fill_random(W, H, 0x5EED000F)
+    turns = 5 * depth + 5
+    want = coracle.run(board, turns)
+    with golhip.Board(W, H) as b:
+        b.comm_init(golhip.unique_id(), 1, 0)
+        b.set_option("force_halo", 1)
+        b.set_option("persistent", 0)
+        b.set_option("wpl", 4)
+        b.set_tb_depth(depth)
+        b.load_bytes(board)
+        b.step(turns)
+        assert b.perf()["halo_bytes"] > 0
+        assert np.array_equal(b.snapshot_bytes(), want)
+        assert b.alive_count() == (int((want == 255).sum()), turns)
+
+
+@pytest.mark.parametrize("W,H", [(131072, 2048), (262144, 1024)])
+def test_quads_auto_on_wide_boards(W, H):
+    """Boards 131072 and 262144 wide pick four words per lane by themselves
+    (per-launch path); digest and count equal two words per lane and the
+    one-turn launches."""
+    res = []
+    for wpl, depth in ((0, 16), (2, 16), (0, 1)):
+        with golhip.Board(W, H) as b:
+            b.set_option("persistent", 0)
+            b.set_option("wpl", wpl)
+            b.set_tb_depth(depth)
+            b.fill_random(0x5EED0003)
+            b.step(40)
+            res.append((b.board_hash(), b.alive_count(), b.perf()["step_launches"]))
+    assert res[0][:2] == res[1][:2] == res[2][:2]
+    assert res[0][2] == 5 and res[1][2] == 3  # 5 x 8 turns (quads) vs 16 + 12 + 12 (pairs)
 
 
 def test_rccl_halo_ring_full_size():
