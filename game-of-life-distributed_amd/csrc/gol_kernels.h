@@ -61,6 +61,7 @@ struct PersistArgs {
     uint32_t *buf0, *buf1;    // the two physical boards
     int first;                // buffer holding generation 0 (0 -> buf0)
     int J;                    // super-steps of `depth` turns
+    int half_last;            // 1: the last super-step runs depth / 2 turns
     int S;                    // rows per wavefront
     int S_old, S_young;       // > 0: unequal bands, first / second half of the band rows (wg_sy even)
     int paired;               // 1: waves w, w + NW/2 share two bands, met from both ends (wg_sy even)

@@ -657,9 +657,17 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
             // every claim of super-step j-1 is done (barrier above): re-arm its counter for j+1
             if (w < NW / 2 && lane == 0) s_claim[(j + 1) & 1][w] = rows_here;
         }
-        cnt = rows_here > 0 ? stream_band<D, true, WPL, GOL_PERSIST_STORE, false>(a, r0, rows_here, tile * tile_words(WPL), b * NW + w,
-                                                                            dir, claim)
-                            : 0u;
+        // half_last: a step of J D - D/2 turns ends with a D/2-turn super-step
+        // here instead of a separate per-launch kernel (16384^2: 110 us for 8
+        // turns as a K1 launch vs ~37 us at the resident rate)
+        if (rows_here <= 0)
+            cnt = 0u;
+        else if (D >= 2 && p.half_last && j == p.J - 1)
+            cnt = stream_band<(D >= 2 ? D / 2 : 1), true, WPL, GOL_PERSIST_STORE, false>(
+                a, r0, rows_here, tile * tile_words(WPL), b * NW + w, dir, claim);
+        else
+            cnt = stream_band<D, true, WPL, GOL_PERSIST_STORE, false>(a, r0, rows_here, tile * tile_words(WPL),
+                                                                       b * NW + w, dir, claim);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         {
             const long long tr_e = (long long)__builtin_amdgcn_s_memrealtime();

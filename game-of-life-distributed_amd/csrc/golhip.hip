@@ -99,6 +99,7 @@ struct golhip {
     int paired_bands = 1;       // option "paired_bands": SIMD mates share two bands from both ends (persistent)
     int dummy_rows = 0;         // option "dummy_rows": halo rows taking the kernels' dummy stores (0: all)
     int persist_wg_tx = 0;      // option "persist_wg_tx": tiles across a persistent workgroup (0: plan)
+    int persist_half = 1;       // option "persist_half": a D/2-turn remainder runs as the resident kernel's last super-step
     unsigned long long *d_trace = nullptr;  // option "trace": persistent-kernel diagnostics
     unsigned *d_sync = nullptr; // persistent kernel: [0] error, [1..] progress per workgroup
     unsigned *h_err = nullptr;  // pinned copy of the error word
@@ -579,7 +580,8 @@ int sync_stream(golhip_t h) {
 // One resident launch of J super-steps of `depth` turns over the rows of
 // `base` (count: the popcount of its last super-step goes to d_scalars);
 // returns false (with *rc == 0) when no workgroup plan fits.
-bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int wpl, bool count, int *rc) {
+bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int wpl, bool count, int *rc,
+                    bool half_last = false) {
     *rc = GOLHIP_OK;
     const int nw = persist_nw_for(h, depth, wpl);
     if (golk::persist_blocks_per_cu(depth, wpl, nw) < 1) return false;
@@ -621,6 +623,7 @@ bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int w
     p.buf1 = h->buf[1];
     p.first = h->cur;
     p.J = (int)J;
+    p.half_last = half_last ? 1 : 0;
     p.error = h->d_sync;
     p.progress = h->d_sync + 1;
     p.timeout_ticks = 100000000ll;  // 1 s at the 100 MHz s_memrealtime clock
@@ -644,8 +647,9 @@ bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int w
     }
     h->persist_pending = true;
     if (J & 1) h->cur ^= 1;
-    h->turns += J * depth;
-    h->persist_turns += J * depth;
+    const int64_t turns = J * depth - (half_last ? depth / 2 : 0);
+    h->turns += turns;
+    h->persist_turns += turns;
     h->persist_launches++;
     if (count) h->alive_turn = h->turns;
     return true;
@@ -663,11 +667,16 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     const int wpl = wpl_for(h);
     const int depth = persist_depth_for(h, wpl);
     if (depth < 4) return 0;
-    const int64_t J = left / depth;
+    int64_t J = left / depth;
     if (J < 2) return 0;
-    const bool count = count_last && J * depth == left;
-    if (!persist_launch(h, step_args(h, nullptr, false), J, depth, wpl, count, rc)) return 0;
-    return J * depth;
+    // a remainder of exactly depth / 2 turns (1000 = 62 x 16 + 8) becomes a
+    // last, half-depth super-step
+    const bool half = h->persist_half && left - J * depth == depth / 2;
+    if (half) ++J;
+    const int64_t turns = J * depth - (half ? depth / 2 : 0);
+    const bool count = count_last && turns == left;
+    if (!persist_launch(h, step_args(h, nullptr, false), J, depth, wpl, count, rc, half)) return 0;
+    return turns;
 }
 
 // Row strip between two deep-halo exchanges of k * d rows: the k launches of
@@ -890,6 +899,11 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "paired_bands %lld", (long long)value);
         h->paired_bands = (int)value;
         for (int &c : h->auto_rpw) c = 0;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "persist_half")) {
+        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "persist_half %lld", (long long)value);
+        h->persist_half = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "persist_wg_tx")) {

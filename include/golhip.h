@@ -102,12 +102,15 @@ int golhip_set_tb_depth(golhip_t h, int32_t turns);
 int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
 /* Named engine options (kernel variants for A/B measurement); results never
  * depend on them.  "fill_skip" (default 1): skip pipeline-fill stage-rows;
- * "wpl" (default 0 = auto): words per lane, 1 or 2 (2 runs on the
- * interleaved pair layout, converted at the I/O boundary); "persistent"
+ * "wpl" (default 0 = auto): words per lane, 1, 2 or 4 (2 and 4 run on the
+ * interleaved pair / quad layouts, converted at the I/O boundary; 4 fuses at
+ * most 8 turns a launch and needs width % 128 == 0); "persistent"
  * (default -1 = auto: on for buffers of at most 64 MiB; 1 on, 0 off):
  * resident multi-super-step kernel for long runs on a whole torus and,
  * in a ring, for the launches between two deep-halo exchanges;
  * "persist_depth" (default 0 = tb_depth): turns per super-step;
+ * "persist_half" (default 1): a remainder of half a super-step runs as the
+ * resident kernel's last, half-depth super-step;
  * "persist_waves" (0 = auto, 8 or 16): waves per persistent workgroup;
  * "paired_bands" (default 1): the two waves of a SIMD stream one two-band
  * region from both ends and meet where they meet; "age_split" (-1 = auto,

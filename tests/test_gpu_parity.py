@@ -480,6 +480,27 @@ def test_quads_auto_on_wide_boards(W, H):
     assert res[0][2] == 5 and res[1][2] == 3  # 5 x 8 turns (quads) vs 16 + 12 + 12 (pairs)
 
 
+@pytest.mark.parametrize("N,depth,wpl,half", [(2048, 16, 1, 1), (2048, 16, 1, 0), (4096, 8, 2, 1), (2048, 4, 1, 1)])
+def test_persistent_half_last_super_step(coracle, N, depth, wpl, half):
+    """J D + D/2 turns: one resident launch whose last super-step runs D/2
+    turns (persist_half), or a resident launch plus a per-launch kernel."""
+    board = coracle.fill_random(N, N, 0x5EED0010)
+    turns = 5 * depth + depth // 2
+    want = coracle.run(board, turns)
+    with golhip.Board(N, N) as b:
+        b.set_option("persistent", 1)
+        b.set_option("persist_half", half)
+        b.set_option("wpl", wpl)
+        b.set_tb_depth(depth)
+        b.load_bytes(board)
+        b.step(turns)
+        p = b.perf()
+        assert p["persist_launches"] == 1 and p["step_launches"] == (0 if half else 1)
+        assert p["persist_turns"] == (turns if half else 5 * depth)
+        assert np.array_equal(b.snapshot_bytes(), want)
+        assert b.alive_count() == (int((want == 255).sum()), turns)
+
+
 def test_rccl_halo_ring_full_size():
     """16384^2 through the one-rank RCCL ring (deep halos; resident and per-launch kernels) == the torus kernel."""
     res = []
