@@ -1055,7 +1055,15 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
         if (rc) return rc;
     }
     while (left > tail) {
-        const DepthRun run = depth_plan(depth_cap(h, halo), left - tail);
+        DepthRun run = depth_plan(depth_cap(h, halo), left - tail);
+        if (halo && persist_on(h)) {
+            // between exchanges the resident kernel runs full-depth super-steps
+            // cheaply and only a remainder goes to per-launch kernels, which
+            // are slow on strips this small: fewest short launches, greedily
+            // (1000 = 62 x 16 + 8, not 61 x 16 + 12 + 12)
+            const int d = largest_depth(std::min<int64_t>(depth_cap(h, halo), left - tail));
+            run = {d, (left - tail) / d};
+        }
         const int d = run.d;
         if (!halo) {
             if (int rc = launch_depth(h, d, left - d == 0, false)) return rc;
