@@ -702,8 +702,9 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
 }
 
 // ---- host-side dispatch over (depth, fill skip, words per lane) ----------
-// Depths 1, 2, 4, 8, 12, 16 (and 24, 32 for WPL = 1: depth 32 at WPL = 2 would
-// exceed 256 VGPRs); the host's depth_plan picks among them.
+// Depths 1, 2, 4, 6, 8, 12, 16 (and 24, 32 for WPL = 1: depth 32 at WPL = 2
+// would exceed 256 VGPRs; WPL = 4 stops at 8); the host's depth_plan picks
+// among them.
 template <typename F>
 static hipError_t dispatch(int depth, bool skip, int wpl, F &&f) {
 #define GOL_CASE(D, SK, WP) \
@@ -715,6 +716,8 @@ static hipError_t dispatch(int depth, bool skip, int wpl, F &&f) {
     GOL_CASE(12, true, 2) GOL_CASE(12, false, 2)
     GOL_CASE(1, true, 4) GOL_CASE(2, true, 4) GOL_CASE(4, true, 4) GOL_CASE(8, true, 4)
     GOL_CASE(1, false, 4) GOL_CASE(2, false, 4) GOL_CASE(4, false, 4) GOL_CASE(8, false, 4)
+    GOL_CASE(6, true, 1) GOL_CASE(6, false, 1) GOL_CASE(6, true, 2) GOL_CASE(6, false, 2)
+    GOL_CASE(6, true, 4) GOL_CASE(6, false, 4)
     GOL_CASE(1, true, 2) GOL_CASE(2, true, 2) GOL_CASE(4, true, 2) GOL_CASE(8, true, 2) GOL_CASE(16, true, 2)
     GOL_CASE(1, false, 2) GOL_CASE(2, false, 2) GOL_CASE(4, false, 2) GOL_CASE(8, false, 2) GOL_CASE(16, false, 2)
 #undef GOL_CASE
@@ -737,6 +740,7 @@ static hipError_t dispatch_pair(int depth, int wpl, F &&f) {
     GOL_QCASE(1, 1) GOL_QCASE(2, 1) GOL_QCASE(4, 1) GOL_QCASE(8, 1) GOL_QCASE(16, 1) GOL_QCASE(32, 1)
     GOL_QCASE(1, 2) GOL_QCASE(2, 2) GOL_QCASE(4, 2) GOL_QCASE(8, 2) GOL_QCASE(16, 2)
     GOL_QCASE(12, 1) GOL_QCASE(24, 1) GOL_QCASE(12, 2) GOL_QCASE(1, 4) GOL_QCASE(2, 4) GOL_QCASE(4, 4) GOL_QCASE(8, 4)
+    GOL_QCASE(6, 1) GOL_QCASE(6, 2) GOL_QCASE(6, 4)
 #undef GOL_QCASE
     return hipErrorInvalidValue;
 }

@@ -67,7 +67,7 @@ int fail(int code, const char *fmt, ...) {
 
 // Turns per launch with an instantiated step kernel (24: one word per lane
 // only, as 32; see max_depth_for).
-constexpr int kDepths[] = {32, 24, 16, 12, 8, 4, 2, 1};
+constexpr int kDepths[] = {32, 24, 16, 12, 8, 6, 4, 2, 1};
 constexpr int kNumDepths = sizeof(kDepths) / sizeof(kDepths[0]);
 // trace buffer: 8 totals + (start, end) per (workgroup < 1024, wave < 64)
 constexpr int64_t kTraceWords = 8 + 2 * 1024 * 64;

@@ -26,13 +26,19 @@ for size, kname in [(s, k) for s in (16384, 65536, 262144) for k in KERNELS]:
             durs.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
     if "FETCH_SIZE" not in vals or "WRITE_SIZE" not in vals:
         continue
+    tpl = 64 if kname == "gol_persist_kernel" else 16
+    for log in glob.glob(os.path.join(src, f"pmc_{size}_*.log")):  # prof_step.py's own line
+        for line in open(log):
+            if line.startswith('{"turns_per_launch"'):
+                tpl = json.loads(line)["turns_per_launch"]
     f = statistics.mean(vals["FETCH_SIZE"]) * 1024
     w = statistics.mean(vals["WRITE_SIZE"]) * 1024
     rec = {"fetch_size_bytes_raw": f, "fetch_bytes_corrected": 2 * f, "write_bytes": w,
            "hbm_bytes_per_launch": 2 * f + w, "board_bytes": size * size / 8, "launches": len(vals["FETCH_SIZE"]),
            "kernel": kname,
-           # prof_step.py: a persistent launch runs 4 super-steps of 16 turns, a per-launch one 16 turns
-           "turns_per_launch": 64 if kname == "gol_persist_kernel" else 16,
+           # prof_step.py: a persistent launch runs 4 super-steps, a per-launch one the
+           # board's launch depth (16, or 8 with four words per lane)
+           "turns_per_launch": tpl,
            "note": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes, scripts/prof_step.py; "
                    "Infinity-Cache hits are counted (a board <= 256 MiB is cache-resident)"}
     if "SQ_INSTS_VALU" in vals:

@@ -1,6 +1,7 @@
 """Fixed workload for rocprofv3 passes: fill a board, run warmup turns, then
 `--launches` fused step launches of `--depth` turns (automatic rows/wave)."""
 import argparse
+import json
 import os
 import sys
 
@@ -27,4 +28,6 @@ with golhip.Board(a.size, a.size, timing=True) as b:
         b.step(4 * a.depth if a.persistent else a.depth)
     b.sync()
     p = b.perf()
-    print(p)
+    n = p["persist_launches"] + p["step_launches"]
+    print(json.dumps({"turns_per_launch": (p["persist_turns"] + p["step_turns"]) / max(1, n), "launches": n,
+                      "words_per_lane": p["words_per_lane"], "tb_depth": p["tb_depth"]}), flush=True)

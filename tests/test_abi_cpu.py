@@ -66,7 +66,7 @@ def test_halo_plan_rejects_depth_above_strip():
 
 @pytest.mark.parametrize("rows,tb,left,want", [(16384, 16, 1000, (16, 8)), (16384, 16, 40, (16, 1)),
                                                (16384, 32, 1000, (32, 4)), (40, 16, 1000, (16, 2)),
-                                               (10, 16, 1000, (8, 1)), (16384, 16, 7, (4, 1)),
+                                               (10, 16, 1000, (8, 1)), (16384, 16, 7, (6, 1)),
                                                (16384, 1, 100, (1, 100)), (16384, 1, 1000, (1, 128)),
                                                (100, 16, 1000, (16, 6))])
 def test_halo_schedule(rows, tb, left, want):
@@ -81,7 +81,8 @@ def test_halo_schedule(rows, tb, left, want):
     (16384, 16, 40, [(16, 1), (12, 2)]),
     (16384, 32, 100, [(32, 2), (24, 1), (12, 1)]),
     (16384, 16, 20, [(12, 1), (8, 1)]),
-    (16384, 16, 7, [(4, 1), (2, 1), (1, 1)]),
+    (16384, 16, 7, [(6, 1), (1, 1)]),
+    (65536, 8, 100, [(8, 11), (6, 2)]),              # quads: no 4-turn tail
     (16384, 16, 36, [(12, 3)]),
 ])
 def test_halo_schedule_sequence(rows, tb, left, want):

@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 golhip = pytest.importorskip("golhip")
 
 CHECKS = [(16, 0), (16, 1), (16, 100), (64, 0), (64, 1), (64, 100), (512, 0), (512, 1), (512, 100)]
-DEPTHS = [1, 2, 4, 8, 12, 16, 24, 32]
+DEPTHS = [1, 2, 4, 6, 8, 12, 16, 24, 32]
 
 
 @pytest.fixture(scope="module")
