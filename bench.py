@@ -16,7 +16,9 @@ For N > 1 the 16384/65536 workloads are weak-scaled: the torus is N boards
 tall, rank r owns rows [r*S, (r+1)*S) and exchanges halo rows with its ring
 neighbours over RCCL every fused launch (the only collective on the path).
 
-Rank 0 prints ONE JSON line; `roofline` is measured on the step kernel with
+Warmup: W untimed steps, then more untimed steps until --warmup-seconds
+(default 0.5 s) have passed, so the timed steps do not see the clock ramp of
+an idle GPU.  Rank 0 prints ONE JSON line; `roofline` is measured on the step kernel with
 HIP events on the engine's stream; `cpu_baseline` times the oracle's port of
 the reference worker pool on a bounded sample (rank 0, N = 1 only), with the
 bit-packed OpenMP CPU comparator beside it (`cpu_baseline.fast_cpu`).
@@ -53,6 +55,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--warmup-seconds", type=float, default=0.5,
+                    help="keep warming up (untimed) until this much wall time has passed: a first run on an idle "
+                         "GPU is ~4 %% slower for its first second (clock ramp, first touch of the buffers)")
     ap.add_argument("--workload", type=int, default=16384, choices=sorted(WORKLOADS))
     ap.add_argument("--turns-per-step", type=int, default=None)
     ap.add_argument("--tb-depth", type=int, default=16)
@@ -174,7 +179,20 @@ def main():
         board.sync()
         torch.cuda.synchronize()
 
+    t_w = time.perf_counter()
     for _ in range(a.warmup):
+        board.step(turns_per_step)
+    board.sync()
+    # every rank runs the same number of extra warmup steps (decided by rank 0's clock)
+    extra = 0
+    if a.warmup > 0 and a.warmup_seconds > 0:
+        per = max(1e-6, (time.perf_counter() - t_w) / a.warmup)
+        extra = min(1000, int(max(0.0, a.warmup_seconds - (time.perf_counter() - t_w)) / per))
+        if dist is not None:
+            x = torch.tensor([extra], dtype=torch.int64, device="cuda")
+            dist.broadcast(x, src=0)
+            extra = int(x.item())
+    for _ in range(extra):
         board.step(turns_per_step)
     barrier()
     board.perf_reset()
@@ -224,6 +242,7 @@ def main():
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
+        "warmup_extra_steps": extra,
         "ms_per_step": round(dt / a.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": wl["scaling"],
