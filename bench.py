@@ -230,8 +230,14 @@ def main():
     try:
         with open(a.pmc) as f:
             rec = json.load(f).get(f"{N}:{kname}")
-        if rec:  # measured per profiled launch; scaled to this run's turns per launch
-            traffic = rec["hbm_bytes_per_launch"] / rec.get("turns_per_launch", kturns / launches) * (kturns / launches)
+        if rec:
+            # measured per profiled launch.  A per-launch kernel makes one pass over
+            # the board whatever its depth (read + write once), so its bytes carry
+            # over as they are; a resident launch makes one pass per super-step, so
+            # its bytes scale with this run's turns per launch.
+            traffic = rec["hbm_bytes_per_launch"]
+            if kname == "gol_persist_kernel":
+                traffic *= (kturns / launches) / rec.get("turns_per_launch", kturns / launches)
     except (OSError, ValueError):
         pass
 
@@ -273,8 +279,8 @@ def main():
             "note": "achieved = 0.25 B/cell-update (SURVEY 8d) x cell-updates per launch / avg launch time; "
                     "a launch fuses many turns, so frac > 1 means temporal blocking beat the single-pass "
                     "HBM roofline (the kernel is VALU-bound, see DESIGN.md 5); traffic = measured HBM bytes "
-                    "per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per turn, profiles/pmc_traffic.json, "
-                    "times this run's turns per launch)",
+                    "per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_traffic.json; one board pass "
+                    "for a per-launch kernel, scaled by super-steps for the resident kernel)",
         },
         "final_alive": alive,
         "final_turn": at_turn,
