@@ -96,13 +96,16 @@ hipError_t launch_hash(const uint32_t *words, int64_t nwords, int64_t word0, uns
 
 // Row-major compaction of set bits of (a ^ b) (b nullable -> a alone) into
 // (x, y) int32 pairs.  Three phases: per-block counts, one-block scan,
-// ordered scatter.  compact_blocks() = per-block slots needed.
+// ordered scatter.  compact_blocks() = per-block slots needed.  Batched
+// lists (golhip_step_flips): `base` (device, nullable) offsets the scan so
+// consecutive turns append, and the scatter drops pairs at index >= cap.
 int64_t compact_blocks(int64_t nwords);
 hipError_t launch_compact_count(const uint32_t *a, const uint32_t *b, int64_t nwords, unsigned long long *blk,
                                 hipStream_t s);
-hipError_t launch_compact_scan(unsigned long long *blk, int64_t nblk, unsigned long long *total, hipStream_t s);
+hipError_t launch_compact_scan(unsigned long long *blk, int64_t nblk, unsigned long long *total, hipStream_t s,
+                              const unsigned long long *base = nullptr);
 hipError_t launch_compact_scatter(const uint32_t *a, const uint32_t *b, int64_t nwords, int Ww,
                                   int64_t row0, const unsigned long long *blk_off, int32_t *xy, int il,
-                                  hipStream_t s);
+                                  hipStream_t s, unsigned long long cap = ~0ull);
 
 }  // namespace golk

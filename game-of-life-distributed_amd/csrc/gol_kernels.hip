@@ -1108,7 +1108,9 @@ __global__ __launch_bounds__(256) void compact_count_kernel(const uint32_t *__re
 }
 
 __global__ __launch_bounds__(1024) void compact_scan_kernel(unsigned long long *blk, int64_t nblk,
+                                                             const unsigned long long *base,
                                                              unsigned long long *total) {
+    const unsigned long long b0 = base ? *base : 0ull;  // batched lists: running offset
     __shared__ unsigned long long part[1024];
     const int64_t per = (nblk + 1023) / 1024;
     const int64_t beg = (int64_t)threadIdx.x * per;
@@ -1124,19 +1126,20 @@ __global__ __launch_bounds__(1024) void compact_scan_kernel(unsigned long long *
         part[threadIdx.x] += t;
         __syncthreads();
     }
-    unsigned long long run = part[threadIdx.x] - s;  // exclusive
+    unsigned long long run = part[threadIdx.x] - s + b0;  // exclusive
     for (int64_t i = beg; i < end; ++i) {
         const unsigned long long v = blk[i];
         blk[i] = run;
         run += v;
     }
-    if (threadIdx.x == 1023) *total = part[1023];
+    if (threadIdx.x == 1023) *total = part[1023] + b0;
 }
 
 __global__ __launch_bounds__(256) void compact_scatter_kernel(const uint32_t *__restrict__ a,
                                                                const uint32_t *__restrict__ b, int64_t n, int Ww,
                                                                int64_t row0, const unsigned long long *blk_off,
-                                                               int32_t *__restrict__ xy, int il) {
+                                                               int32_t *__restrict__ xy, unsigned long long cap,
+                                                               int il) {
     const int64_t base = (int64_t)blockIdx.x * kBlkWords + (int64_t)threadIdx.x * kWpt;
     uint32_t c = 0;
     for (int k = 0; k < kWpt; ++k)
@@ -1153,8 +1156,10 @@ __global__ __launch_bounds__(256) void compact_scatter_kernel(const uint32_t *__
         while (m) {
             const int bit = __builtin_ctz(m);
             m &= m - 1;
-            xy[2 * o] = wc * 32 + bit;
-            xy[2 * o + 1] = (int32_t)(row0 + row);
+            if (o < cap) {  // batched lists stop at the caller's capacity
+                xy[2 * o] = wc * 32 + bit;
+                xy[2 * o + 1] = (int32_t)(row0 + row);
+            }
             ++o;
         }
     }
@@ -1168,17 +1173,19 @@ hipError_t launch_compact_count(const uint32_t *a, const uint32_t *b, int64_t nw
     return hipGetLastError();
 }
 
-hipError_t launch_compact_scan(unsigned long long *blk, int64_t nblk, unsigned long long *total, hipStream_t s) {
-    hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, s, blk, nblk, total);
+hipError_t launch_compact_scan(unsigned long long *blk, int64_t nblk, unsigned long long *total, hipStream_t s,
+                              const unsigned long long *base) {
+    hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, s, blk, nblk, base, total);
     return hipGetLastError();
 }
 
 hipError_t launch_compact_scatter(const uint32_t *a, const uint32_t *b, int64_t nwords, int Ww, int64_t row0,
-                                  const unsigned long long *blk_off, int32_t *xy, int il, hipStream_t s) {
+                                  const unsigned long long *blk_off, int32_t *xy, int il, hipStream_t s,
+                                  unsigned long long cap) {
     const int64_t nb = compact_blocks(nwords);
     if (nb == 0) return hipSuccess;
     hipLaunchKernelGGL(compact_scatter_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, b, nwords, Ww, row0, blk_off,
-                       xy, il);
+                       xy, cap, il);
     return hipGetLastError();
 }
 

@@ -118,6 +118,8 @@ struct golhip {
     int64_t blk_cap = 0;
     int32_t *d_xy = nullptr;
     int64_t xy_cap = 0;
+    unsigned long long *d_run = nullptr;  // golhip_step_flips: running list offsets
+    int64_t run_cap = 0;
     uint8_t *d_stage = nullptr;  // byte staging for load/snapshot
     int64_t stage_cap = 0;
     bool flips_valid = false;
@@ -820,6 +822,7 @@ int golhip_destroy(golhip_t h) {
     if (h->h_scalars) HIP_RC(hipHostFree(h->h_scalars));
     HIP_RC(hipFree(h->d_blk));
     HIP_RC(hipFree(h->d_xy));
+    HIP_RC(hipFree(h->d_run));
     HIP_RC(hipFree(h->d_stage));
     HIP_RC(hipFree(h->d_sync));
     HIP_RC(hipFree(h->d_trace));
@@ -1234,6 +1237,65 @@ int golhip_flips(golhip_t h, int32_t *xy, uint64_t cap, uint64_t *n) {
         return fail(GOLHIP_EINVAL, "no flip list: step with want_flips first");
     }
     return finish_compact(h, h->cur_rows(), h->prev_rows(), xy, cap, n);
+}
+
+// nturns single turns, each followed by its flip compaction appended on the
+// device (the scan starts at the running offset d_run[t], writes d_run[t+1]),
+// then ONE copy of all lists and their counts: the per-turn CellFlipped
+// stream of distributor.go:93-173 + :212-220 without a host round trip per
+// turn.  The board always advances nturns; past cap the lists are cut short
+// and ERANGE reports the total needed in *n.
+int golhip_step_flips(golhip_t h, int64_t nturns, int32_t *xy, uint64_t cap, uint64_t *counts, uint64_t *n) {
+    if (int rc = check(h)) return rc;
+    if (n) *n = 0;
+    if (nturns < 0) return fail(GOLHIP_EINVAL, "nturns %lld", (long long)nturns);
+    if (nturns > 0 && !counts) return fail(GOLHIP_EINVAL, "counts is null");
+    if (cap > 0 && !xy) return fail(GOLHIP_EINVAL, "xy is null");
+    std::lock_guard<std::mutex> g(h->mu);
+    if (!h->loaded) return fail(GOLHIP_EINVAL, "no board loaded");
+    if (h->nranks == 1 && !h->torus()) return fail(GOLHIP_EINVAL, "strip handle needs golhip_comm_init or golhip_group_step");
+    if (int rc = set_dev(h)) return rc;
+    if (int rc = set_layout(h, want_il(h))) return rc;
+    h->flips_valid = false;
+    if (nturns == 0) return GOLHIP_OK;
+    const bool halo = h->comm && (h->nranks > 1 || h->force_halo);
+    const int64_t nw = h->local_words();
+    const int64_t nb = golk::compact_blocks(nw);
+    if (int rc = ensure_blk(h, nb)) return rc;
+    if (int rc = ensure_xy(h, (int64_t)std::min<uint64_t>(cap, (uint64_t)INT64_MAX / 16))) return rc;
+    if (h->run_cap < nturns + 1) {
+        if (h->d_run) HIP_OR_FAIL(hipFree(h->d_run));
+        h->d_run = nullptr;
+        h->run_cap = 0;
+        HIP_OR_FAIL(hipMalloc(&h->d_run, (size_t)(nturns + 1) * sizeof(unsigned long long)));
+        h->run_cap = nturns + 1;
+    }
+    HIP_OR_FAIL(hipMemsetAsync(h->d_run, 0, sizeof(unsigned long long), h->stream));
+    for (int64_t t = 0; t < nturns; ++t) {
+        if (halo)
+            if (int rc = exchange_rccl(h, 1, h->stream)) return rc;
+        if (int rc = launch_depth(h, 1, t == nturns - 1, halo)) return rc;
+        HIP_OR_FAIL(golk::launch_compact_count(h->cur_rows(), h->prev_rows(), nw, h->d_blk, h->stream));
+        HIP_OR_FAIL(golk::launch_compact_scan(h->d_blk, nb, h->d_run + t + 1, h->stream, h->d_run + t));
+        HIP_OR_FAIL(golk::launch_compact_scatter(h->cur_rows(), h->prev_rows(), nw, h->Ww, h->row0, h->d_blk, h->d_xy,
+                                                 h->il, h->stream, (unsigned long long)cap));
+    }
+    std::vector<unsigned long long> run((size_t)nturns + 1);
+    HIP_OR_FAIL(hipMemcpyAsync(run.data(), h->d_run, run.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                               h->stream));
+    if (int rc_ = sync_stream(h)) return rc_;
+    for (int64_t t = 0; t < nturns; ++t) counts[t] = run[t + 1] - run[t];
+    const uint64_t total = run[nturns];
+    if (n) *n = total;
+    const uint64_t got = std::min<uint64_t>(total, cap);
+    if (got > 0) {
+        HIP_OR_FAIL(hipMemcpyAsync(xy, h->d_xy, got * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, h->stream));
+        if (int rc_ = sync_stream(h)) return rc_;
+    }
+    if (total > cap)
+        return fail(GOLHIP_ERANGE, "buffer holds %llu cells, %llu needed", (unsigned long long)cap,
+                    (unsigned long long)total);
+    return GOLHIP_OK;
 }
 
 int golhip_alive_cells(golhip_t h, int32_t *xy, uint64_t cap, uint64_t *n) {

@@ -108,6 +108,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "golhip_alive_count": ([H, P(u64), P(i64)], ctypes.c_int),
         "golhip_alive_count_global": ([H, P(u64), P(i64)], ctypes.c_int),
         "golhip_flips": ([H, ctypes.c_void_p, u64, P(u64)], ctypes.c_int),
+        "golhip_step_flips": ([H, i64, ctypes.c_void_p, u64, ctypes.c_void_p, P(u64)], ctypes.c_int),
         "golhip_alive_cells": ([H, ctypes.c_void_p, u64, P(u64)], ctypes.c_int),
         "golhip_snapshot_bytes": ([H, ctypes.c_void_p], ctypes.c_int),
         "golhip_snapshot_bits": ([H, ctypes.c_void_p], ctypes.c_int),
@@ -262,6 +263,21 @@ class Board:
     def flips(self) -> np.ndarray:
         """(x=col, y=row) pairs, row-major, of cells changed by the last turn."""
         return self._cells(load().golhip_flips)
+
+    def step_flips(self, nturns: int, cap: int, xy: np.ndarray | None = None):
+        """Advance nturns turns and return (xy, counts): every turn's flip
+        list concatenated in turn order (golhip_step_flips).  Raises
+        GolHipError (ERANGE) when the lists exceed cap pairs; the board has
+        advanced nturns either way.  A preallocated (>= cap, 2) int32 `xy`
+        is filled in place."""
+        if xy is None:
+            xy = np.empty((max(cap, 1), 2), dtype=np.int32)
+        if xy.shape[0] < cap or xy.dtype != np.int32 or not xy.flags.c_contiguous:
+            raise ValueError("xy must be a C-contiguous int32 array of >= cap rows")
+        counts = np.zeros(max(nturns, 1), dtype=np.uint64)
+        n = ctypes.c_uint64()
+        _check(load().golhip_step_flips(self._h, nturns, _ptr(xy), cap, _ptr(counts), ctypes.byref(n)))
+        return xy[: n.value], counts[:nturns]
 
     def alive_cells(self) -> np.ndarray:
         return self._cells(load().golhip_alive_cells)

@@ -176,6 +176,15 @@ int golhip_alive_count_global(golhip_t h, uint64_t *count, int64_t *at_turn);
 /* Cells that changed in the last stepped turn (want_flips), row-major,
  * (x = col, y = row) pairs in global coordinates.  ERANGE sets *n. */
 int golhip_flips(golhip_t h, int32_t *xy, uint64_t cap, uint64_t *n);
+/* Batched CellFlipped stream (distributor.go:93-173 with the per-turn
+ * initializeAliveCells :212-220): advance nturns turns one at a time and
+ * return every turn's flip list, concatenated in turn order (row-major within
+ * a turn, same pairs as golhip_flips), with counts[t] = flips of turn t.
+ * One host round trip for the whole batch.  The board always advances
+ * nturns; if the lists exceed cap pairs, xy holds the first cap, *n the
+ * total and the call returns GOLHIP_ERANGE.  Reserves cap pairs on the
+ * device. */
+int golhip_step_flips(golhip_t h, int64_t nturns, int32_t *xy, uint64_t cap, uint64_t *counts, uint64_t *n);
 /* Alive cells, row-major (x = col, y = row) pairs — calculateAliveCells. */
 int golhip_alive_cells(golhip_t h, int32_t *xy, uint64_t cap, uint64_t *n);
 /* Board as 0/255 bytes / bit words (this handle's rows). */

@@ -5,11 +5,15 @@ Prints one JSON object with:
   events_on       one turn per step + the turn's CellFlipped list copied to the
                   host (golhip_flips, row-major) + AliveCellsCount every 2 s:
                   turns/s, flips/s, GCUPS
+  events_batched  golhip_step_flips: batches of BATCH turns, every turn's
+                  CellFlipped list copied to the host in one transfer per
+                  batch (same flips as events_on): turns/s, flips/s, GCUPS
   snapshot_s      one 's' snapshot (golhip_snapshot_bytes + PGM write), ms
 The synthetic board is the counter-hash generator with seed 0x5EED0005.
 """
 import json
 import os
+import numpy as np
 import sys
 import tempfile
 import time
@@ -47,6 +51,24 @@ with golhip.Board(N, N, timing=True) as b:
     dt = time.perf_counter() - t0
     out["events_on"] = {"turns": turns, "seconds": dt, "turns_per_s": turns / dt, "flips": flips_total,
                         "flips_per_s": flips_total / dt, "gcups": N * N * turns / dt / 1e9, "ticks": ticks}
+
+    # same 200 turns again from the same board state, batched
+    b.fill_random(SEED)
+    b.step(64)
+    b.step(2000)
+    b.sync()
+    BATCH = 50
+    xy = np.empty((BATCH * 1_500_000, 2), dtype=np.int32)
+    xy.fill(0)  # touch the pages outside the timed region
+    flips_b = 0
+    t0 = time.perf_counter()
+    for _ in range(turns // BATCH):
+        got, counts = b.step_flips(BATCH, cap=xy.shape[0], xy=xy)
+        flips_b += len(got)
+    dt = time.perf_counter() - t0
+    out["events_batched"] = {"turns": turns, "batch": BATCH, "seconds": dt, "turns_per_s": turns / dt,
+                             "flips": flips_b, "flips_per_s": flips_b / dt, "gcups": N * N * turns / dt / 1e9,
+                             "same_flips_as_events_on": flips_b == flips_total}
 
     t0 = time.perf_counter()
     snap = b.snapshot_bytes()

@@ -155,6 +155,62 @@ def test_flips_after_multi_turn_step(fixtures):
         assert np.array_equal(b.flips(), flips_np(a, step_np(a)))
 
 
+@pytest.mark.parametrize("n,batches", [(512, [1, 7, 32, 60]), (256, [20, 1, 13]), (64, [64, 64]), (48, [9, 4])])
+def test_step_flips_batched_stream(fixtures, n, batches):
+    """golhip_step_flips: every turn's list of a batch, concatenated, equals the
+    oracle's per-turn diffs; the shadow board replays the alive-count CSV
+    (sdl_test.go:107-116) where the reference ships one.  48 x 48 takes the
+    generic-width kernel."""
+    if n == 48:
+        rng = np.random.default_rng(48)
+        board = np.where(rng.random((n, n)) < 0.35, 255, 0).astype(np.uint8)
+    else:
+        board = img(fixtures, n)
+    exp = fixtures.get(f"alive_{n}")
+    shadow = board.copy()
+    t = 0
+    with golhip.Board(n, n) as b:
+        b.load_bytes(board)
+        for k in batches:
+            xy, counts = b.step_flips(k, cap=k * n * n)
+            assert len(counts) == k and int(counts.sum()) == len(xy)
+            off = 0
+            for c in counts:
+                nxt = step_np(board)
+                assert np.array_equal(xy[off:off + int(c)], flips_np(board, nxt))
+                shadow[xy[off:off + int(c), 1], xy[off:off + int(c), 0]] ^= 0xFF
+                board, off, t = nxt, off + int(c), t + 1
+                if exp is not None and t < len(exp):
+                    assert int((shadow == 255).sum()) == exp[t]
+            assert b.alive_count() == (int((board == 255).sum()), t)
+        assert np.array_equal(b.snapshot_bytes(), board)
+        assert np.array_equal(shadow, board)
+
+
+def test_step_flips_capacity_and_edges(fixtures):
+    """cap too small: ERANGE with the total, the first cap pairs kept, the board
+    still advanced; zero turns; a still board gives empty lists."""
+    board = img(fixtures, 256)
+    with golhip.Board(256, 256) as b:
+        b.load_bytes(board)
+        xy_all = [flips_np(run_np(board, i), run_np(board, i + 1)) for i in range(5)]
+        want = np.concatenate(xy_all)
+        buf = np.zeros((100, 2), dtype=np.int32)
+        with pytest.raises(golhip.GolHipError) as e:
+            b.step_flips(5, cap=100, xy=buf)
+        assert e.value.code == golhip.GOLHIP_ERANGE
+        assert np.array_equal(buf, want[:100])
+        assert np.array_equal(b.snapshot_bytes(), run_np(board, 5))
+        xy, counts = b.step_flips(0, cap=0)
+        assert len(xy) == 0 and len(counts) == 0
+        assert b.alive_count()[1] == 5
+    z = np.zeros((64, 64), dtype=np.uint8)
+    with golhip.Board(64, 64) as b:
+        b.load_bytes(z)
+        xy, counts = b.step_flips(10, cap=16)
+        assert len(xy) == 0 and list(counts) == [0] * 10
+
+
 # ---------------------------------------------------------------- kernel geometry sweeps
 @pytest.mark.parametrize("depth", DEPTHS)
 @pytest.mark.parametrize("rpw", [0, 1, 2, 5, 37, 512])
