@@ -1057,7 +1057,10 @@ hipError_t launch_hash(const uint32_t *words, int64_t nwords, int64_t word0, uns
 // count pass, a single-block exclusive scan of block counts, and a scatter
 // pass that re-scans inside the block keep the output strictly row-major.
 // ---------------------------------------------------------------------------
-constexpr int kWpt = 16;
+#ifndef GOL_COMPACT_WPT
+#define GOL_COMPACT_WPT 4  // words per thread (A/B builds override)
+#endif
+constexpr int kWpt = GOL_COMPACT_WPT;
 constexpr int kBlkWords = 256 * kWpt;
 
 int64_t compact_blocks(int64_t nwords) { return (nwords + kBlkWords - 1) / kBlkWords; }
