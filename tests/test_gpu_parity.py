@@ -498,6 +498,24 @@ def test_rccl_halo_ring_one_rank(coracle, W, H, depth, persistent):
         assert np.array_equal(b.flips(), flips_np(want, nxt))
 
 
+@pytest.mark.parametrize("W,H", [(512, 512), (1024, 300), (100, 64)])
+def test_rccl_halo_ring_step_flips(coracle, W, H):
+    """golhip_step_flips through the halo path (one RCCL exchange per turn)."""
+    board = coracle.fill_random(W, H, 0x5EED0010)
+    with golhip.Board(W, H) as b:
+        b.comm_init(golhip.unique_id(), 1, 0)
+        b.set_option("force_halo", 1)
+        b.load_bytes(board)
+        xy, counts = b.step_flips(9, cap=9 * W * H)
+        off = 0
+        for c in counts:
+            nxt = coracle.run(board, 1)
+            assert np.array_equal(xy[off:off + int(c)], flips_np(board, nxt))
+            board, off = nxt, off + int(c)
+        assert np.array_equal(b.snapshot_bytes(), board)
+        assert b.alive_count() == (int((board == 255).sum()), 9)
+
+
 @pytest.mark.parametrize("W,H,depth", [(2048, 1024, 16), (4096, 96, 8), (1024, 300, 4)])
 def test_rccl_halo_ring_quads(coracle, W, H, depth):
     """The one-rank RCCL ring with four words per lane (interleaved quads,
