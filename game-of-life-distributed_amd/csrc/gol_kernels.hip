@@ -531,7 +531,7 @@ __global__ __launch_bounds__(256) void gol_tb_kernel(StepArgs a) {
 // shared LDS counter until they meet, so the SIMD arbiter's oldest-first
 // service no longer leaves the younger wave running alone at the end of the
 // launch.
-template <int D, int WPL>
+template <int D, int WPL, bool CNT>
 __global__ __launch_bounds__(512) void gol_tb_pair_kernel(StepArgs a) {
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -543,14 +543,36 @@ __global__ __launch_bounds__(512) void gol_tb_pair_kernel(StepArgs a) {
     const int r0 = region * 2 * S;
     const int len = r0 < a.rows_out ? min(2 * S, a.rows_out - r0) : 0;
     __shared__ int s_claim[4];
+    __shared__ unsigned long long s_cnt;  // (waves arrived << 40) | cells, for the fused count
     if (w < 4 && lane == 0) s_claim[w] = len;
+    if (CNT && threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
     if (len == 0) return;  // wave-uniform, after the only barrier
     const uint32_t cnt = stream_band<D, true, WPL, GOL_PAIR_STORE, true>(a, r0, len, tile * tile_words(WPL), blockIdx.x * 8 + w,
                                                    w < 4 ? 1 : -1, &s_claim[w & 3]);
-    if (a.alive) {
+    if constexpr (!CNT) {
+        if (a.alive) {
+            const uint32_t tot = wave_sum_u32(cnt);
+            if (lane == 0 && tot) atomicAdd(a.alive, (unsigned long long)tot);
+        }
+    } else if (a.alive) {
+        // The counting instance (last launch of a step): one device atomic per
+        // workgroup, by the last wave to arrive.  Device atomics on one address
+        // serialise (~20 ns each); per wave they cost a 1-turn launch at 5120^2
+        // (3 840 waves finishing together) 78 us on 10 us.  A separate
+        // instance because the extra code slowed the count-free launches.
         const uint32_t tot = wave_sum_u32(cnt);
-        if (lane == 0 && tot) atomicAdd(a.alive, (unsigned long long)tot);
+        int active = 0;
+        for (int i = 0; i < 4; ++i) {
+            const int qi = blockIdx.x * 4 + i;
+            active += (qi / tiles_x) * 2 * S < a.rows_out ? 2 : 0;
+        }
+        if (lane == 0) {
+            const unsigned long long mine = (1ull << 40) | tot;
+            const unsigned long long now = atomicAdd(&s_cnt, mine) + mine;
+            const unsigned long long sum = now & ((1ull << 40) - 1);
+            if ((int)(now >> 40) == active && sum) atomicAdd(a.alive, sum);
+        }
     }
 }
 
@@ -734,9 +756,9 @@ int tb_waves(const StepArgs &a, int wpl) {
 }
 
 template <typename F>
-static hipError_t dispatch_pair(int depth, int wpl, F &&f) {
+static hipError_t dispatch_pair(int depth, int wpl, F &&f, bool cnt = false) {
 #define GOL_QCASE(D, WP) \
-    if (depth == D && wpl == WP) return f(gol_tb_pair_kernel<D, WP>);
+    if (depth == D && wpl == WP) return cnt ? f(gol_tb_pair_kernel<D, WP, true>) : f(gol_tb_pair_kernel<D, WP, false>);
     GOL_QCASE(1, 1) GOL_QCASE(2, 1) GOL_QCASE(4, 1) GOL_QCASE(8, 1) GOL_QCASE(16, 1) GOL_QCASE(32, 1)
     GOL_QCASE(1, 2) GOL_QCASE(2, 2) GOL_QCASE(4, 2) GOL_QCASE(8, 2) GOL_QCASE(16, 2)
     GOL_QCASE(12, 1) GOL_QCASE(24, 1) GOL_QCASE(12, 2) GOL_QCASE(1, 4) GOL_QCASE(2, 4) GOL_QCASE(4, 4) GOL_QCASE(8, 4)
@@ -753,10 +775,13 @@ int tb_pair_blocks(const StepArgs &a, int wpl) {
 hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s, bool fill_skip, int wpl, bool paired) {
     if (paired && fill_skip) {
         const dim3 grid(tb_pair_blocks(a, wpl)), block(512);
-        return dispatch_pair(depth, wpl, [&](auto kern) {
-            hipLaunchKernelGGL(kern, grid, block, 0, s, a);
-            return hipGetLastError();
-        });
+        return dispatch_pair(
+            depth, wpl,
+            [&](auto kern) {
+                hipLaunchKernelGGL(kern, grid, block, 0, s, a);
+                return hipGetLastError();
+            },
+            a.alive != nullptr);
     }
     const int waves = tb_waves(a, wpl);
     const dim3 grid((waves + 3) / 4), block(256);
