@@ -594,6 +594,9 @@ __global__ __launch_bounds__(512) void gol_tb_pair_kernel(StepArgs a) {
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr int persist_waves(int depth, int wpl) { return depth * wpl <= 16 ? 16 : 8; }
 
+#ifndef GOL_PERSIST_WG_COUNT
+#define GOL_PERSIST_WG_COUNT 1  // per-workgroup count atomic in K1p (0 = per wave, A/B builds)
+#endif
 template <int D, int WPL, int NW>
 __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
     const int lane = threadIdx.x & 63;
@@ -636,6 +639,10 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
     }
     __shared__ int s_abort;
     __shared__ int s_claim[2][NW / 2];  // per pair, double-buffered over super-steps
+#if GOL_PERSIST_WG_COUNT
+    __shared__ unsigned long long s_cnt;  // (waves arrived << 40) | cells, for the fused count
+    if (threadIdx.x == 0) s_cnt = 0;
+#endif
     if (threadIdx.x == 0) s_abort = 0;
     if (paired && w < NW / 2 && lane == 0) s_claim[0][w] = rows_here;
     __syncthreads();
@@ -719,7 +726,17 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
     }
     if (p.base.alive) {
         const uint32_t tot = wave_sum_u32(cnt);
+#if GOL_PERSIST_WG_COUNT
+        // one device atomic per workgroup (see gol_tb_pair_kernel<D, WPL, true>)
+        if (lane == 0) {
+            const unsigned long long mine = (1ull << 40) | tot;
+            const unsigned long long now = atomicAdd(&s_cnt, mine) + mine;
+            const unsigned long long sum = now & ((1ull << 40) - 1);
+            if ((int)(now >> 40) == NW && sum) atomicAdd(p.base.alive, sum);
+        }
+#else
         if (lane == 0 && tot) atomicAdd(p.base.alive, (unsigned long long)tot);
+#endif
     }
 }
 
