@@ -1,27 +1,33 @@
 """bench.py — cell-updates/s of the MI355X Game of Life engine (libgolhip.so).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload 16384|65536|262144]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload 65536|16384|262144]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-A "step" is one pass of the hot path over the whole board: `--turns-per-step`
-B3/S23 turns (default 1000) of the synthetic torus, run as fused launches of
-`--tb-depth` turns.  Timed region: exactly K steps, bracketed by a barrier and
+A "step" is one run of the workload's BASELINE config over the whole board:
+its turns (configs[2]: 1,000) of the synthetic torus, run as fused launches.
+Timed region: exactly K steps, bracketed by a barrier and
 torch.cuda.synchronize() on both sides, max over ranks.
 
-Workloads (BASELINE.json configs; synthetic boards, data="synthetic"):
-  16384  (default, configs[1]) 16384 x 16384 per GPU, seed 0x5EED0001, 10 steps = 10k turns
-  65536  (configs[2])          65536 x 65536 per GPU, seed 0x5EED0002
-  262144 (configs[3])          262144 x 262144 total, strong-scaled over N GPUs, seed 0x5EED0003
-For N > 1 the 16384/65536 workloads are weak-scaled: the torus is N boards
-tall, rank r owns rows [r*S, (r+1)*S) and exchanges halo rows with its ring
-neighbours over RCCL every fused launch (the only collective on the path).
+Workloads (BASELINE.json configs; synthetic boards, data="synthetic"), all
+strong-scaled: ONE board of the config, rank r of N owns rows
+[r*N_rows/N, (r+1)*N_rows/N) and exchanges halo rows with its ring neighbours
+over RCCL (the only collective on the path):
+  65536  (default, configs[2]) 65536^2,  seed 0x5EED0002, 1,000 turns a step
+  16384  (configs[1])          16384^2,  seed 0x5EED0001, 10,000 turns a step
+  262144 (configs[3])          262144^2, seed 0x5EED0003, 100 turns a step
 
-Warmup: W untimed steps, then more untimed steps until --warmup-seconds
-(default 0.5 s) have passed, so the timed steps do not see the clock ramp of
-an idle GPU.  Rank 0 prints ONE JSON line; `roofline` is measured on the step kernel with
-HIP events on the engine's stream; `cpu_baseline` times the oracle's port of
-the reference worker pool on a bounded sample (rank 0, N = 1 only), with the
-bit-packed OpenMP CPU comparator beside it (`cpu_baseline.fast_cpu`).
+Parity: the first untimed step starts from the freshly filled board, so after
+it the board is at exactly the config's turns; its digest (golhip_board_hash,
+summed over ranks) and alive count must equal tests/golden/fullsize.json (the
+oracle's answer, tests/golden/make_fullsize.py).  The JSON line carries
+"parity": true/false and the run exits 1 after printing on a mismatch.
+
+Warmup: W untimed steps (at least 1, the parity step), then more untimed steps
+until --warmup-seconds have passed.  Rank 0 prints ONE JSON line; `roofline`
+is measured live on the step kernels with HIP events on the engine's stream
+(see roofline_block); `cpu_baseline` times the oracle's port of the reference
+worker pool on a bounded sample (rank 0, N = 1 only), with the bit-packed
+OpenMP CPU comparator beside it (`cpu_baseline.fast_cpu`).
 """
 from __future__ import annotations
 
@@ -41,13 +47,19 @@ for _p in (ROOT, os.path.join(ROOT, "game-of-life-distributed_amd")):
 import golhip  # noqa: E402
 
 METRIC = "cell-updates/sec (GCUPS) at 1/2/4/8 MI355X; % of HBM roofline"
-HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
-ALG_BYTES_PER_UPDATE = 0.25  # 1 bit read + 1 bit written per cell-update
+HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md: 8.0 TB/s spec
+ALG_BYTES_PER_UPDATE = 0.25   # 1 bit read + 1 bit written per cell-update
+# VALU issue peak (MI355X_MICROARCH.md, chip table + "Wave scheduling"): 256 CUs x
+# 4 SIMD-32 x one wave64 VALU instruction per 2 cycles x 2.4 GHz max clock.
+# A "slot" is one full-rate wave64 instruction; DPP moves and v_alignbit_b32
+# issue at half rate on gfx950 (scripts/ubench) and cost 2.
+VALU_PEAK_GSLOTS = 256 * 4 * 0.5 * 2.4
 WORKLOADS = {
-    16384: dict(seed=0x5EED0001, scaling="weak", desc="configs[1]: 16384^2 random 25% per GPU"),
-    65536: dict(seed=0x5EED0002, scaling="weak", desc="configs[2]: 65536^2 random 25% per GPU"),
-    262144: dict(seed=0x5EED0003, scaling="strong", desc="configs[3]: 262144^2 random 25%, strong-scaled"),
+    65536: dict(key="c2", seed=0x5EED0002, turns=1000, desc="configs[2]: 65536^2 random 25%, 1000 turns a step"),
+    16384: dict(key="c1", seed=0x5EED0001, turns=10000, desc="configs[1]: 16384^2 random 25%, 10000 turns a step"),
+    262144: dict(key="c3", seed=0x5EED0003, turns=100, desc="configs[3]: 262144^2 random 25%, 100 turns a step"),
 }
+FULLSIZE = os.path.join(ROOT, "tests", "golden", "fullsize.json")
 
 
 def parse():
@@ -58,14 +70,16 @@ def parse():
     ap.add_argument("--warmup-seconds", type=float, default=0.5,
                     help="keep warming up (untimed) until this much wall time has passed: a first run on an idle "
                          "GPU is ~4 %% slower for its first second (clock ramp, first touch of the buffers)")
-    ap.add_argument("--workload", type=int, default=16384, choices=sorted(WORKLOADS))
-    ap.add_argument("--turns-per-step", type=int, default=None)
+    ap.add_argument("--workload", type=int, default=65536, choices=sorted(WORKLOADS))
+    ap.add_argument("--turns-per-step", type=int, default=None,
+                    help="default: the config's turns (parity is only checked then)")
     ap.add_argument("--tb-depth", type=int, default=16)
     ap.add_argument("--rows-per-wave", type=int, default=0, help="0 = automatic")
+    ap.add_argument("--option", action="append", default=[], help="engine option key=value (A/B runs)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
-                    help="measured HBM traffic per launch (from rocprofv3 --pmc), keyed by workload")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_bench.json"),
+                    help="rocprofv3 --pmc summary of this bench command (scripts/pmc_bench.py)")
     return ap.parse_args()
 
 
@@ -87,19 +101,17 @@ def cpu_threads() -> int:
     return max(1, min(16, os.cpu_count() or 1))
 
 
-def cpu_baseline(W: int, target_s: float) -> dict:
+def cpu_baseline(W: int, seed: int, target_s: float) -> dict:
     """Oracle port of the reference worker pool (distributor.go:116-173) on a
-    bounded sample of the same synthetic board: a 4096-row band of the board,
+    bounded sample of the same synthetic board: a band of up to 4096 rows,
     as many turns as fit in ~target_s.  Beside it (`fast_cpu`), the bit-packed
-    OpenMP comparator (oracle/gol_fastcpu.c) on the whole board, ~target_s / 2."""
+    OpenMP comparator (oracle/gol_fastcpu.c) on up to 16384 rows, ~target_s / 2."""
     from oracle.oracle import COracle
 
     o = COracle()
-    seed = WORKLOADS.get(W, WORKLOADS[16384])["seed"]
     rows = min(4096, W)
     board = o.fill_random(W, rows, seed)
-    threads = cpu_threads() - 1  # Threads; the pool runs Threads+1 workers
-    threads = max(1, threads)
+    threads = max(1, cpu_threads() - 1)  # Threads; the pool runs Threads+1 workers
     t0 = time.perf_counter()
     o.run_workerpool(board, 1, threads)
     one = time.perf_counter() - t0
@@ -116,14 +128,12 @@ def cpu_baseline(W: int, target_s: float) -> dict:
                   f"worker-pool port (Threads={threads}, Threads+1 workers), {dt:.1f} s",
         "host": host_info(),
     }
-    # fast comparator: whole board if it fits in a few GB of host memory, else a band
-    fast_rows = W if W <= 65536 else 16384
-    words = o.pack64(o.fill_random(W, fast_rows, seed)) if W <= 16384 else \
-        np.ascontiguousarray(np.random.default_rng(seed).integers(0, 2**64, (fast_rows, W // 64), dtype=np.uint64))
     nth = cpu_threads()
+    fast_rows = min(W, 16384)
+    words = o.fill_random64(W, fast_rows, seed, nth)
     t0 = time.perf_counter()
-    o.run_fast_words(words, W, 4, nth)
-    one = (time.perf_counter() - t0) / 4
+    o.run_fast_words(words, W, 2, nth)
+    one = (time.perf_counter() - t0) / 2
     fturns = max(1, int(target_s / 2 / max(one, 1e-6)))
     t0 = time.perf_counter()
     o.run_fast_words(words, W, fturns, nth)
@@ -139,6 +149,72 @@ def cpu_baseline(W: int, target_s: float) -> dict:
     return out
 
 
+def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str) -> dict:
+    """Roofline of the dominant step kernel, from HIP events around every launch
+    on the engine stream (GOLHIP_FLAG_TIMING; launch-averaged).
+
+    The kernels are VALU-issue-bound: a launch fuses 8-16
+    turns per board pass, so HBM moves ~1/D of the single-pass bytes.  `frac`
+    is therefore the VALU issue fraction: algorithmic issue slots per launch
+    (output words x turns / 64 lanes x slots per word-turn: 9 bitop3 LUTs + 2
+    half-rate shifts per `words_per_lane` words, i.e. 9 + 8/wpl; tile-halo
+    lanes and pipeline fill are overhead, not counted) / launch time / peak.
+    The HBM side comes from the rocprofv3 PMC passes of this same bench
+    command (scripts/pmc_bench.sh -> profiles/pmc_bench.json): measured bytes
+    (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) per launch of the same
+    kernel / the live launch time / 8 TB/s."""
+    if perf["persist_kernel_ms"] >= perf["step_kernel_ms"]:
+        kname, launches, kms, kturns = "gol_persist_kernel", perf["persist_launches"], perf["persist_kernel_ms"], \
+            perf["persist_turns"]
+    else:
+        kname, launches, kms, kturns = "gol_tb_pair_kernel", perf["step_launches"], perf["step_kernel_ms"], \
+            perf["step_turns"]
+    launches = max(1, launches)
+    avg_s = kms / launches * 1e-3
+    wpl = max(1, perf["words_per_lane"])
+    spw = 9.0 + 8.0 / wpl
+    words = rows * ((W + 31) // 32)
+    tpl = kturns / launches
+    slots = words * tpl / 64.0 * spw
+    achieved = slots / avg_s / 1e9 if avg_s > 0 else None
+    alg_bytes = W * rows * tpl * ALG_BYTES_PER_UPDATE
+    out = {
+        "bound": "valu",
+        "achieved": round(achieved, 1) if achieved else None,
+        "peak": VALU_PEAK_GSLOTS,
+        "unit": "Gslot/s (wave64 VALU issue slots)",
+        "frac": round(achieved / VALU_PEAK_GSLOTS, 4) if achieved else None,
+        "traffic": None,
+        "kernel": f"{kname}<{perf['tb_depth']}, {wpl}>",
+        "avg_launch_ms": round(avg_s * 1e3, 5),
+        "launches": launches,
+        "turns_per_launch": tpl,
+        "slots_per_word_turn": spw,
+        "alg_bytes_per_launch": alg_bytes,
+        "temporal_blocking": {"alg_bytes_GBps": round(alg_bytes / avg_s / 1e9, 1) if avg_s > 0 else None,
+                              "note": "0.25 B/cell-update (SURVEY 8d) over the launch time: the single-pass "
+                                      "HBM-equivalent rate, > 8 TB/s because one pass fuses many turns"},
+    }
+    try:
+        with open(pmc_path) as f:
+            rec = json.load(f).get(f"{workload}:{kname}")
+    except (OSError, ValueError):
+        rec = None
+    if rec:
+        traffic = rec["hbm_bytes_per_launch"] * (tpl / rec["turns_per_launch"] if kname == "gol_persist_kernel" else 1)
+        out["traffic"] = traffic
+        out["hbm"] = {"achieved_GBps": round(traffic / avg_s / 1e9, 1), "peak_GBps": HBM_PEAK_GBS,
+                      "frac": round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 4), "source": os.path.relpath(pmc_path, ROOT)}
+        if rec.get("sq_insts_valu"):
+            inst = rec["sq_insts_valu"] * (tpl / rec["turns_per_launch"] if kname == "gol_persist_kernel" else 1)
+            out["valu_measured"] = {"sq_insts_valu_per_launch": inst,
+                                    "issue_frac_vs_peak": round(inst / avg_s / 1e9 / VALU_PEAK_GSLOTS, 4),
+                                    "valu_active_frac": rec.get("valu_active_frac"),
+                                    "clock_ghz": rec.get("clock_ghz_est"),
+                                    "note": "SQ_INSTS_VALU counts instructions (half-rate ones once)"}
+    return out
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -148,13 +224,12 @@ def main():
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     wl = WORKLOADS[a.workload]
     N = a.workload
-    if wl["scaling"] == "weak":
-        W, H, rows = N, N * world, N
-    else:
-        W = H = N
-        rows = H // world
+    if N % world:
+        raise SystemExit(f"{N} rows do not split over {world} ranks")
+    W = H = N
+    rows = H // world
     row0 = rank * rows
-    turns_per_step = a.turns_per_step or (1000 if N <= 16384 else 100)
+    tps = a.turns_per_step or wl["turns"]
 
     import torch
     torch.cuda.set_device(local)
@@ -167,6 +242,9 @@ def main():
         else golhip.Board(W, H, device=local, timing=True)
     board.set_tb_depth(a.tb_depth)
     board.set_rows_per_wave(a.rows_per_wave)
+    for kv in a.option:
+        k, v = kv.split("=")
+        board.set_option(k, int(v))
     if world > 1:
         uid = [golhip.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -179,26 +257,47 @@ def main():
         board.sync()
         torch.cuda.synchronize()
 
+    def global_sum(x: int) -> int:  # mod 2^64 over ranks
+        if dist is None:
+            return x % (1 << 64)
+        t = torch.tensor([x - (1 << 64) if x >= (1 << 63) else x], dtype=torch.int64, device="cuda")
+        dist.all_reduce(t)
+        return int(t.item()) % (1 << 64)
+
+    # warmup step 1 from the fresh board = the parity run
     t_w = time.perf_counter()
-    for _ in range(a.warmup):
-        board.step(turns_per_step)
+    board.step(tps)
+    board.sync()
+    digest = global_sum(board.board_hash())
+    alive = global_sum(board.alive_count()[0])
+    parity = {"turns": tps, "digest": f"{digest:016x}", "alive": alive}
+    try:
+        with open(FULLSIZE) as f:
+            cp = json.load(f)[wl["key"]]["checkpoints"].get(str(tps))
+    except (OSError, ValueError, KeyError):
+        cp = None
+    parity["ok"] = None if cp is None else (cp["hash"] == parity["digest"] and cp["alive"] == alive)
+    parity["fixture"] = "tests/golden/fullsize.json " + (f"{wl['key']} turn {tps}" if cp else "(no checkpoint)")
+    for _ in range(max(0, a.warmup - 1)):
+        board.step(tps)
     board.sync()
     # every rank runs the same number of extra warmup steps (decided by rank 0's clock)
     extra = 0
-    if a.warmup > 0 and a.warmup_seconds > 0:
-        per = max(1e-6, (time.perf_counter() - t_w) / a.warmup)
+    done_w = max(1, a.warmup)
+    if a.warmup_seconds > 0:
+        per = max(1e-6, (time.perf_counter() - t_w) / done_w)
         extra = min(1000, int(max(0.0, a.warmup_seconds - (time.perf_counter() - t_w)) / per))
         if dist is not None:
             x = torch.tensor([extra], dtype=torch.int64, device="cuda")
             dist.broadcast(x, src=0)
             extra = int(x.item())
     for _ in range(extra):
-        board.step(turns_per_step)
+        board.step(tps)
     barrier()
     board.perf_reset()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        board.step(turns_per_step)
+        board.step(tps)
     board.sync()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
@@ -208,39 +307,9 @@ def main():
         dt = float(t.item())
         dist.barrier()
     perf = board.perf()
-    alive, at_turn = board.alive_count(global_sum=world > 1)
+    alive_end, at_turn = board.alive_count(global_sum=world > 1)
 
-    total_updates = W * H * turns_per_step * a.steps if wl["scaling"] == "weak" or world == 1 \
-        else W * H * turns_per_step * a.steps
-    gcups = total_updates / dt / 1e9
-    # dominant kernel (by device time): the persistent or the per-launch step
-    # kernel, each timed with HIP events on the engine stream around every launch
-    if perf["persist_kernel_ms"] >= perf["step_kernel_ms"]:
-        kname, launches, kms, kturns = "gol_persist_kernel", perf["persist_launches"], perf["persist_kernel_ms"], \
-            perf["persist_turns"]
-    else:
-        # per-launch K1: the paired-band kernel (engine default, paired_bands = fill_skip = 1)
-        kname, launches, kms, kturns = "gol_tb_pair_kernel", perf["step_launches"], perf["step_kernel_ms"], \
-            perf["step_turns"]
-    launches = max(1, launches)
-    avg_ms = kms / launches
-    alg_bytes_per_launch = W * rows * (kturns / launches) * ALG_BYTES_PER_UPDATE
-    achieved = alg_bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else None
-    traffic = None
-    try:
-        with open(a.pmc) as f:
-            rec = json.load(f).get(f"{N}:{kname}")
-        if rec:
-            # measured per profiled launch.  A per-launch kernel makes one pass over
-            # the board whatever its depth (read + write once), so its bytes carry
-            # over as they are; a resident launch makes one pass per super-step, so
-            # its bytes scale with this run's turns per launch.
-            traffic = rec["hbm_bytes_per_launch"]
-            if kname == "gol_persist_kernel":
-                traffic *= (kturns / launches) / rec.get("turns_per_launch", kturns / launches)
-    except (OSError, ValueError):
-        pass
-
+    gcups = W * H * tps * a.steps / dt / 1e9
     out = {
         "metric": METRIC,
         "value": round(gcups, 3),
@@ -251,47 +320,35 @@ def main():
         "warmup_extra_steps": extra,
         "ms_per_step": round(dt / a.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": wl["scaling"],
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u32 bit-sliced (1 bit/cell)",
         "data": "synthetic (splitmix64 counter-hash board, 25% alive)",
+        "parity": parity["ok"],
+        "parity_check": parity,
         "config": {
             "workload": wl["desc"],
             "board": [H, W],
             "rows_per_rank": rows,
-            "turns_per_step": turns_per_step,
+            "turns_per_step": tps,
             "tb_depth": a.tb_depth,
             "rows_per_wave": perf["rows_per_wave"],
-            "parallelism": f"row-strips x{world} (RCCL halo ring)" if world > 1 else "single GPU torus",
+            "words_per_lane": perf["words_per_lane"],
+            "parallelism": f"row strips x{world} (RCCL halo ring)" if world > 1 else "single GPU torus",
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved, 1) if achieved else None,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-            "traffic": traffic,
-            "kernel": f"{kname}<{perf['tb_depth']}, {perf['words_per_lane']}>",
-            "avg_launch_ms": round(avg_ms, 5),
-            "launches": launches,
-            "turns_per_launch": kturns / launches,
-            "alg_bytes_per_launch": alg_bytes_per_launch,
-            "note": "achieved = 0.25 B/cell-update (SURVEY 8d) x cell-updates per launch / avg launch time; "
-                    "a launch fuses many turns, so frac > 1 means temporal blocking beat the single-pass "
-                    "HBM roofline (the kernel is VALU-bound, see DESIGN.md 5); traffic = measured HBM bytes "
-                    "per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_traffic.json; one board pass "
-                    "for a per-launch kernel, scaled by super-steps for the resident kernel)",
-        },
-        "final_alive": alive,
+        "roofline": roofline_block(perf, W, rows, N, a.pmc),
+        "final_alive": alive_end,
         "final_turn": at_turn,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(W, a.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(W, wl["seed"], a.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     board.close()
     if dist is not None:
         dist.destroy_process_group()
+    if parity["ok"] is False:
+        sys.exit(1)
 
 
 if __name__ == "__main__":

@@ -1262,7 +1262,12 @@ int golhip_step_flips(golhip_t h, int64_t nturns, int32_t *xy, uint64_t cap, uin
     const int64_t nw = h->local_words();
     const int64_t nb = golk::compact_blocks(nw);
     if (int rc = ensure_blk(h, nb)) return rc;
-    if (int rc = ensure_xy(h, (int64_t)std::min<uint64_t>(cap, (uint64_t)INT64_MAX / 16))) return rc;
+    // a turn flips at most every cell: nturns x local cells bounds the lists
+    // whatever the caller's host-side cap (a generous cap must not
+    // turn into a 10 GB device allocation)
+    const uint64_t most = (uint64_t)nturns * (uint64_t)h->W * (uint64_t)h->rows;
+    const uint64_t dcap = std::min<uint64_t>({cap, most, (uint64_t)INT64_MAX / 16});
+    if (int rc = ensure_xy(h, (int64_t)dcap)) return rc;
     if (h->run_cap < nturns + 1) {
         if (h->d_run) HIP_OR_FAIL(hipFree(h->d_run));
         h->d_run = nullptr;
@@ -1278,7 +1283,7 @@ int golhip_step_flips(golhip_t h, int64_t nturns, int32_t *xy, uint64_t cap, uin
         HIP_OR_FAIL(golk::launch_compact_count(h->cur_rows(), h->prev_rows(), nw, h->d_blk, h->stream));
         HIP_OR_FAIL(golk::launch_compact_scan(h->d_blk, nb, h->d_run + t + 1, h->stream, h->d_run + t));
         HIP_OR_FAIL(golk::launch_compact_scatter(h->cur_rows(), h->prev_rows(), nw, h->Ww, h->row0, h->d_blk, h->d_xy,
-                                                 h->il, h->stream, (unsigned long long)cap));
+                                                 h->il, h->stream, (unsigned long long)dcap));
     }
     std::vector<unsigned long long> run((size_t)nturns + 1);
     HIP_OR_FAIL(hipMemcpyAsync(run.data(), h->d_run, run.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
@@ -1338,6 +1343,22 @@ int golhip_snapshot_bits(golhip_t h, uint32_t *out) {
     HIP_OR_FAIL(golk::launch_convert_layout(h->cur_rows(), h->local_words(), 0, il, h->stream));
     if (int rc_ = sync_stream(h)) return rc_;
     return GOLHIP_OK;
+}
+
+int golhip_snapshot_rows(golhip_t h, int32_t row, int32_t nrows, uint32_t *out) {
+    if (int rc = check(h)) return rc;
+    if (!out || row < 0 || nrows < 0 || (int64_t)row + nrows > h->rows)
+        return fail(GOLHIP_EINVAL, "rows [%d, %d) not in [0, %d)", row, row + nrows, h->rows);
+    if (nrows == 0) return GOLHIP_OK;
+    std::lock_guard<std::mutex> g(h->mu);
+    if (int rc = set_dev(h)) return rc;
+    // a row holds whole pairs / quads in their layouts, so the range converts alone
+    uint32_t *p = h->cur_rows() + (int64_t)row * h->Ww;
+    const int64_t n = (int64_t)nrows * h->Ww;
+    HIP_OR_FAIL(golk::launch_convert_layout(p, n, h->il, 0, h->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(out, p, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_OR_FAIL(golk::launch_convert_layout(p, n, 0, h->il, h->stream));
+    return sync_stream(h);
 }
 
 int golhip_board_hash(golhip_t h, uint64_t *hash) {

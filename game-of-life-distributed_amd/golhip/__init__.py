@@ -112,6 +112,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "golhip_alive_cells": ([H, ctypes.c_void_p, u64, P(u64)], ctypes.c_int),
         "golhip_snapshot_bytes": ([H, ctypes.c_void_p], ctypes.c_int),
         "golhip_snapshot_bits": ([H, ctypes.c_void_p], ctypes.c_int),
+        "golhip_snapshot_rows": ([H, i32, i32, ctypes.c_void_p], ctypes.c_int),
         "golhip_board_hash": ([H, P(u64)], ctypes.c_int),
         "golhip_perf": ([H, P(Perf)], ctypes.c_int),
         "golhip_perf_reset": ([H], ctypes.c_int),
@@ -290,6 +291,12 @@ class Board:
     def snapshot_bits(self) -> np.ndarray:
         out = np.empty((self.rows, self.words), dtype=np.uint32)
         _check(load().golhip_snapshot_bits(self._h, _ptr(out)))
+        return out
+
+    def snapshot_rows(self, row: int, nrows: int) -> np.ndarray:
+        """Canonical bit words of rows [row, row + nrows) of this handle."""
+        out = np.empty((nrows, self.words), dtype=np.uint32)
+        _check(load().golhip_snapshot_rows(self._h, row, nrows, _ptr(out)))
         return out
 
     def board_hash(self) -> int:

@@ -190,6 +190,10 @@ int golhip_alive_cells(golhip_t h, int32_t *xy, uint64_t cap, uint64_t *n);
 /* Board as 0/255 bytes / bit words (this handle's rows). */
 int golhip_snapshot_bytes(golhip_t h, uint8_t *out);
 int golhip_snapshot_bits(golhip_t h, uint32_t *out);
+/* Bit words of rows [row, row + nrows) of this handle (nrows x ceil(width/32)
+ * uint32): a few rows of a board too large to copy whole (the 262144^2
+ * full-size checks). */
+int golhip_snapshot_rows(golhip_t h, int32_t row, int32_t nrows, uint32_t *out);
 /* Order-independent board digest: sum over words of
  * splitmix64((global_word_index << 32) | word) mod 2^64 (strips add up). */
 int golhip_board_hash(golhip_t h, uint64_t *hash);

@@ -80,6 +80,61 @@ static void step_rows(const uint64_t *in, uint64_t *out, int nw, int H, int y0, 
     }
 }
 
+/* ---- full-size fixture helpers (tests/golden/make_fullsize.py) ------------
+ * The BASELINE configs' synthetic boards generated directly
+ * in the packed layout: cell (y, x) alive <=> (splitmix64(seed ^ (y*W + x)) & 3)
+ * == 0, the same rule as oracle_fill_random in gol_oracle.c. */
+static inline uint64_t fc_splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__attribute__((target_clones("avx512f", "avx2", "default")))
+static uint64_t fill_word(uint64_t seed, uint64_t base) {
+    uint64_t v = 0;
+    for (int b = 0; b < 64; b++) v |= (uint64_t)((fc_splitmix64(seed ^ (base + (uint64_t)b)) & 3u) == 0) << b;
+    return v;
+}
+
+/* Rows [row0, row0 + H) of a W-wide synthetic board (strips agree with the whole). */
+int fastcpu_fill_random(uint64_t *words, int W, int H, int64_t row0, uint64_t seed, int threads) {
+    if (W <= 0 || H <= 0 || W % 64 || threads < 1) return -1;
+    const int nw = W / 64;
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (int64_t y = 0; y < H; y++)
+        for (int k = 0; k < nw; k++)
+            words[y * nw + k] = fill_word(seed, (uint64_t)(row0 + y) * (uint64_t)W + 64u * (uint64_t)k);
+    return 0;
+}
+
+/* golhip_board_hash of the same board (include/golhip.h): the sum mod 2^64
+ * over canonical 32-bit words i (row-major, W/32 per row) of
+ * splitmix64((i << 32) | word_i); word 2k of a row is the low half of the
+ * packed uint64 k, word 2k + 1 the high half.  word0 = the global index of
+ * the first 32-bit word (strips add up). */
+uint64_t fastcpu_hash(const uint64_t *words, int W, int H, int64_t word0, int threads) {
+    if (W <= 0 || H <= 0 || W % 64 || threads < 1) return 0;
+    const int64_t n = (int64_t)H * (W / 64);
+    uint64_t h = 0;
+#pragma omp parallel for num_threads(threads) reduction(+ : h) schedule(static)
+    for (int64_t i = 0; i < n; i++) {
+        const uint64_t v = words[i], j = (uint64_t)(word0 + 2 * i);
+        h += fc_splitmix64((j << 32) | (v & 0xFFFFFFFFu)) + fc_splitmix64(((j + 1) << 32) | (v >> 32));
+    }
+    return h;
+}
+
+uint64_t fastcpu_popcount(const uint64_t *words, int W, int H, int threads) {
+    if (W <= 0 || H <= 0 || W % 64 || threads < 1) return 0;
+    const int64_t n = (int64_t)H * (W / 64);
+    uint64_t c = 0;
+#pragma omp parallel for num_threads(threads) reduction(+ : c) schedule(static)
+    for (int64_t i = 0; i < n; i++) c += (uint64_t)__builtin_popcountll(words[i]);
+    return c;
+}
+
 /* `turns` turns in place on H x W/64 words with `threads` OpenMP threads. */
 int fastcpu_run(uint64_t *words, int W, int H, long turns, int threads) {
     if (W <= 0 || H < 3 || W % 64 || threads < 1) return -1;

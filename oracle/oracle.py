@@ -164,6 +164,12 @@ class COracle:
         lib.fastcpu_pack.argtypes = [u8p, ctypes.c_int, ctypes.c_int, u64p]
         lib.fastcpu_unpack.argtypes = [u64p, ctypes.c_int, ctypes.c_int, u8p]
         lib.fastcpu_run.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int]
+        lib.fastcpu_fill_random.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64,
+                                            ctypes.c_int]
+        lib.fastcpu_hash.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int]
+        lib.fastcpu_hash.restype = ctypes.c_uint64
+        lib.fastcpu_popcount.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        lib.fastcpu_popcount.restype = ctypes.c_uint64
         self.lib = lib
 
     @staticmethod
@@ -236,6 +242,22 @@ class COracle:
         H = words.shape[0]
         if self.lib.fastcpu_run(self._p(words, ctypes.c_uint64), W, H, turns, threads) != 0:
             raise ValueError("fastcpu_run")
+
+    def fill_random64(self, W: int, H: int, seed: int, threads: int, row0: int = 0) -> np.ndarray:
+        """Synthetic board (fill_random's rule) packed 64 cells per uint64."""
+        w = np.empty((H, W // 64), dtype=np.uint64)
+        if self.lib.fastcpu_fill_random(self._p(w, ctypes.c_uint64), W, H, row0, seed, threads) != 0:
+            raise ValueError("fastcpu_fill_random needs W % 64 == 0")
+        return w
+
+    def hash64(self, words: np.ndarray, W: int, threads: int, word0: int = 0) -> int:
+        """golhip_board_hash of packed words (strips: word0 = first global 32-bit word)."""
+        return int(self.lib.fastcpu_hash(self._p(np.ascontiguousarray(words), ctypes.c_uint64), W,
+                                         words.shape[0], word0, threads))
+
+    def popcount64(self, words: np.ndarray, W: int, threads: int) -> int:
+        return int(self.lib.fastcpu_popcount(self._p(np.ascontiguousarray(words), ctypes.c_uint64), W,
+                                             words.shape[0], threads))
 
     def run_fast(self, board: np.ndarray, turns: int, threads: int = 1) -> np.ndarray:
         W = board.shape[1]

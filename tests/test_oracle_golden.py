@@ -130,3 +130,44 @@ def test_fastcpu_comparator_matches_golden_boards(fixtures, coracle, n, t):
 def test_fastcpu_comparator_matches_oracle(coracle, W, H, turns, threads):
     b = coracle.fill_random(W, H, 0x5EED0042 + W)
     assert np.array_equal(coracle.run_fast(b, turns, threads), coracle.run(b, turns))
+
+
+# ------------------------------------------- full-size fixture generator (make_fullsize.py)
+@pytest.mark.parametrize("W,H,seed,row0", [(128, 64, 1, 0), (1024, 300, 0x5EED0005, 0), (640, 17, 7, 33)])
+def test_fastcpu_fixture_helpers(coracle, W, H, seed, row0):
+    """fastcpu_fill_random / _hash / _popcount (the full-size fixture generator)
+    equal the per-cell oracle's board and the host digest of golhip_board_hash."""
+    import golhip
+    b = coracle.fill_random(W, H + row0, seed)[row0:]
+    w = coracle.fill_random64(W, H, seed, 4, row0=row0)
+    assert np.array_equal(coracle.unpack64(w, W), b)
+    assert coracle.hash64(w, W, 4, word0=row0 * (W // 32)) == golhip.board_hash_np(pack_bits(b), row0=row0)
+    assert coracle.popcount64(w, W, 4) == int((b == 255).sum())
+    coracle.run_fast_words(w, W, 9, 3)
+    want = coracle.run(coracle.fill_random(W, H, seed), 9) if row0 == 0 else None
+    if want is not None:
+        assert coracle.hash64(w, W, 2) == golhip.board_hash_np(pack_bits(want))
+
+
+def test_fullsize_fixture_file_is_consistent():
+    """tests/golden/fullsize.json covers every GPU config of BASELINE.json and
+    its turn-0 entries equal the generator rule (digest of the fresh board)."""
+    import json
+    import os
+    path = os.path.join(os.path.dirname(__file__), "golden", "fullsize.json")
+    with open(path) as f:
+        js = json.load(f)
+    assert {"c1", "c2", "c3", "c4"} <= set(js)
+    assert js["c1"]["width"] == 16384 and "10000" in js["c1"]["checkpoints"]
+    assert js["c2"]["width"] == 65536 and "1000" in js["c2"]["checkpoints"]
+    assert js["c3"]["width"] == 262144 and "100" in js["c3"]["checkpoints"]
+    assert js["c4"]["width"] == 5120 and len(js["c4"]["flip_counts"]) == js["c4"]["turns"] == 50
+    # configs[3]'s count exceeds 2^31: the 64-bit count path matters
+    assert js["c3"]["checkpoints"]["0"]["alive"] > 2 ** 31
+    # 16384^2 turn 0 recomputed here (0.3 s)
+    co = COracle()
+    w = co.fill_random64(16384, 16384, js["c1"]["seed"], 8)
+    assert f"{co.hash64(w, 16384, 8):016x}" == js["c1"]["checkpoints"]["0"]["hash"]
+    assert co.popcount64(w, 16384, 8) == js["c1"]["checkpoints"]["0"]["alive"]
+    co.run_fast_words(w, 16384, 1, 8)
+    assert f"{co.hash64(w, 16384, 8):016x}" == js["c1"]["checkpoints"]["1"]["hash"]
