@@ -108,4 +108,34 @@ hipError_t launch_compact_scatter(const uint32_t *a, const uint32_t *b, int64_t 
                                   int64_t row0, const unsigned long long *blk_off, int32_t *xy, int il,
                                   hipStream_t s, unsigned long long cap = ~0ull);
 
+// K5: one turn fused with its CellFlipped list (golhip_flip_stream): each
+// block steps 1024 consecutive words of the canonical board (W % 32 == 0),
+// XORs old and new, finds its entries' offset with a single-pass decoupled
+// look-back over the blocks, and writes its entries row-major through LDS.
+// One launch per turn; the turn's lists append at run[0] and run[1] receives
+// the running end.
+constexpr int kFlipFormatXY = 0;   // int32 (x, y) pairs, 8 B per flip
+constexpr int kFlipFormatIdx = 1;  // uint32 y * W + x, 4 B per flip
+struct FlipTurnArgs {
+    const uint32_t *src;
+    uint32_t *dst;
+    int W, Ww, rows;                // rows of this handle
+    int dst_base;                   // physical row of local output row 0
+    RowMap in;                      // input rows, as StepArgs::in
+    long long row0;                 // global row of local row 0
+    int format;                     // kFlipFormat*
+    void *out;                      // entries (device)
+    unsigned long long cap;         // entries that fit in out
+    unsigned long long *run;        // run[0]: entries before this turn; run[1] <- after it
+    unsigned *ticket;               // zeroed before the launch: virtual block ids
+    unsigned long long *status;     // one look-back word per block
+    unsigned epoch;                 // distinct for consecutive launches
+    unsigned *ctl;                  // [0] stop: set by a turn that overflows cap (stop_on_overflow),
+                                    //     every later launch returns at once; [1] error (spin bound)
+    int stop_on_overflow;
+    unsigned long long *alive;      // nullable: += popcount of the new board
+};
+int64_t flip_turn_blocks(int64_t nwords);
+hipError_t launch_flip_turn(const FlipTurnArgs &a, hipStream_t s);
+
 }  // namespace golk

@@ -961,6 +961,224 @@ hipError_t launch_step_generic(const StepArgs &a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
+// K5: one turn + its CellFlipped list, fused (the event stream of
+// distributor.go:93-173 with initializeAliveCells :212-220, BASELINE
+// configs[4]).  Per block of 256 threads, 1024 consecutive canonical words
+// (word k * 256 + tid of the block: every load and board store is a
+// coalesced 256-word access):
+//   1. the turn: three input rows per word, the column neighbours from the
+//      adjacent lanes (DPP; a row's first / last word and the wave's edge
+//      lanes load theirs), the bit-sliced row sums and the 3-LUT rule of K1;
+//   2. flips = old ^ new, counted per word into a packed 4 x 16-bit vector
+//      (one field per k) so ONE block scan orders the block's words;
+//   3. decoupled look-back (blocks take virtual ids from a ticket, so every
+//      predecessor is already running): the block publishes its aggregate,
+//      wave 0 reads up to 64 predecessors per step (one lane each) until the
+//      nearest one holding an inclusive prefix, then publishes its own;
+//      status words are 64-bit agent-scope atomics carrying (flag, epoch,
+//      value) together, so there is no separate payload to hand off;
+//   4. entries (row-major: word order, then bit order) go to LDS at their
+//      block-relative positions and leave in one coalesced copy (blocks
+//      with more entries than LDS holds store them directly).
+// HBM traffic per turn: the board read once (neighbour words hit L1/L2),
+// written once, plus the entries.
+// ---------------------------------------------------------------------------
+constexpr int kFtThreads = 256, kFtK = 4, kFtWords = kFtThreads * kFtK;
+constexpr int kFtLdsBytes = 65536;
+constexpr unsigned long long kFtAgg = 1ull << 62, kFtPrefix = 2ull << 62;
+constexpr unsigned long long kFtValMask = (1ull << 40) - 1;
+
+__device__ __forceinline__ unsigned long long ft_word(unsigned long long flag, unsigned epoch, unsigned long long v) {
+    return flag | ((unsigned long long)(epoch & 0x3FFFFFu) << 40) | (v & kFtValMask);
+}
+
+__global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
+    if (a.ctl[0]) return;  // an earlier turn of the batch overflowed: the host rolls back to it
+    __shared__ unsigned s_vid;
+    __shared__ unsigned long long s_wsum[4];
+    __shared__ unsigned long long s_excl;
+    __shared__ uint32_t s_alive[4];
+    __shared__ alignas(16) unsigned char s_buf[kFtLdsBytes];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (tid == 0) s_vid = atomicAdd(a.ticket, 1u);
+    __syncthreads();
+    const unsigned vid = s_vid;
+    const unsigned Ww = (unsigned)a.Ww;
+    const unsigned nwords = (unsigned)a.rows * Ww;  // host: < 2^32
+    const unsigned base = vid * (unsigned)kFtWords;
+
+    uint32_t flip[kFtK];
+    unsigned long long packed = 0;
+    uint32_t alive_c = 0;
+#pragma unroll
+    for (int k = 0; k < kFtK; ++k) {
+        const unsigned i = base + (unsigned)(k * kFtThreads + tid);
+        const bool valid = i < nwords;
+        const unsigned ii = valid ? i : nwords - 1;  // every lane stays active for the DPP moves
+        const unsigned y = ii / Ww, c = ii - y * Ww;
+        const uint32_t *rows[3] = {a.src + (size_t)map_in_row(a.in, (int)y - 1) * Ww,
+                                   a.src + (size_t)map_in_row(a.in, (int)y) * Ww,
+                                   a.src + (size_t)map_in_row(a.in, (int)y + 1) * Ww};
+        const bool ledge = lane == 0 || c == 0, redge = lane == 63 || c == Ww - 1;
+        const unsigned cl = c == 0 ? Ww - 1 : c - 1, cr = c == Ww - 1 ? 0 : c + 1;
+        uint32_t x[3], h0[3], h1[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            x[j] = rows[j][c];
+            uint32_t l = from_left_lane(x[j]), r = from_right_lane(x[j]);
+            if (ledge) l = rows[j][cl];
+            if (redge) r = rows[j][cr];
+            const uint32_t w = __builtin_amdgcn_alignbit(x[j], l, 31);  // bit b = cell b-1
+            const uint32_t e = __builtin_amdgcn_alignbit(r, x[j], 1);   // bit b = cell b+1
+            h0[j] = bop<kXor3>(w, x[j], e);
+            h1[j] = bop<kMaj>(w, x[j], e);
+        }
+        const uint32_t u0 = bop<kXor3>(h0[0], h0[1], h0[2]), u1 = bop<kMaj>(h0[0], h0[1], h0[2]);
+        const uint32_t v0 = bop<kXor3>(h1[0], h1[1], h1[2]), v1 = bop<kMaj>(h1[0], h1[1], h1[2]);
+        const uint32_t g1 = bop<kG1>(u1, v0, v1), g2 = bop<kG2>(u0, v1, x[1]);
+        const uint32_t nx = bop<kNext>(u0, g1, g2);
+        if (valid) a.dst[(size_t)(a.dst_base + (int)y) * Ww + c] = nx;
+        flip[k] = valid ? (nx ^ x[1]) : 0u;
+        alive_c += valid ? (uint32_t)__builtin_popcount(nx) : 0u;
+        packed |= (unsigned long long)__builtin_popcount(flip[k]) << (16 * k);
+    }
+
+    // block scan of the packed per-k counts (each field <= 256 x 32 < 2^16)
+    unsigned long long inc = packed;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+    }
+    if (lane == 63) s_wsum[wid] = inc;
+    if (a.alive) {
+        const uint32_t t = wave_sum_u32(alive_c);
+        if (lane == 0) s_alive[wid] = t;
+    }
+    __syncthreads();
+    unsigned long long pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        if (w < wid) pre += s_wsum[w];
+        tot += s_wsum[w];
+    }
+    const unsigned long long excl_packed = pre + inc - packed;
+    uint32_t kpre[kFtK], T = 0;
+#pragma unroll
+    for (int k = 0; k < kFtK; ++k) {
+        kpre[k] = T;
+        T += (uint32_t)((tot >> (16 * k)) & 0xFFFFu);
+    }
+
+    if (wid == 0) {
+        unsigned long long excl = 0;
+        if (vid == 0) {
+            excl = a.run[0];
+            if (lane == 0)
+                __hip_atomic_store(&a.status[0], ft_word(kFtPrefix, a.epoch, excl + T), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0)
+                __hip_atomic_store(&a.status[vid], ft_word(kFtAgg, a.epoch, T), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            long long j = (long long)vid - 1 - lane;  // this lane's predecessor
+            const unsigned long long ep = (unsigned long long)(a.epoch & 0x3FFFFFu);
+            for (;;) {
+                unsigned long long st = kFtPrefix;  // lanes past block 0: an empty prefix (never reached)
+                if (j >= 0) {
+                    int spins = 0;
+                    for (;;) {
+                        st = __hip_atomic_load(&a.status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if ((st >> 62) != 0 && ((st >> 40) & 0x3FFFFFull) == ep) break;
+                        if (++spins > (1 << 22)) {  // bounded: record, then treat as an empty prefix
+                            atomicOr(&a.ctl[1], 1u);
+                            st = kFtPrefix | (ep << 40);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+                const unsigned long long pm = __ballot((st >> 62) == 2);
+                if (pm) {
+                    const int first = __builtin_ctzll(pm);  // nearest predecessor with an inclusive prefix
+                    excl += wave_sum_u64(lane <= first ? (st & kFtValMask) : 0ull);
+                    break;
+                }
+                excl += wave_sum_u64(st & kFtValMask);
+                j -= 64;
+            }
+            if (lane == 0)
+                __hip_atomic_store(&a.status[vid], ft_word(kFtPrefix, a.epoch, excl + T), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) {
+            s_excl = excl;
+            if (vid == gridDim.x - 1) {  // the last block's inclusive prefix closes the turn
+                const unsigned long long end = excl + T;
+                a.run[1] = end;
+                if (a.stop_on_overflow && end > a.cap) atomicOr(&a.ctl[0], 1u);
+            }
+            if (a.alive) {
+                const uint32_t al = s_alive[0] + s_alive[1] + s_alive[2] + s_alive[3];
+                if (al) atomicAdd(a.alive, (unsigned long long)al);
+            }
+        }
+    }
+    __syncthreads();
+    const unsigned long long bex = s_excl;
+    const int esz = a.format == kFlipFormatXY ? 8 : 4;
+    const bool staged = T <= (uint32_t)(kFtLdsBytes / esz);
+    auto put = [&](uint32_t pos, unsigned x, unsigned y) {
+        const unsigned long long gy = (unsigned long long)a.row0 + y;
+        if (staged) {
+            if (a.format == kFlipFormatXY)
+                reinterpret_cast<int2 *>(s_buf)[pos] = make_int2((int)x, (int)gy);
+            else
+                reinterpret_cast<uint32_t *>(s_buf)[pos] = (uint32_t)(gy * (unsigned)a.W + x);
+        } else if (bex + pos < a.cap) {
+            if (a.format == kFlipFormatXY)
+                reinterpret_cast<int2 *>(a.out)[bex + pos] = make_int2((int)x, (int)gy);
+            else
+                reinterpret_cast<uint32_t *>(a.out)[bex + pos] = (uint32_t)(gy * (unsigned)a.W + x);
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < kFtK; ++k) {
+        uint32_t m = flip[k];
+        if (!m) continue;
+        uint32_t pos = kpre[k] + (uint32_t)((excl_packed >> (16 * k)) & 0xFFFFu);
+        const unsigned i = base + (unsigned)(k * kFtThreads + tid);
+        const unsigned y = i / Ww, c = i - y * Ww;
+        while (m) {
+            const int b = __builtin_ctz(m);
+            m &= m - 1;
+            put(pos++, c * 32u + (unsigned)b, y);
+        }
+    }
+    if (!staged) return;
+    __syncthreads();
+    const unsigned long long lim = bex >= a.cap ? 0ull : (a.cap - bex < T ? a.cap - bex : (unsigned long long)T);
+    if (a.format == kFlipFormatXY) {
+        const unsigned long long *s = reinterpret_cast<const unsigned long long *>(s_buf);
+        unsigned long long *d = reinterpret_cast<unsigned long long *>(a.out) + bex;
+        for (unsigned long long e = tid; e < lim; e += kFtThreads) d[e] = s[e];
+    } else {
+        const uint32_t *s = reinterpret_cast<const uint32_t *>(s_buf);
+        uint32_t *d = reinterpret_cast<uint32_t *>(a.out) + bex;
+        for (unsigned long long e = tid; e < lim; e += kFtThreads) d[e] = s[e];
+    }
+}
+
+int64_t flip_turn_blocks(int64_t nwords) { return (nwords + kFtWords - 1) / kFtWords; }
+
+hipError_t launch_flip_turn(const FlipTurnArgs &a, hipStream_t s) {
+    const int64_t nb = flip_turn_blocks((int64_t)a.rows * a.Ww);
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(gol_flip_turn_kernel, dim3((unsigned)nb), dim3(kFtThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // K4: pack (0/255 bytes -> bits, alive <=> == 255) and unpack (bits -> 0/255).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void pack_kernel(const uint8_t *__restrict__ bytes, uint32_t *__restrict__ words,

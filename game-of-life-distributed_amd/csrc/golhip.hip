@@ -105,6 +105,13 @@ struct golhip {
     unsigned *h_err = nullptr;  // pinned copy of the error word
     bool persist_pending = false;
     int64_t persist_launches = 0;
+    // resident-launch guard (torus): the board as it was before the step's
+    // resident launch, restored and re-run on the per-launch kernels if that
+    // launch times out (its workgroups were not all co-resident)
+    uint32_t *backup = nullptr;
+    bool guarded = false;
+    int64_t persist_fallbacks = 0;
+    int64_t persist_timeout_ticks = 100000000ll;  // 1 s at the 100 MHz s_memrealtime clock (option "persist_timeout_us")
     int auto_rpw[kNumDepths] = {};  // cache per depth index
     bool loaded = false;
     int il = 0;                 // word layout of the board: 0 canonical, 2 interleaved pairs, 4 quads (= wpl)
@@ -118,8 +125,19 @@ struct golhip {
     int64_t blk_cap = 0;
     int32_t *d_xy = nullptr;
     int64_t xy_cap = 0;
-    unsigned long long *d_run = nullptr;  // golhip_step_flips: running list offsets
+    unsigned long long *d_run = nullptr;  // flip streams: running list offsets
     int64_t run_cap = 0;
+    // flip stream (K5, golhip_flip_stream / golhip_step_flips)
+    unsigned long long *d_ftstatus = nullptr;  // look-back word per block (zeroed once)
+    int64_t ftstatus_cap = 0;
+    unsigned *d_ftticket = nullptr;            // virtual block ids, one counter per turn
+    int64_t ftticket_cap = 0;
+    unsigned *d_ftctl = nullptr;               // [0] stop, [1] look-back spin error
+    void *d_ev = nullptr;                      // entries of a batch
+    int64_t ev_cap_bytes = 0;
+    unsigned flip_epoch = 0;
+    int64_t flip_launches = 0, flip_entries = 0;
+    double flip_ms = 0;
     uint8_t *d_stage = nullptr;  // byte staging for load/snapshot
     int64_t stage_cap = 0;
     bool flips_valid = false;
@@ -135,7 +153,7 @@ struct golhip {
     std::vector<hipEvent_t> ev_pool;
     struct Timed {
         hipEvent_t e0, e1;
-        bool persistent;
+        int kind;  // 0 per-launch step, 1 resident step, 2 flip turn (K5)
     };
     std::vector<Timed> ev_pending;
     double step_ms = 0, persist_ms = 0;
@@ -426,7 +444,7 @@ int drain_events(golhip_t h) {
         HIP_OR_FAIL(hipEventSynchronize(p.e1));
         float ms = 0;
         HIP_OR_FAIL(hipEventElapsedTime(&ms, p.e0, p.e1));
-        (p.persistent ? h->persist_ms : h->step_ms) += ms;
+        (p.kind == 1 ? h->persist_ms : p.kind == 2 ? h->flip_ms : h->step_ms) += ms;
         h->ev_pool.push_back(p.e0);
         h->ev_pool.push_back(p.e1);
     }
@@ -509,7 +527,7 @@ int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int
     if (e != hipSuccess) return fail(GOLHIP_EHIP, "step launch: %s", hipGetErrorString(e));
     if (e1) {
         HIP_OR_FAIL(hipEventRecord(e1, st));
-        h->ev_pending.push_back({e0, e1, false});
+        h->ev_pending.push_back({e0, e1, 0});
         if (h->ev_pending.size() >= 4096) {
             int rc = drain_events(h);
             if (rc) return rc;
@@ -547,6 +565,25 @@ int launch_depth(golhip_t h, int depth, bool count, bool halo) {
 int halo_launches(int rows, int depth, int64_t run) {
     const int64_t k = std::min<int64_t>({(int64_t)kHalo / depth, run, (int64_t)rows / depth});
     return (int)std::max<int64_t>(1, k);
+}
+
+// The next exchange of a halo-mode step: one exchange of k * d rows feeds k
+// launches (resident: k super-steps) of d turns.  The one schedule of both
+// golhip_step and golhip_halo_schedule (what tests/test_dist_gloo.py replays).
+// Per-launch kernels take depth_plan's schedule; between exchanges the
+// resident kernel runs full-depth super-steps cheaply and only a remainder
+// goes to per-launch kernels, which are slow on strips this small: fewest
+// short launches, greedily (1000 = 62 x 16 + 8, not 61 x 16 + 12 + 12).
+struct HaloRun {
+    int d, k;
+};
+HaloRun halo_next(int cap, int rows, bool resident, int64_t left) {
+    DepthRun run = depth_plan(cap, left);
+    if (resident) {
+        const int d = largest_depth(std::min<int64_t>(cap, left));
+        run = {d, left / d};
+    }
+    return {run.d, halo_launches(rows, run.d, run.n)};
 }
 
 int launch_ext(golhip_t h, int depth, bool count, int ext) {
@@ -593,6 +630,9 @@ bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int w
     const int age_split = h->age_split >= 0 ? h->age_split : (nw == 8 ? 65 : 0);
     const bool split = age_split > 0 && age_split < 100;
     if (!golk::plan_persist(h->Ww, base.rows_out, depth, h->cu_count, wpl, nw, &p, h->persist_wg_tx)) return false;
+    // every workgroup must be resident at once (they wait on their neighbours):
+    // the grid may not exceed what the occupancy query admits on this device
+    if ((int64_t)p.cols * p.wg_y > (int64_t)golk::persist_blocks_per_cu(depth, wpl, nw) * h->cu_count) return false;
     if (h->paired_bands && p.wg_sy >= 2 && p.wg_sy % 2 == 0) {
         // the older and the younger wave of a SIMD stream a shared two-band
         // region from both ends and meet where the arbiter's service put them
@@ -628,7 +668,7 @@ bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int w
     p.half_last = half_last ? 1 : 0;
     p.error = h->d_sync;
     p.progress = h->d_sync + 1;
-    p.timeout_ticks = 100000000ll;  // 1 s at the 100 MHz s_memrealtime clock
+    p.timeout_ticks = h->persist_timeout_ticks;
     p.trace = h->d_trace;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (e == hipSuccess && (h->flags & GOLHIP_FLAG_TIMING)) {
@@ -640,7 +680,7 @@ bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int w
         e = golk::launch_persist(p, depth, wpl, h->stream);
     if (e == hipSuccess && e1) {
         e = hipEventRecord(e1, h->stream);
-        h->ev_pending.push_back({e0, e1, true});
+        h->ev_pending.push_back({e0, e1, 1});
     }
     if (e == hipSuccess) e = hipMemcpyAsync(h->h_err, h->d_sync, sizeof(unsigned), hipMemcpyDeviceToHost, h->stream);
     if (e != hipSuccess) {
@@ -677,7 +717,20 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     if (half) ++J;
     const int64_t turns = J * depth - (half ? depth / 2 : 0);
     const bool count = count_last && turns == left;
+    // keep the board recoverable: golhip_step restores it and re-runs the step
+    // on the per-launch kernels if this launch times out
+    const size_t bytes = (size_t)h->local_words() * 4;
+    if (!h->backup && hipMalloc(&h->backup, bytes) != hipSuccess) {
+        h->backup = nullptr;
+        return 0;  // no room for the guard: per-launch kernels
+    }
+    hipError_t e = hipMemcpyAsync(h->backup, h->cur_rows(), bytes, hipMemcpyDeviceToDevice, h->stream);
+    if (e != hipSuccess) {
+        *rc = fail(GOLHIP_EHIP, "resident-launch guard copy: %s", hipGetErrorString(e));
+        return 0;
+    }
     if (!persist_launch(h, step_args(h, nullptr, false), J, depth, wpl, count, rc, half)) return 0;
+    h->guarded = true;
     return turns;
 }
 
@@ -776,6 +829,206 @@ int create_common(int32_t width, int32_t height, int32_t row0, int32_t rows, int
     return GOLHIP_OK;
 }
 
+// Alive count of this handle's rows at the current turn (h->mu held): the
+// fused count of the last launch if it belongs to this turn, else a popcount.
+int alive_count_locked(golhip_t h, uint64_t *count, int64_t *at_turn) {
+    if (int rc = set_dev(h)) return rc;
+    if (h->alive_turn != h->turns) {
+        HIP_OR_FAIL(hipMemsetAsync(h->d_scalars, 0, sizeof(unsigned long long), h->stream));
+        HIP_OR_FAIL(golk::launch_popcount(h->cur_rows(), h->local_words(), h->d_scalars, h->stream));
+        h->alive_turn = h->turns;
+    }
+    HIP_OR_FAIL(hipMemcpyAsync(h->h_scalars, h->d_scalars, sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
+    if (int rc_ = sync_stream(h)) return rc_;
+    *count = h->h_scalars[0];
+    if (at_turn) *at_turn = h->alive_turn;
+    return GOLHIP_OK;
+}
+
+// Grow-only device scratch (contents are not kept).
+template <typename T>
+int ensure_dev(golhip_t h, T **p, int64_t *cap, int64_t n, bool zero = false) {
+    if (*cap >= n) return GOLHIP_OK;
+    if (*p) HIP_OR_FAIL(hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    HIP_OR_FAIL(hipMalloc((void **)p, (size_t)std::max<int64_t>(n, 1) * sizeof(T)));
+    if (zero) HIP_OR_FAIL(hipMemsetAsync(*p, 0, (size_t)std::max<int64_t>(n, 1) * sizeof(T), h->stream));
+    *cap = n;
+    return GOLHIP_OK;
+}
+
+// The CellFlipped stream (distributor.go:93-173 with initializeAliveCells,
+// :212-220): up to nturns single turns, each with its flip list appended in
+// turn order to `out` (row-major within a turn; format: int32 (x, y) pairs or
+// uint32 y * W + x).  stop: never lose an entry — the batch ends before the
+// first turn whose list would not fit (the board is left at the last turn
+// that did, *done says which); otherwise the board advances nturns and the
+// lists are cut at cap (*total is what they needed).  counts[t] = entries
+// of turn t, for t < *done.
+int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64_t cap, uint64_t *counts,
+                       int64_t *done_out, uint64_t *total_out, bool stop) {
+    *done_out = 0;
+    *total_out = 0;
+    if (!h->loaded) return fail(GOLHIP_EINVAL, "no board loaded");
+    if (h->nranks == 1 && !h->torus()) return fail(GOLHIP_EINVAL, "strip handle needs golhip_comm_init");
+    if (int rc = set_dev(h)) return rc;
+    h->flips_valid = false;
+    if (nturns == 0) return GOLHIP_OK;
+    const bool halo = h->comm && (h->nranks > 1 || h->force_halo);
+    const int esz = format == GOLHIP_FLIPS_XY ? 8 : 4;
+    const int64_t nw = h->local_words();
+    const uint64_t most = (uint64_t)nturns * (uint64_t)h->W * (uint64_t)h->rows;
+    const uint64_t dcap = std::min<uint64_t>({cap, most, (uint64_t)INT64_MAX / 16});
+    if (int rc = ensure_dev(h, &h->d_run, &h->run_cap, nturns + 1)) return rc;
+    std::vector<unsigned long long> run((size_t)nturns + 1, 0);
+    unsigned ctl[2] = {0, 0};
+    const int64_t t0 = h->turns;
+    const int c0 = h->cur;
+
+    if (h->W % 32 != 0 || nw >= (1ll << 32) - 4096) {
+        // generic widths (the 16 x 16 fixture) and giant strips: the three-pass
+        // compaction one turn at a time, checked on the host after each turn
+        const int64_t nb = golk::compact_blocks(nw);
+        if (int rc = ensure_blk(h, nb)) return rc;
+        if (int rc = ensure_xy(h, (int64_t)std::min<uint64_t>(dcap, (uint64_t)nw * 32))) return rc;
+        if (int rc = set_layout(h, want_il(h))) return rc;
+        std::vector<int32_t> xy;
+        int64_t t = 0;
+        for (; t < nturns; ++t) {
+            if (halo)
+                if (int rc = exchange_rccl(h, 1, h->stream)) return rc;
+            if (int rc = launch_depth(h, 1, t == nturns - 1, halo)) return rc;
+            HIP_OR_FAIL(golk::launch_compact_count(h->cur_rows(), h->prev_rows(), nw, h->d_blk, h->stream));
+            HIP_OR_FAIL(golk::launch_compact_scan(h->d_blk, nb, h->d_scalars + 1, h->stream));
+            HIP_OR_FAIL(hipMemcpyAsync(h->h_scalars + 1, h->d_scalars + 1, 8, hipMemcpyDeviceToHost, h->stream));
+            if (int rc = sync_stream(h)) return rc;
+            const uint64_t k = h->h_scalars[1];
+            if (stop && run[t] + k > dcap) {  // roll back this turn
+                h->cur ^= 1;
+                h->turns -= 1;
+                h->alive_turn = -1;
+                run[t + 1] = run[t] + k;
+                break;
+            }
+            run[t + 1] = run[t] + k;
+            const uint64_t keep = run[t] >= dcap ? 0 : std::min<uint64_t>(k, dcap - run[t]);
+            if (keep > 0) {
+                HIP_OR_FAIL(golk::launch_compact_scatter(h->cur_rows(), h->prev_rows(), nw, h->Ww, h->row0, h->d_blk,
+                                                         h->d_xy, h->il, h->stream, (unsigned long long)h->xy_cap));
+                xy.resize(2 * keep);
+                HIP_OR_FAIL(hipMemcpyAsync(xy.data(), h->d_xy, keep * 8, hipMemcpyDeviceToHost, h->stream));
+                if (int rc = sync_stream(h)) return rc;
+                for (uint64_t e = 0; e < keep; ++e) {
+                    if (format == GOLHIP_FLIPS_XY) {
+                        static_cast<int32_t *>(out)[2 * (run[t] + e)] = xy[2 * e];
+                        static_cast<int32_t *>(out)[2 * (run[t] + e) + 1] = xy[2 * e + 1];
+                    } else {
+                        static_cast<uint32_t *>(out)[run[t] + e] =
+                            (uint32_t)((uint64_t)xy[2 * e + 1] * (uint64_t)h->W + (uint64_t)xy[2 * e]);
+                    }
+                }
+            }
+        }
+        const int64_t done = t;
+        for (int64_t i = 0; i < done; ++i) counts[i] = run[i + 1] - run[i];
+        *done_out = done;
+        *total_out = (stop && done < nturns) ? (done == 0 ? run[1] : run[done]) : run[done];
+        return GOLHIP_OK;
+    }
+
+    // fused turn + list (K5) on the canonical layout
+    if (int rc = set_layout(h, 0)) return rc;
+    const int64_t nb = golk::flip_turn_blocks(nw);
+    if (int rc = ensure_dev(h, &h->d_ftstatus, &h->ftstatus_cap, nb, true)) return rc;
+    if (int rc = ensure_dev(h, &h->d_ftticket, &h->ftticket_cap, nturns)) return rc;
+    int64_t ctl_cap = h->d_ftctl ? 2 : 0;
+    if (int rc = ensure_dev(h, &h->d_ftctl, &ctl_cap, 2)) return rc;
+    {
+        int64_t bytes_cap = h->ev_cap_bytes;
+        unsigned char *p = static_cast<unsigned char *>(h->d_ev);
+        if (int rc = ensure_dev(h, &p, &bytes_cap, (int64_t)std::max<uint64_t>(dcap, 1) * esz)) return rc;
+        h->d_ev = p;
+        h->ev_cap_bytes = bytes_cap;
+    }
+    HIP_OR_FAIL(hipMemsetAsync(h->d_run, 0, sizeof(unsigned long long), h->stream));
+    HIP_OR_FAIL(hipMemsetAsync(h->d_ftticket, 0, (size_t)nturns * sizeof(unsigned), h->stream));
+    HIP_OR_FAIL(hipMemsetAsync(h->d_ftctl, 0, 2 * sizeof(unsigned), h->stream));
+    golk::StepArgs sa = step_args(h, nullptr, halo);
+    for (int64_t t = 0; t < nturns; ++t) {
+        if (halo)
+            if (int rc = exchange_rccl(h, 1, h->stream)) return rc;
+        const bool last = t == nturns - 1;
+        if (last) HIP_OR_FAIL(hipMemsetAsync(h->d_scalars, 0, sizeof(unsigned long long), h->stream));
+        golk::FlipTurnArgs a{};
+        a.src = h->buf[h->cur];
+        a.dst = h->buf[h->cur ^ 1];
+        a.W = h->W;
+        a.Ww = h->Ww;
+        a.rows = h->rows;
+        a.dst_base = kHalo;
+        a.in = sa.in;
+        a.row0 = h->row0;
+        a.format = format == GOLHIP_FLIPS_XY ? golk::kFlipFormatXY : golk::kFlipFormatIdx;
+        a.out = h->d_ev;
+        a.cap = dcap;
+        a.run = h->d_run + t;
+        a.ticket = h->d_ftticket + t;
+        a.status = h->d_ftstatus;
+        h->flip_epoch = (h->flip_epoch + 1) & 0x3FFFFFu;
+        if (h->flip_epoch == 0) h->flip_epoch = 1;  // 0 is the zeroed status array's epoch
+        a.epoch = h->flip_epoch;
+        a.ctl = h->d_ftctl;
+        a.stop_on_overflow = stop ? 1 : 0;
+        a.alive = last ? h->d_scalars : nullptr;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (h->flags & GOLHIP_FLAG_TIMING) {
+            e0 = take_event(h);
+            e1 = take_event(h);
+            if (!e0 || !e1) return fail(GOLHIP_EHIP, "hipEventCreate failed");
+            HIP_OR_FAIL(hipEventRecord(e0, h->stream));
+        }
+        HIP_OR_FAIL(golk::launch_flip_turn(a, h->stream));
+        if (e1) {
+            HIP_OR_FAIL(hipEventRecord(e1, h->stream));
+            h->ev_pending.push_back({e0, e1, 2});
+        }
+        h->flip_launches++;
+        h->cur ^= 1;
+        h->turns += 1;
+    }
+    HIP_OR_FAIL(hipMemcpyAsync(run.data(), h->d_run, run.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                               h->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(ctl, h->d_ftctl, sizeof ctl, hipMemcpyDeviceToHost, h->stream));
+    if (int rc = sync_stream(h)) return rc;
+    if (ctl[1]) return fail(GOLHIP_EHIP, "flip stream: look-back spin bound exceeded (board undefined)");
+    int64_t done = nturns;
+    if (stop)
+        for (int64_t t = 0; t < nturns; ++t)
+            if (run[t + 1] > dcap) {
+                done = t;
+                break;
+            }
+    if (done < nturns) {  // turn `done` overflowed and the later launches returned at once
+        h->cur = (c0 + (int)(done & 1)) & 1;
+        h->turns = t0 + done;
+        h->alive_turn = -1;
+    } else {
+        h->alive_turn = h->turns;
+    }
+    for (int64_t t = 0; t < done; ++t) counts[t] = run[t + 1] - run[t];
+    const uint64_t total = done < nturns ? (done == 0 ? run[1] : run[done]) : run[nturns];
+    const uint64_t got = done == 0 && nturns > 0 && stop ? 0 : std::min<uint64_t>(run[done], cap);
+    if (got > 0) {
+        HIP_OR_FAIL(hipMemcpyAsync(out, h->d_ev, got * esz, hipMemcpyDeviceToHost, h->stream));
+        if (int rc = sync_stream(h)) return rc;
+    }
+    h->flip_entries += (int64_t)got;
+    *done_out = done;
+    *total_out = total;
+    return GOLHIP_OK;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -823,9 +1076,14 @@ int golhip_destroy(golhip_t h) {
     HIP_RC(hipFree(h->d_blk));
     HIP_RC(hipFree(h->d_xy));
     HIP_RC(hipFree(h->d_run));
+    HIP_RC(hipFree(h->d_ftstatus));
+    HIP_RC(hipFree(h->d_ftticket));
+    HIP_RC(hipFree(h->d_ftctl));
+    HIP_RC(hipFree(h->d_ev));
     HIP_RC(hipFree(h->d_stage));
     HIP_RC(hipFree(h->d_sync));
     HIP_RC(hipFree(h->d_trace));
+    HIP_RC(hipFree(h->backup));
     if (h->h_err) HIP_RC(hipHostFree(h->h_err));
     if (h->own_stream && h->stream) HIP_RC(hipStreamDestroy(h->stream));
     delete h;
@@ -924,6 +1182,11 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         }
         return GOLHIP_OK;
     }
+    if (!strcmp(key, "persist_timeout_us")) {
+        if (value < 1 || value > 60000000) return fail(GOLHIP_EINVAL, "persist_timeout_us %lld", (long long)value);
+        h->persist_timeout_ticks = value * 100;  // s_memrealtime: 100 MHz
+        return GOLHIP_OK;
+    }
     if (!strcmp(key, "force_halo")) {
         h->force_halo = value != 0;
         return GOLHIP_OK;
@@ -972,13 +1235,13 @@ int golhip_comm_init(golhip_t h, const uint8_t id[GOLHIP_UNIQUE_ID_BYTES], int32
     return GOLHIP_OK;
 }
 
-int golhip_halo_schedule(int32_t strip_rows, int32_t tb_depth, int64_t turns_left, int32_t *depth,
-                         int32_t *launches) {
+int golhip_halo_schedule(int32_t strip_rows, int32_t tb_depth, int32_t resident, int64_t turns_left,
+                         int32_t *depth, int32_t *launches) {
     if (!depth || !launches || strip_rows <= 0 || tb_depth < 1 || tb_depth > GOLHIP_MAX_TB_DEPTH || turns_left < 1)
         return fail(GOLHIP_EINVAL, "bad halo schedule request");
-    const DepthRun run = depth_plan(std::min(tb_depth, strip_rows), turns_left);
-    *depth = run.d;
-    *launches = halo_launches(strip_rows, run.d, run.n);
+    const HaloRun hr = halo_next(std::min(tb_depth, strip_rows), strip_rows, resident != 0, turns_left);
+    *depth = hr.d;
+    *launches = hr.k;
     return GOLHIP_OK;
 }
 
@@ -1038,13 +1301,11 @@ int golhip_fill_random(golhip_t h, uint64_t seed) {
     return GOLHIP_OK;
 }
 
-int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
-    if (int rc = check(h)) return rc;
-    if (nturns < 0) return fail(GOLHIP_EINVAL, "nturns %lld", (long long)nturns);
-    std::lock_guard<std::mutex> g(h->mu);
-    if (!h->loaded) return fail(GOLHIP_EINVAL, "no board loaded");
-    if (h->nranks == 1 && !h->torus()) return fail(GOLHIP_EINVAL, "strip handle needs golhip_comm_init or golhip_group_step");
-    if (int rc = set_dev(h)) return rc;
+}  // extern "C"
+
+namespace {
+// golhip_step with h->mu held.
+int step_locked(golhip_t h, int64_t nturns, int32_t want_flips) {
     if (int rc = set_layout(h, want_il(h))) return rc;
     h->flips_valid = false;
     int64_t left = nturns;
@@ -1058,22 +1319,14 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
         if (rc) return rc;
     }
     while (left > tail) {
-        DepthRun run = depth_plan(depth_cap(h, halo), left - tail);
-        if (halo && persist_on(h)) {
-            // between exchanges the resident kernel runs full-depth super-steps
-            // cheaply and only a remainder goes to per-launch kernels, which
-            // are slow on strips this small: fewest short launches, greedily
-            // (1000 = 62 x 16 + 8, not 61 x 16 + 12 + 12)
-            const int d = largest_depth(std::min<int64_t>(depth_cap(h, halo), left - tail));
-            run = {d, (left - tail) / d};
-        }
-        const int d = run.d;
         if (!halo) {
+            const int d = depth_plan(depth_cap(h, false), left - tail).d;
             if (int rc = launch_depth(h, d, left - d == 0, false)) return rc;
             left -= d;
             continue;
         }
-        const int k = halo_launches(sched_rows(h), d, run.n);
+        const HaloRun hr = halo_next(depth_cap(h, true), sched_rows(h), persist_on(h), left - tail);
+        const int d = hr.d, k = hr.k;
         if (int rc = exchange_rccl(h, k * d, h->stream)) return rc;
         int prc = GOLHIP_OK;
         if (try_persist_halo(h, d, k, left - k * d == 0, &prc)) {
@@ -1093,6 +1346,44 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
         if (int rc = start_flips(h)) return rc;
     }
     return GOLHIP_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
+    if (int rc = check(h)) return rc;
+    if (nturns < 0) return fail(GOLHIP_EINVAL, "nturns %lld", (long long)nturns);
+    std::lock_guard<std::mutex> g(h->mu);
+    if (!h->loaded) return fail(GOLHIP_EINVAL, "no board loaded");
+    if (h->nranks == 1 && !h->torus()) return fail(GOLHIP_EINVAL, "strip handle needs golhip_comm_init or golhip_group_step");
+    if (int rc = set_dev(h)) return rc;
+    const int64_t turns0 = h->turns;
+    const int cur0 = h->cur;
+    const int64_t persist_turns0 = h->persist_turns, persist_launches0 = h->persist_launches;
+    int rc = step_locked(h, nturns, want_flips);
+    if (rc || !h->guarded) return rc;
+    // A resident launch ran (torus): check it before returning.  Its
+    // workgroups wait on their neighbours, so a co-tenant kernel holding CUs
+    // can starve one past the bounded spin; then every workgroup drains out
+    // with the error word set and the board is restored from the guard copy
+    // (the board before this step) and re-run on the per-launch kernels.
+    h->guarded = false;
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    h->persist_pending = false;
+    if (!*h->h_err) return GOLHIP_OK;
+    *h->h_err = 0;
+    h->persistent = 0;  // this device is shared: no more resident launches on this handle
+    h->persist_fallbacks++;
+    h->persist_turns = persist_turns0;
+    h->persist_launches = persist_launches0;
+    HIP_OR_FAIL(hipMemcpyAsync(h->buf[cur0] + (int64_t)kHalo * h->Ww, h->backup, (size_t)h->local_words() * 4,
+                               hipMemcpyDeviceToDevice, h->stream));
+    h->cur = cur0;
+    h->turns = turns0;
+    h->alive_turn = -1;
+    h->flips_valid = false;
+    return step_locked(h, nturns, want_flips);
 }
 
 int golhip_group_step(golhip_t *hs, int32_t n, int64_t nturns) {
@@ -1201,23 +1492,17 @@ int golhip_alive_count(golhip_t h, uint64_t *count, int64_t *at_turn) {
     if (int rc = check(h)) return rc;
     if (!count) return fail(GOLHIP_EINVAL, "null out");
     std::lock_guard<std::mutex> g(h->mu);
-    if (int rc = set_dev(h)) return rc;
-    if (h->alive_turn != h->turns) {
-        HIP_OR_FAIL(hipMemsetAsync(h->d_scalars, 0, sizeof(unsigned long long), h->stream));
-        HIP_OR_FAIL(golk::launch_popcount(h->cur_rows(), h->local_words(), h->d_scalars, h->stream));
-        h->alive_turn = h->turns;
-    }
-    HIP_OR_FAIL(hipMemcpyAsync(h->h_scalars, h->d_scalars, sizeof(unsigned long long), hipMemcpyDeviceToHost, h->stream));
-    if (int rc_ = sync_stream(h)) return rc_;
-    *count = h->h_scalars[0];
-    if (at_turn) *at_turn = h->alive_turn;
-    return GOLHIP_OK;
+    return alive_count_locked(h, count, at_turn);
 }
 
 int golhip_alive_count_global(golhip_t h, uint64_t *count, int64_t *at_turn) {
-    if (int rc = golhip_alive_count(h, count, at_turn)) return rc;
-    if (h->nranks == 1 || !h->comm) return GOLHIP_OK;
+    if (int rc = check(h)) return rc;
+    if (!count) return fail(GOLHIP_EINVAL, "null out");
+    // one critical section: local count, copy and allreduce all belong to the
+    // same turn (a concurrent golhip_step cannot advance the board between them)
     std::lock_guard<std::mutex> g(h->mu);
+    if (int rc = alive_count_locked(h, count, at_turn)) return rc;
+    if (h->nranks == 1 || !h->comm) return GOLHIP_OK;
     HIP_OR_FAIL(hipMemcpyAsync(h->d_scalars + 3, h->d_scalars, sizeof(unsigned long long), hipMemcpyDeviceToDevice,
                                h->stream));
     NCCL_OR_FAIL(ncclAllReduce(h->d_scalars + 3, h->d_scalars + 3, 1, ncclUint64, ncclSum, h->comm, h->stream));
@@ -1239,12 +1524,6 @@ int golhip_flips(golhip_t h, int32_t *xy, uint64_t cap, uint64_t *n) {
     return finish_compact(h, h->cur_rows(), h->prev_rows(), xy, cap, n);
 }
 
-// nturns single turns, each followed by its flip compaction appended on the
-// device (the scan starts at the running offset d_run[t], writes d_run[t+1]),
-// then ONE copy of all lists and their counts: the per-turn CellFlipped
-// stream of distributor.go:93-173 + :212-220 without a host round trip per
-// turn.  The board always advances nturns; past cap the lists are cut short
-// and ERANGE reports the total needed in *n.
 int golhip_step_flips(golhip_t h, int64_t nturns, int32_t *xy, uint64_t cap, uint64_t *counts, uint64_t *n) {
     if (int rc = check(h)) return rc;
     if (n) *n = 0;
@@ -1252,53 +1531,37 @@ int golhip_step_flips(golhip_t h, int64_t nturns, int32_t *xy, uint64_t cap, uin
     if (nturns > 0 && !counts) return fail(GOLHIP_EINVAL, "counts is null");
     if (cap > 0 && !xy) return fail(GOLHIP_EINVAL, "xy is null");
     std::lock_guard<std::mutex> g(h->mu);
-    if (!h->loaded) return fail(GOLHIP_EINVAL, "no board loaded");
-    if (h->nranks == 1 && !h->torus()) return fail(GOLHIP_EINVAL, "strip handle needs golhip_comm_init or golhip_group_step");
-    if (int rc = set_dev(h)) return rc;
-    if (int rc = set_layout(h, want_il(h))) return rc;
-    h->flips_valid = false;
-    if (nturns == 0) return GOLHIP_OK;
-    const bool halo = h->comm && (h->nranks > 1 || h->force_halo);
-    const int64_t nw = h->local_words();
-    const int64_t nb = golk::compact_blocks(nw);
-    if (int rc = ensure_blk(h, nb)) return rc;
-    // a turn flips at most every cell: nturns x local cells bounds the lists
-    // whatever the caller's host-side cap (a generous cap must not
-    // turn into a 10 GB device allocation)
-    const uint64_t most = (uint64_t)nturns * (uint64_t)h->W * (uint64_t)h->rows;
-    const uint64_t dcap = std::min<uint64_t>({cap, most, (uint64_t)INT64_MAX / 16});
-    if (int rc = ensure_xy(h, (int64_t)dcap)) return rc;
-    if (h->run_cap < nturns + 1) {
-        if (h->d_run) HIP_OR_FAIL(hipFree(h->d_run));
-        h->d_run = nullptr;
-        h->run_cap = 0;
-        HIP_OR_FAIL(hipMalloc(&h->d_run, (size_t)(nturns + 1) * sizeof(unsigned long long)));
-        h->run_cap = nturns + 1;
-    }
-    HIP_OR_FAIL(hipMemsetAsync(h->d_run, 0, sizeof(unsigned long long), h->stream));
-    for (int64_t t = 0; t < nturns; ++t) {
-        if (halo)
-            if (int rc = exchange_rccl(h, 1, h->stream)) return rc;
-        if (int rc = launch_depth(h, 1, t == nturns - 1, halo)) return rc;
-        HIP_OR_FAIL(golk::launch_compact_count(h->cur_rows(), h->prev_rows(), nw, h->d_blk, h->stream));
-        HIP_OR_FAIL(golk::launch_compact_scan(h->d_blk, nb, h->d_run + t + 1, h->stream, h->d_run + t));
-        HIP_OR_FAIL(golk::launch_compact_scatter(h->cur_rows(), h->prev_rows(), nw, h->Ww, h->row0, h->d_blk, h->d_xy,
-                                                 h->il, h->stream, (unsigned long long)dcap));
-    }
-    std::vector<unsigned long long> run((size_t)nturns + 1);
-    HIP_OR_FAIL(hipMemcpyAsync(run.data(), h->d_run, run.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                               h->stream));
-    if (int rc_ = sync_stream(h)) return rc_;
-    for (int64_t t = 0; t < nturns; ++t) counts[t] = run[t + 1] - run[t];
-    const uint64_t total = run[nturns];
+    int64_t done = 0;
+    uint64_t total = 0;
+    if (int rc = flip_stream_locked(h, nturns, GOLHIP_FLIPS_XY, xy, cap, counts, &done, &total, false)) return rc;
     if (n) *n = total;
-    const uint64_t got = std::min<uint64_t>(total, cap);
-    if (got > 0) {
-        HIP_OR_FAIL(hipMemcpyAsync(xy, h->d_xy, got * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, h->stream));
-        if (int rc_ = sync_stream(h)) return rc_;
-    }
     if (total > cap)
         return fail(GOLHIP_ERANGE, "buffer holds %llu cells, %llu needed", (unsigned long long)cap,
+                    (unsigned long long)total);
+    return GOLHIP_OK;
+}
+
+int golhip_flip_stream(golhip_t h, int64_t nturns, int32_t format, void *out, uint64_t cap, uint64_t *counts,
+                       int64_t *turns_done, uint64_t *n) {
+    if (int rc = check(h)) return rc;
+    if (n) *n = 0;
+    if (turns_done) *turns_done = 0;
+    if (nturns < 0) return fail(GOLHIP_EINVAL, "nturns %lld", (long long)nturns);
+    if (format != GOLHIP_FLIPS_XY && format != GOLHIP_FLIPS_INDEX) return fail(GOLHIP_EINVAL, "format %d", format);
+    if (nturns > 0 && (!counts || !turns_done || !n)) return fail(GOLHIP_EINVAL, "counts / turns_done / n is null");
+    if (cap > 0 && !out) return fail(GOLHIP_EINVAL, "out is null");
+    if (format == GOLHIP_FLIPS_INDEX && (uint64_t)h->W * (uint64_t)h->H > (1ull << 32))
+        return fail(GOLHIP_EINVAL, "cell indices of a %dx%d board do not fit in 32 bits", h->W, h->H);
+    std::lock_guard<std::mutex> g(h->mu);
+    if (h->comm && h->nranks > 1)
+        return fail(GOLHIP_EINVAL, "golhip_flip_stream stops early on one rank alone: use golhip_step_flips in a ring");
+    int64_t done = 0;
+    uint64_t total = 0;
+    if (int rc = flip_stream_locked(h, nturns, format, out, cap, counts, &done, &total, true)) return rc;
+    *turns_done = done;
+    *n = total;
+    if (nturns > 0 && done == 0)
+        return fail(GOLHIP_ERANGE, "buffer holds %llu entries, the next turn needs %llu", (unsigned long long)cap,
                     (unsigned long long)total);
     return GOLHIP_OK;
 }
@@ -1391,7 +1654,11 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     out->persist_launches = h->persist_launches;
     out->persist_turns = h->persist_turns;
     out->persist_kernel_ms = h->persist_ms;
-    out->cell_updates = (int64_t)h->W * h->rows * (h->step_turns + h->persist_turns);
+    out->persist_fallbacks = h->persist_fallbacks;
+    out->flip_launches = h->flip_launches;
+    out->flip_kernel_ms = h->flip_ms;
+    out->flip_entries = h->flip_entries;
+    out->cell_updates = (int64_t)h->W * h->rows * (h->step_turns + h->persist_turns + h->flip_launches);
     out->alg_bytes = out->cell_updates / 4;
     out->halo_bytes = h->halo_bytes;
     const bool halo = h->comm && (h->nranks > 1 || h->force_halo);
@@ -1434,6 +1701,8 @@ int golhip_perf_reset(golhip_t h) {
     h->step_ms = h->persist_ms = 0;
     h->step_launches = h->step_turns = h->halo_bytes = 0;
     h->persist_launches = h->persist_turns = 0;
+    h->flip_launches = h->flip_entries = 0;
+    h->flip_ms = 0;
     return GOLHIP_OK;
 }
 

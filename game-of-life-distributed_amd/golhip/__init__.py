@@ -18,6 +18,7 @@ HEADER = os.path.join(HERE, "..", "..", "include", "golhip.h")
 
 GOLHIP_OK = 0
 GOLHIP_ERANGE = -4
+FLIPS_XY, FLIPS_INDEX = 0, 1
 FLAG_TIMING = 0x1
 UNIQUE_ID_BYTES = 128
 MAX_TB_DEPTH = 32
@@ -46,6 +47,10 @@ class Perf(ctypes.Structure):
         ("rows_per_wave", ctypes.c_int32),
         ("kernel_variant", ctypes.c_int32),
         ("words_per_lane", ctypes.c_int32),
+        ("persist_fallbacks", ctypes.c_int64),
+        ("flip_launches", ctypes.c_int64),
+        ("flip_entries", ctypes.c_int64),
+        ("flip_kernel_ms", ctypes.c_double),
     ]
 
     def as_dict(self) -> dict:
@@ -98,7 +103,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "golhip_comm_init": ([H, ctypes.c_char_p, i32, i32], ctypes.c_int),
         "golhip_group_step": ([P(H), i32, i64], ctypes.c_int),
         "golhip_halo_plan": ([i32, i32, i32, i32, i32, P(HaloPlan)], ctypes.c_int),
-        "golhip_halo_schedule": ([i32, i32, i64, P(i32), P(i32)], ctypes.c_int),
+        "golhip_halo_schedule": ([i32, i32, i32, i64, P(i32), P(i32)], ctypes.c_int),
         "golhip_load_bytes": ([H, ctypes.c_void_p], ctypes.c_int),
         "golhip_load_bits": ([H, ctypes.c_void_p], ctypes.c_int),
         "golhip_fill_random": ([H, u64], ctypes.c_int),
@@ -110,6 +115,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "golhip_flips": ([H, ctypes.c_void_p, u64, P(u64)], ctypes.c_int),
         "golhip_step_flips": ([H, i64, ctypes.c_void_p, u64, ctypes.c_void_p, P(u64)], ctypes.c_int),
         "golhip_alive_cells": ([H, ctypes.c_void_p, u64, P(u64)], ctypes.c_int),
+        "golhip_flip_stream": ([H, i64, i32, ctypes.c_void_p, u64, ctypes.c_void_p, P(i64), P(u64)], ctypes.c_int),
         "golhip_snapshot_bytes": ([H, ctypes.c_void_p], ctypes.c_int),
         "golhip_snapshot_bits": ([H, ctypes.c_void_p], ctypes.c_int),
         "golhip_snapshot_rows": ([H, i32, i32, ctypes.c_void_p], ctypes.c_int),
@@ -144,10 +150,11 @@ def halo_plan(width: int, strip_rows: int, nranks: int, rank: int, depth: int) -
     return {k: getattr(p, k) for k, _ in p._fields_}
 
 
-def halo_schedule(strip_rows: int, tb_depth: int, turns_left: int) -> tuple[int, int]:
+def halo_schedule(strip_rows: int, tb_depth: int, turns_left: int, resident: bool = False) -> tuple[int, int]:
     """(depth, launches) of the next halo exchange (golhip_halo_schedule)."""
     d, k = ctypes.c_int32(), ctypes.c_int32()
-    _check(load().golhip_halo_schedule(strip_rows, tb_depth, turns_left, ctypes.byref(d), ctypes.byref(k)))
+    _check(load().golhip_halo_schedule(strip_rows, tb_depth, 1 if resident else 0, turns_left, ctypes.byref(d),
+                                       ctypes.byref(k)))
     return d.value, k.value
 
 
@@ -279,6 +286,23 @@ class Board:
         n = ctypes.c_uint64()
         _check(load().golhip_step_flips(self._h, nturns, _ptr(xy), cap, _ptr(counts), ctypes.byref(n)))
         return xy[: n.value], counts[:nturns]
+
+    def flip_stream(self, nturns: int, cap: int, fmt: int = FLIPS_XY, out: np.ndarray | None = None):
+        """golhip_flip_stream: up to nturns turns with their flip lists, never
+        dropping one.  Returns (entries, counts, turns_done): entries are
+        (n, 2) int32 (x, y) pairs (FLIPS_XY) or (n,) uint32 cell indices
+        y * width + x (FLIPS_INDEX).  Raises GolHipError (ERANGE) when not
+        even the first turn fits in cap."""
+        shape, dt = ((cap, 2), np.int32) if fmt == FLIPS_XY else ((cap,), np.uint32)
+        if out is None:
+            out = np.empty((max(cap, 1),) + shape[1:], dtype=dt)
+        if out.shape[0] < cap or out.dtype != dt or not out.flags.c_contiguous:
+            raise ValueError("out must be a C-contiguous array of >= cap entries")
+        counts = np.zeros(max(nturns, 1), dtype=np.uint64)
+        done, n = ctypes.c_int64(), ctypes.c_uint64()
+        _check(load().golhip_flip_stream(self._h, nturns, fmt, _ptr(out), cap, _ptr(counts), ctypes.byref(done),
+                                         ctypes.byref(n)))
+        return out[: n.value], counts[: done.value], done.value
 
     def alive_cells(self) -> np.ndarray:
         return self._cells(load().golhip_alive_cells)

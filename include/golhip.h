@@ -71,6 +71,11 @@ typedef struct golhip_perf {
     int32_t rows_per_wave;    /* rows streamed per wavefront (full-depth launch)*/
     int32_t kernel_variant;   /* 0 = generic (width % 32 != 0), 1 = bit-sliced*/
     int32_t words_per_lane;   /* 1, 2 (interleaved pairs) or 4 (quads); 0 generic */
+    int64_t persist_fallbacks; /* resident launches that timed out (not all workgroups
+                                  co-resident) and were re-run on per-launch kernels */
+    int64_t flip_launches;    /* fused turn + flip-list kernels (one turn each)  */
+    int64_t flip_entries;     /* flip-list entries copied to the caller          */
+    double flip_kernel_ms;    /* their summed device time (GOLHIP_FLAG_TIMING)   */
 } golhip_perf_t;
 
 /* ---- library ---------------------------------------------------------- */
@@ -118,6 +123,10 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * is off; "persist_wg_tx" (0 = plan): tiles across a persistent workgroup;
  * "dummy_rows" (0 = all halo rows): rows that absorb masked stores;
  * "trace" (0): persistent-kernel diagnostics (golhip_persist_trace);
+ * "persist_timeout_us" (default 1000000): how long a resident workgroup waits
+ * for a neighbour before the launch is abandoned (whole torus: the board is
+ * restored and the step re-run on per-launch kernels, persist_fallbacks; a
+ * ring strip: the step fails with GOLHIP_EHIP);
  * "force_halo" (0): after golhip_comm_init with one rank, run a whole board
  * through the multi-GPU path as a one-rank RCCL ring (tests, measurement). */
 int golhip_set_option(golhip_t h, const char *key, int64_t value);
@@ -145,13 +154,18 @@ typedef struct golhip_halo_plan {
 } golhip_halo_plan_t;
 int golhip_halo_plan(int32_t width, int32_t strip_rows, int32_t nranks, int32_t rank, int32_t depth,
                      golhip_halo_plan_t *out);
-/* Exchange schedule of a strip: each exchange moves launches * depth halo
- * rows, then `launches` step launches of `depth` turns follow; launch i
- * (0-based) steps rows [-e, strip_rows + e), e = (launches - 1 - i) * depth,
- * so it rebuilds the next launch's halos from the deeper exchanged ones
- * (kernel-side rows, W % 32 == 0; other widths run one turn per launch). */
-int golhip_halo_schedule(int32_t strip_rows, int32_t tb_depth, int64_t turns_left, int32_t *depth,
-                         int32_t *launches);
+/* Exchange schedule of a strip, exactly as golhip_step runs it: each
+ * exchange moves launches * depth halo rows, then `launches` step launches of
+ * `depth` turns follow; launch i (0-based) steps rows [-e, strip_rows + e),
+ * e = (launches - 1 - i) * depth, so it rebuilds the next launch's halos from
+ * the deeper exchanged ones (kernel-side rows, W % 32 == 0; other widths run
+ * one turn per launch).  tb_depth: the most turns a launch may fuse (the
+ * setting capped by the kernel's words per lane, golhip_perf tb_depth);
+ * resident != 0: the strip runs the resident kernel between exchanges
+ * (option "persistent", on by default for strips of <= 64 MiB), which takes
+ * full-depth super-steps greedily instead of the balanced launch plan. */
+int golhip_halo_schedule(int32_t strip_rows, int32_t tb_depth, int32_t resident, int64_t turns_left,
+                         int32_t *depth, int32_t *launches);
 
 /* ---- board I/O -------------------------------------------------------- */
 /* Load this handle's rows (height x width bytes, or its strip's rows). */
@@ -185,6 +199,22 @@ int golhip_flips(golhip_t h, int32_t *xy, uint64_t cap, uint64_t *n);
  * total and the call returns GOLHIP_ERANGE.  Reserves cap pairs on the
  * device. */
 int golhip_step_flips(golhip_t h, int64_t nturns, int32_t *xy, uint64_t cap, uint64_t *counts, uint64_t *n);
+/* The CellFlipped stream without loss: advance UP TO nturns turns, one at a
+ * time, each fused with its flip list on the device (initializeAliveCells,
+ * :212-220), and append the lists in turn order to `out` (row-major within a
+ * turn): format GOLHIP_FLIPS_XY = int32 (x = col, y = row) pairs, 8 bytes a
+ * flip; GOLHIP_FLIPS_INDEX = uint32 y * width + x, 4 bytes a flip (boards of
+ * at most 2^32 cells).  cap counts entries.  The batch stops before the
+ * first turn whose list would not fit, so no flip is ever dropped: the board
+ * is left at the last turn that fitted, *turns_done says how many ran
+ * (counts[t] for t < *turns_done), *n = entries written.  If not even the
+ * first turn fits: GOLHIP_ERANGE, nothing advanced, *n = entries it needs.
+ * One host round trip per call.  Not for multi-rank rings (a stop on one
+ * rank would desynchronise them): use golhip_step_flips there. */
+#define GOLHIP_FLIPS_XY 0
+#define GOLHIP_FLIPS_INDEX 1
+int golhip_flip_stream(golhip_t h, int64_t nturns, int32_t format, void *out, uint64_t cap, uint64_t *counts,
+                       int64_t *turns_done, uint64_t *n);
 /* Alive cells, row-major (x = col, y = row) pairs — calculateAliveCells. */
 int golhip_alive_cells(golhip_t h, int32_t *xy, uint64_t cap, uint64_t *n);
 /* Board as 0/255 bytes / bit words (this handle's rows). */

@@ -2,7 +2,8 @@
 
 Each rank owns a strip of the 64x64 fixture torus and follows libgolhip's
 RCCL path (golhip.hip golhip_step / exchange_rccl): the library's own
-golhip_halo_schedule says how deep the next exchange is (k launches of
+golhip_halo_schedule (the same helper golhip_step calls, for both the
+per-launch and the resident kernel's schedule) says how deep the next exchange is (k launches of
 `depth` turns per exchange of k * depth rows), golhip_halo_plan which rows to
 send / receive, and the four p2p operations are posted in the same order
 (send up, recv bottom, send down, recv top), which is what makes 2 ranks
@@ -33,7 +34,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, splits, turns, tb, q):
+def _worker(rank, world, port, splits, turns, tb, resident, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import sys
@@ -52,7 +53,7 @@ def _worker(rank, world, port, splits, turns, tb, q):
     left = turns
     while left > 0:
         # every rank derives the same schedule from the smallest strip
-        d, k = g.halo_schedule(min(splits), tb, left)
+        d, k = g.halo_schedule(min(splits), tb, left, resident)
         x = k * d
         p = g.halo_plan(64, rows, world, rank, x)
         up = torch.from_numpy(buf[p["send_up_row"]:p["send_up_row"] + x].copy())
@@ -85,13 +86,14 @@ def _worker(rank, world, port, splits, turns, tb, q):
 
 @pytest.mark.parametrize("splits,tb", [([32, 32], 16), ([10, 54], 8), ([20, 20, 24], 32), ([16, 16, 16, 16], 4),
                                        ([1, 63], 32)])
-def test_gloo_strips_match_golden(fixtures, splits, tb):
+@pytest.mark.parametrize("resident", [False, True])
+def test_gloo_strips_match_golden(fixtures, splits, tb, resident):
     from oracle.oracle import unpack_bits
     world = len(splits)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, splits, 100, tb, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, splits, 100, tb, resident, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=240)

@@ -175,3 +175,27 @@ def test_config4_5120_event_stream_per_turn(full):
             assert len(fl) == rec["flip_counts"][t], t
             sha.update(fl.tobytes())
         assert sha.hexdigest() == rec["flips_sha256"]
+
+
+def test_config4_5120_flip_stream_index(full):
+    """configs[4] through golhip_flip_stream (fused K5 kernel, 4-byte cell
+    indices, a 16 M-entry buffer so calls stop early and resume): decoded to
+    (x, y) pairs the stream hashes to the fixture."""
+    js, _ = full
+    rec = js["c4"]
+    N = rec["width"]
+    sha, counts_all = hashlib.sha256(), []
+    cap = 16 << 20  # turns 1..50 flip 2.6-7.2 M cells each
+    out = np.empty(cap, dtype=np.uint32)
+    with golhip.Board(N, N) as b:
+        b.fill_random(rec["seed"])
+        while len(counts_all) < rec["turns"]:
+            ent, counts, done = b.flip_stream(rec["turns"] - len(counts_all), cap=cap, fmt=golhip.FLIPS_INDEX,
+                                              out=out)
+            assert done >= 1
+            idx = ent.astype(np.int64)
+            sha.update(np.stack([idx % N, idx // N], axis=1).astype(np.int32).tobytes())
+            counts_all += [int(c) for c in counts]
+        assert counts_all == rec["flip_counts"]
+        assert sha.hexdigest() == rec["flips_sha256"]
+        assert (f"{b.board_hash():016x}", b.alive_count()) == (rec["final"]["hash"], (rec["final"]["alive"], 50))
