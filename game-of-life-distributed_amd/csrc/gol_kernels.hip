@@ -984,7 +984,9 @@ hipError_t launch_step_generic(const StepArgs &a, hipStream_t s) {
 // written once, plus the entries.
 // ---------------------------------------------------------------------------
 constexpr int kFtThreads = 256, kFtK = 4, kFtWords = kFtThreads * kFtK;
-constexpr int kFtLdsBytes = 65536;
+// 32 KiB of entry staging: four blocks per CU, so a 5120^2 turn (800 blocks)
+// is resident at once; a block with more entries stores them directly.
+constexpr int kFtLdsBytes = 32768;
 constexpr unsigned long long kFtAgg = 1ull << 62, kFtPrefix = 2ull << 62;
 constexpr unsigned long long kFtValMask = (1ull << 40) - 1;
 
@@ -992,6 +994,25 @@ __device__ __forceinline__ unsigned long long ft_word(unsigned long long flag, u
     return flag | ((unsigned long long)(epoch & 0x3FFFFFu) << 40) | (v & kFtValMask);
 }
 
+// 3-LUT B3/S23 rule of K1 on three rows' words with their west / east
+// neighbour words already aligned (bit b = cell b -+ 1).
+__device__ __forceinline__ uint32_t ft_rule(const uint32_t (&w)[3], const uint32_t (&x)[3], const uint32_t (&e)[3]) {
+    uint32_t h0[3], h1[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        h0[j] = bop<kXor3>(w[j], x[j], e[j]);
+        h1[j] = bop<kMaj>(w[j], x[j], e[j]);
+    }
+    const uint32_t u0 = bop<kXor3>(h0[0], h0[1], h0[2]), u1 = bop<kMaj>(h0[0], h0[1], h0[2]);
+    const uint32_t v0 = bop<kXor3>(h1[0], h1[1], h1[2]), v1 = bop<kMaj>(h1[0], h1[1], h1[2]);
+    const uint32_t g1 = bop<kG1>(u1, v0, v1), g2 = bop<kG2>(u0, v1, x[1]);
+    return bop<kNext>(u0, g1, g2);
+}
+
+// CONTIG (Ww % 4 == 0): thread tid of the block owns the 4 consecutive words
+// base + 4 tid .. + 3 of one row (16-byte loads and stores); otherwise word
+// base + k * 256 + tid for k = 0..3 (4-byte accesses, any Ww).
+template <bool CONTIG>
 __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
     if (a.ctl[0]) return;  // an earlier turn of the batch overflowed: the host rolls back to it
     __shared__ unsigned s_vid;
@@ -1008,42 +1029,89 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
     const unsigned base = vid * (unsigned)kFtWords;
 
     uint32_t flip[kFtK];
-    unsigned long long packed = 0;
+    unsigned long long packed = 0;  // CONTIG: the thread's count in field 0; else one 16-bit field per k
     uint32_t alive_c = 0;
-#pragma unroll
-    for (int k = 0; k < kFtK; ++k) {
-        const unsigned i = base + (unsigned)(k * kFtThreads + tid);
-        const bool valid = i < nwords;
-        const unsigned ii = valid ? i : nwords - 1;  // every lane stays active for the DPP moves
+    if constexpr (CONTIG) {
+        const unsigned i0 = base + 4u * (unsigned)tid;
+        const bool valid = i0 < nwords;
+        const unsigned ii = valid ? i0 : nwords - 4;  // every lane stays active for the DPP moves
         const unsigned y = ii / Ww, c = ii - y * Ww;
         const uint32_t *rows[3] = {a.src + (size_t)map_in_row(a.in, (int)y - 1) * Ww,
                                    a.src + (size_t)map_in_row(a.in, (int)y) * Ww,
                                    a.src + (size_t)map_in_row(a.in, (int)y + 1) * Ww};
-        const bool ledge = lane == 0 || c == 0, redge = lane == 63 || c == Ww - 1;
-        const unsigned cl = c == 0 ? Ww - 1 : c - 1, cr = c == Ww - 1 ? 0 : c + 1;
-        uint32_t x[3], h0[3], h1[3];
+        const unsigned cl = c == 0 ? Ww - 1 : c - 1, cr = c + 4 == Ww ? 0 : c + 4;
+        const bool ledge = lane == 0 || c == 0, redge = lane == 63 || c + 4 == Ww;
+        // all loads first (the edge words unconditionally: L1 hits beside the 16-B loads)
+        uint4 q[3];
+        uint32_t le[3], re[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            x[j] = rows[j][c];
-            uint32_t l = from_left_lane(x[j]), r = from_right_lane(x[j]);
-            if (ledge) l = rows[j][cl];
-            if (redge) r = rows[j][cr];
-            const uint32_t w = __builtin_amdgcn_alignbit(x[j], l, 31);  // bit b = cell b-1
-            const uint32_t e = __builtin_amdgcn_alignbit(r, x[j], 1);   // bit b = cell b+1
-            h0[j] = bop<kXor3>(w, x[j], e);
-            h1[j] = bop<kMaj>(w, x[j], e);
+            q[j] = *reinterpret_cast<const uint4 *>(rows[j] + c);
+            le[j] = rows[j][cl];
+            re[j] = rows[j][cr];
         }
-        const uint32_t u0 = bop<kXor3>(h0[0], h0[1], h0[2]), u1 = bop<kMaj>(h0[0], h0[1], h0[2]);
-        const uint32_t v0 = bop<kXor3>(h1[0], h1[1], h1[2]), v1 = bop<kMaj>(h1[0], h1[1], h1[2]);
-        const uint32_t g1 = bop<kG1>(u1, v0, v1), g2 = bop<kG2>(u0, v1, x[1]);
-        const uint32_t nx = bop<kNext>(u0, g1, g2);
-        if (valid) a.dst[(size_t)(a.dst_base + (int)y) * Ww + c] = nx;
-        flip[k] = valid ? (nx ^ x[1]) : 0u;
-        alive_c += valid ? (uint32_t)__builtin_popcount(nx) : 0u;
-        packed |= (unsigned long long)__builtin_popcount(flip[k]) << (16 * k);
+        uint32_t x[4][3], wv[4][3], ev[4][3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const uint32_t v[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+            uint32_t l = from_left_lane(v[3]), r = from_right_lane(v[0]);
+            l = ledge ? le[j] : l;
+            r = redge ? re[j] : r;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                x[k][j] = v[k];
+                wv[k][j] = __builtin_amdgcn_alignbit(v[k], k == 0 ? l : v[k - 1], 31);  // bit b = cell b-1
+                ev[k][j] = __builtin_amdgcn_alignbit(k == 3 ? r : v[k + 1], v[k], 1);  // bit b = cell b+1
+            }
+        }
+        uint32_t nx[4], cnt = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            nx[k] = ft_rule(wv[k], x[k], ev[k]);
+            flip[k] = valid ? (nx[k] ^ x[k][1]) : 0u;
+            cnt += (uint32_t)__builtin_popcount(flip[k]);
+            alive_c += valid ? (uint32_t)__builtin_popcount(nx[k]) : 0u;
+        }
+        if (valid)
+            *reinterpret_cast<uint4 *>(a.dst + (size_t)(a.dst_base + (int)y) * Ww + c) =
+                make_uint4(nx[0], nx[1], nx[2], nx[3]);
+        packed = cnt;
+    } else {
+#pragma unroll
+        for (int k = 0; k < kFtK; ++k) {
+            const unsigned i = base + (unsigned)(k * kFtThreads + tid);
+            const bool valid = i < nwords;
+            const unsigned ii = valid ? i : nwords - 1;
+            const unsigned y = ii / Ww, c = ii - y * Ww;
+            const uint32_t *rows[3] = {a.src + (size_t)map_in_row(a.in, (int)y - 1) * Ww,
+                                       a.src + (size_t)map_in_row(a.in, (int)y) * Ww,
+                                       a.src + (size_t)map_in_row(a.in, (int)y + 1) * Ww};
+            const bool ledge = lane == 0 || c == 0, redge = lane == 63 || c == Ww - 1;
+            const unsigned cl = c == 0 ? Ww - 1 : c - 1, cr = c == Ww - 1 ? 0 : c + 1;
+            uint32_t x[3], le[3], re[3], w[3], e[3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                x[j] = rows[j][c];
+                le[j] = rows[j][cl];
+                re[j] = rows[j][cr];
+            }
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                uint32_t l = from_left_lane(x[j]), r = from_right_lane(x[j]);
+                l = ledge ? le[j] : l;
+                r = redge ? re[j] : r;
+                w[j] = __builtin_amdgcn_alignbit(x[j], l, 31);
+                e[j] = __builtin_amdgcn_alignbit(r, x[j], 1);
+            }
+            const uint32_t nx = ft_rule(w, x, e);
+            if (valid) a.dst[(size_t)(a.dst_base + (int)y) * Ww + c] = nx;
+            flip[k] = valid ? (nx ^ x[1]) : 0u;
+            alive_c += valid ? (uint32_t)__builtin_popcount(nx) : 0u;
+            packed |= (unsigned long long)__builtin_popcount(flip[k]) << (16 * k);
+        }
     }
 
-    // block scan of the packed per-k counts (each field <= 256 x 32 < 2^16)
+    // block scan of the packed counts (each field <= 256 x 128 < 2^16)
     unsigned long long inc = packed;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1063,11 +1131,18 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
         tot += s_wsum[w];
     }
     const unsigned long long excl_packed = pre + inc - packed;
-    uint32_t kpre[kFtK], T = 0;
+    uint32_t pos[kFtK], T = 0;
+    if constexpr (CONTIG) {
+        T = (uint32_t)(tot & 0xFFFFu);
+        pos[0] = (uint32_t)(excl_packed & 0xFFFFu);
 #pragma unroll
-    for (int k = 0; k < kFtK; ++k) {
-        kpre[k] = T;
-        T += (uint32_t)((tot >> (16 * k)) & 0xFFFFu);
+        for (int k = 1; k < kFtK; ++k) pos[k] = pos[k - 1] + (uint32_t)__builtin_popcount(flip[k - 1]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < kFtK; ++k) {
+            pos[k] = T + (uint32_t)((excl_packed >> (16 * k)) & 0xFFFFu);
+            T += (uint32_t)((tot >> (16 * k)) & 0xFFFFu);
+        }
     }
 
     if (wid == 0) {
@@ -1128,44 +1203,44 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
     const unsigned long long bex = s_excl;
     const int esz = a.format == kFlipFormatXY ? 8 : 4;
     const bool staged = T <= (uint32_t)(kFtLdsBytes / esz);
-    auto put = [&](uint32_t pos, unsigned x, unsigned y) {
+    auto put = [&](uint32_t p, unsigned x, unsigned y) {
         const unsigned long long gy = (unsigned long long)a.row0 + y;
         if (staged) {
             if (a.format == kFlipFormatXY)
-                reinterpret_cast<int2 *>(s_buf)[pos] = make_int2((int)x, (int)gy);
+                reinterpret_cast<int2 *>(s_buf)[p] = make_int2((int)x, (int)gy);
             else
-                reinterpret_cast<uint32_t *>(s_buf)[pos] = (uint32_t)(gy * (unsigned)a.W + x);
-        } else if (bex + pos < a.cap) {
+                reinterpret_cast<uint32_t *>(s_buf)[p] = (uint32_t)(gy * (unsigned)a.W + x);
+        } else if (bex + p < a.cap) {
             if (a.format == kFlipFormatXY)
-                reinterpret_cast<int2 *>(a.out)[bex + pos] = make_int2((int)x, (int)gy);
+                reinterpret_cast<int2 *>(a.out)[bex + p] = make_int2((int)x, (int)gy);
             else
-                reinterpret_cast<uint32_t *>(a.out)[bex + pos] = (uint32_t)(gy * (unsigned)a.W + x);
+                reinterpret_cast<uint32_t *>(a.out)[bex + p] = (uint32_t)(gy * (unsigned)a.W + x);
         }
     };
 #pragma unroll
     for (int k = 0; k < kFtK; ++k) {
         uint32_t m = flip[k];
         if (!m) continue;
-        uint32_t pos = kpre[k] + (uint32_t)((excl_packed >> (16 * k)) & 0xFFFFu);
-        const unsigned i = base + (unsigned)(k * kFtThreads + tid);
+        uint32_t p = pos[k];
+        const unsigned i = CONTIG ? base + 4u * (unsigned)tid + (unsigned)k : base + (unsigned)(k * kFtThreads + tid);
         const unsigned y = i / Ww, c = i - y * Ww;
         while (m) {
             const int b = __builtin_ctz(m);
             m &= m - 1;
-            put(pos++, c * 32u + (unsigned)b, y);
+            put(p++, c * 32u + (unsigned)b, y);
         }
     }
     if (!staged) return;
     __syncthreads();
     const unsigned long long lim = bex >= a.cap ? 0ull : (a.cap - bex < T ? a.cap - bex : (unsigned long long)T);
     if (a.format == kFlipFormatXY) {
-        const unsigned long long *s = reinterpret_cast<const unsigned long long *>(s_buf);
+        const unsigned long long *sb = reinterpret_cast<const unsigned long long *>(s_buf);
         unsigned long long *d = reinterpret_cast<unsigned long long *>(a.out) + bex;
-        for (unsigned long long e = tid; e < lim; e += kFtThreads) d[e] = s[e];
+        for (unsigned long long e = tid; e < lim; e += kFtThreads) d[e] = sb[e];
     } else {
-        const uint32_t *s = reinterpret_cast<const uint32_t *>(s_buf);
+        const uint32_t *sb = reinterpret_cast<const uint32_t *>(s_buf);
         uint32_t *d = reinterpret_cast<uint32_t *>(a.out) + bex;
-        for (unsigned long long e = tid; e < lim; e += kFtThreads) d[e] = s[e];
+        for (unsigned long long e = tid; e < lim; e += kFtThreads) d[e] = sb[e];
     }
 }
 
@@ -1174,7 +1249,10 @@ int64_t flip_turn_blocks(int64_t nwords) { return (nwords + kFtWords - 1) / kFtW
 hipError_t launch_flip_turn(const FlipTurnArgs &a, hipStream_t s) {
     const int64_t nb = flip_turn_blocks((int64_t)a.rows * a.Ww);
     if (nb == 0) return hipSuccess;
-    hipLaunchKernelGGL(gol_flip_turn_kernel, dim3((unsigned)nb), dim3(kFtThreads), 0, s, a);
+    if (a.Ww % 4 == 0)
+        hipLaunchKernelGGL(gol_flip_turn_kernel<true>, dim3((unsigned)nb), dim3(kFtThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL(gol_flip_turn_kernel<false>, dim3((unsigned)nb), dim3(kFtThreads), 0, s, a);
     return hipGetLastError();
 }
 

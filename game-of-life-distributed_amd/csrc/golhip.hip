@@ -35,6 +35,25 @@ namespace {
 
 thread_local std::string g_err;
 
+// Page-locked, device-mapped host buffers from golhip_host_alloc: the flip
+// stream writes its entries into them straight from the kernel.
+struct HostBuf {
+    uintptr_t base;
+    size_t bytes;
+    void *dev;  // device address of base
+};
+std::mutex g_host_mu;
+std::vector<HostBuf> g_host_bufs;
+
+// Device address of [p, p + bytes) if it lies inside one golhip_host_alloc buffer.
+void *mapped_device_ptr(const void *p, size_t bytes) {
+    std::lock_guard<std::mutex> g(g_host_mu);
+    const uintptr_t a = (uintptr_t)p;
+    for (const HostBuf &b : g_host_bufs)
+        if (a >= b.base && a + bytes <= b.base + b.bytes) return (char *)b.dev + (a - b.base);
+    return nullptr;
+}
+
 int fail(int code, const char *fmt, ...) {
     char buf[512];
     va_list ap;
@@ -937,14 +956,16 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
         return GOLHIP_OK;
     }
 
-    // fused turn + list (K5) on the canonical layout
+    // fused turn + list (K5) on the canonical layout; into a golhip_host_alloc
+    // buffer the kernel writes the entries itself (no device list, no copy)
     if (int rc = set_layout(h, 0)) return rc;
+    void *direct = mapped_device_ptr(out, (size_t)dcap * esz);
     const int64_t nb = golk::flip_turn_blocks(nw);
     if (int rc = ensure_dev(h, &h->d_ftstatus, &h->ftstatus_cap, nb, true)) return rc;
     if (int rc = ensure_dev(h, &h->d_ftticket, &h->ftticket_cap, nturns)) return rc;
     int64_t ctl_cap = h->d_ftctl ? 2 : 0;
     if (int rc = ensure_dev(h, &h->d_ftctl, &ctl_cap, 2)) return rc;
-    {
+    if (!direct) {
         int64_t bytes_cap = h->ev_cap_bytes;
         unsigned char *p = static_cast<unsigned char *>(h->d_ev);
         if (int rc = ensure_dev(h, &p, &bytes_cap, (int64_t)std::max<uint64_t>(dcap, 1) * esz)) return rc;
@@ -970,7 +991,7 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
         a.in = sa.in;
         a.row0 = h->row0;
         a.format = format == GOLHIP_FLIPS_XY ? golk::kFlipFormatXY : golk::kFlipFormatIdx;
-        a.out = h->d_ev;
+        a.out = direct ? direct : h->d_ev;
         a.cap = dcap;
         a.run = h->d_run + t;
         a.ticket = h->d_ftticket + t;
@@ -1019,7 +1040,7 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
     for (int64_t t = 0; t < done; ++t) counts[t] = run[t + 1] - run[t];
     const uint64_t total = done < nturns ? (done == 0 ? run[1] : run[done]) : run[nturns];
     const uint64_t got = done == 0 && nturns > 0 && stop ? 0 : std::min<uint64_t>(run[done], cap);
-    if (got > 0) {
+    if (got > 0 && !direct) {
         HIP_OR_FAIL(hipMemcpyAsync(out, h->d_ev, got * esz, hipMemcpyDeviceToHost, h->stream));
         if (int rc = sync_stream(h)) return rc;
     }
@@ -1045,6 +1066,36 @@ int golhip_device_count(int32_t *n) {
     int c = 0;
     HIP_OR_FAIL(hipGetDeviceCount(&c));
     *n = c;
+    return GOLHIP_OK;
+}
+
+int golhip_host_alloc(uint64_t bytes, void **out) {
+    if (!out || bytes == 0) return fail(GOLHIP_EINVAL, "bad host allocation");
+    *out = nullptr;
+    void *p = nullptr, *d = nullptr;
+    hipError_t e = hipHostMalloc(&p, (size_t)bytes, hipHostMallocDefault);
+    if (e != hipSuccess) return fail(GOLHIP_ENOMEM, "hipHostMalloc(%llu): %s", (unsigned long long)bytes, hipGetErrorString(e));
+    e = hipHostGetDevicePointer(&d, p, 0);
+    if (e != hipSuccess) {
+        (void)hipHostFree(p);
+        return fail(GOLHIP_EHIP, "hipHostGetDevicePointer: %s", hipGetErrorString(e));
+    }
+    std::lock_guard<std::mutex> g(g_host_mu);
+    g_host_bufs.push_back({(uintptr_t)p, (size_t)bytes, d});
+    *out = p;
+    return GOLHIP_OK;
+}
+
+int golhip_host_free(void *p) {
+    if (!p) return GOLHIP_OK;
+    {
+        std::lock_guard<std::mutex> g(g_host_mu);
+        auto it = std::find_if(g_host_bufs.begin(), g_host_bufs.end(),
+                               [&](const HostBuf &b) { return b.base == (uintptr_t)p; });
+        if (it == g_host_bufs.end()) return fail(GOLHIP_EINVAL, "not a golhip_host_alloc buffer");
+        g_host_bufs.erase(it);
+    }
+    HIP_OR_FAIL(hipHostFree(p));
     return GOLHIP_OK;
 }
 

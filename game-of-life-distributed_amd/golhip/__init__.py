@@ -91,6 +91,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "golhip_version": ([], ctypes.c_char_p),
         "golhip_last_error": ([], ctypes.c_char_p),
         "golhip_device_count": ([P(i32)], ctypes.c_int),
+        "golhip_host_alloc": ([u64, P(ctypes.c_void_p)], ctypes.c_int),
+        "golhip_host_free": ([ctypes.c_void_p], ctypes.c_int),
         "golhip_create": ([i32, i32, i32, u32, P(H)], ctypes.c_int),
         "golhip_create_strip": ([i32, i32, i32, i32, i32, u32, P(H)], ctypes.c_int),
         "golhip_destroy": ([H], ctypes.c_int),
@@ -156,6 +158,31 @@ def halo_schedule(strip_rows: int, tb_depth: int, turns_left: int, resident: boo
     _check(load().golhip_halo_schedule(strip_rows, tb_depth, 1 if resident else 0, turns_left, ctypes.byref(d),
                                        ctypes.byref(k)))
     return d.value, k.value
+
+
+class HostArray(np.ndarray):
+    """numpy view of golhip_host_alloc memory (page-locked, device-mapped); freed with the array."""
+
+    def __del__(self):
+        p = getattr(self, "_golhip_ptr", None)
+        if p:
+            self._golhip_ptr = None
+            try:
+                load().golhip_host_free(ctypes.c_void_p(p))
+            except Exception:
+                pass
+
+
+def host_array(shape, dtype) -> np.ndarray:
+    """A flip buffer the device writes directly (golhip_host_alloc)."""
+    dt = np.dtype(dtype)
+    n = int(np.prod(shape)) * dt.itemsize
+    p = ctypes.c_void_p()
+    _check(load().golhip_host_alloc(n, ctypes.byref(p)))
+    buf = (ctypes.c_char * n).from_address(p.value)
+    a = np.frombuffer(buf, dtype=dt).reshape(shape).view(HostArray)
+    a._golhip_ptr = p.value
+    return a
 
 
 def unique_id() -> bytes:

@@ -83,6 +83,13 @@ const char *golhip_version(void);
 const char *golhip_last_error(void);
 int golhip_device_count(int32_t *n);
 
+/* Page-locked host memory that the device writes directly (hipHostMalloc,
+ * mapped).  A golhip_flip_stream whose `out` lies inside such a buffer gets
+ * its entries written by the kernel itself over PCIe: no device list and no
+ * copy after the batch.  Go callers use it as C memory (unsafe.Slice). */
+int golhip_host_alloc(uint64_t bytes, void **out);
+int golhip_host_free(void *p);
+
 /* ---- handles ---------------------------------------------------------- */
 /* Whole width x height torus on one device.  Replaces the world allocation
  * of distributor.go:66-69. */

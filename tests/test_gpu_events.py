@@ -92,6 +92,36 @@ def test_flip_stream_stops_without_loss(fixtures, coracle, W, H, fmt):
         assert np.array_equal(got[t], want[t]), t
 
 
+@pytest.mark.parametrize("fmt", [0, 1])
+def test_flip_stream_into_pinned_host_buffer(fixtures, coracle, fmt):
+    """out inside a golhip_host_alloc buffer: the kernel writes the entries
+    over PCIe itself; same lists, same early stop."""
+    W = H = 512
+    board = unpack_bits(fixtures["image_512"], 512)
+    want, cur = [], board
+    for _ in range(30):
+        nxt = step_np(cur)
+        want.append(flips_np(cur, nxt))
+        cur = nxt
+    cap = max(len(w) for w in want) * 4
+    out = golhip.host_array((cap, 2) if fmt == 0 else (cap,), np.int32 if fmt == 0 else np.uint32)
+    got = []
+    with golhip.Board(W, H) as b:
+        b.load_bytes(board)
+        while len(got) < 30:
+            ent, counts, done = b.flip_stream(30 - len(got), cap=cap, fmt=fmt, out=out)
+            assert done >= 1
+            xy = ent if fmt == 0 else idx_to_xy(ent, W)
+            off = 0
+            for c in counts:
+                got.append(xy[off:off + int(c)].copy())
+                off += int(c)
+        assert np.array_equal(b.snapshot_bytes(), cur)
+    for t in range(30):
+        assert np.array_equal(got[t], want[t]), t
+    del out
+
+
 def test_flip_stream_first_turn_too_big(fixtures):
     """cap below the first turn's list: ERANGE, *n = what it needs, board untouched."""
     board = unpack_bits(fixtures["image_256"], 256)
