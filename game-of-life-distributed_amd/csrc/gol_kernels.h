@@ -133,9 +133,14 @@ struct FlipTurnArgs {
     unsigned *ctl;                  // [0] stop: set by a turn that overflows cap (stop_on_overflow),
                                     //     every later launch returns at once; [1] error (spin bound)
     int stop_on_overflow;
+    int dbg;                        // measurement only (option "flip_debug"): 1 no look-back, 2 no entries
+    int coresident;                 // 1: the whole grid is resident at once (host-checked): block order is
+                                    //    blockIdx and each block sums ALL its predecessors' aggregates;
+                                    // 0: virtual ids from `ticket` and a decoupled look-back
     unsigned long long *alive;      // nullable: += popcount of the new board
 };
 int64_t flip_turn_blocks(int64_t nwords);
 hipError_t launch_flip_turn(const FlipTurnArgs &a, hipStream_t s);
+int flip_turn_blocks_per_cu(bool contig);
 
 }  // namespace golk

@@ -1016,14 +1016,20 @@ template <bool CONTIG>
 __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
     if (a.ctl[0]) return;  // an earlier turn of the batch overflowed: the host rolls back to it
     __shared__ unsigned s_vid;
-    __shared__ unsigned long long s_wsum[4];
+    __shared__ unsigned long long s_wsum[4], s_part[4];
     __shared__ unsigned long long s_excl;
     __shared__ uint32_t s_alive[4];
     __shared__ alignas(16) unsigned char s_buf[kFtLdsBytes];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    if (tid == 0) s_vid = atomicAdd(a.ticket, 1u);
-    __syncthreads();
-    const unsigned vid = s_vid;
+    // Block order: blockIdx when every block is resident at once (no
+    // contended counter: 800 returning atomics on one word cost ~9 us);
+    // otherwise a ticket, so every predecessor is already running.
+    unsigned vid = blockIdx.x;
+    if (!a.coresident) {
+        if (tid == 0) s_vid = atomicAdd(a.ticket, 1u);
+        __syncthreads();
+        vid = s_vid;
+    }
     const unsigned Ww = (unsigned)a.Ww;
     const unsigned nwords = (unsigned)a.rows * Ww;  // host: < 2^32
     const unsigned base = vid * (unsigned)kFtWords;
@@ -1145,7 +1151,53 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
         }
     }
 
-    if (wid == 0) {
+    if (wid == 0 && (a.dbg & 1)) {  // measurement only: no look-back (entries overlap)
+        if (lane == 0) {
+            s_excl = a.run[0];
+            if (vid == gridDim.x - 1) a.run[1] = a.run[0];
+        }
+    } else if (a.coresident) {
+        // publish the aggregate, then every thread sums its share of ALL
+        // predecessors' aggregates (<= 4 words each at 5120^2): one round of
+        // loads instead of a chain of look-back windows
+        if (tid == 0)
+            __hip_atomic_store(&a.status[vid], ft_word(kFtAgg, a.epoch, T), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long ep = (unsigned long long)(a.epoch & 0x3FFFFFu);
+        unsigned long long part = 0;
+        for (unsigned j = (unsigned)tid; j < vid; j += kFtThreads) {
+            unsigned long long st;
+            int spins = 0;
+            for (;;) {
+                st = __hip_atomic_load(&a.status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((st >> 62) != 0 && ((st >> 40) & 0x3FFFFFull) == ep) break;
+                if (++spins > (1 << 22)) {  // a predecessor never ran: not co-resident after all
+                    atomicOr(&a.ctl[1], 1u);
+                    st = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            part += st & kFtValMask;
+        }
+        if ((a.dbg & 4) && tid == 0 && vid == 0) atomicOr(&a.ctl[1], 1u);  // test hook: the fallback
+        part = wave_sum_u64(part);
+        if (lane == 0) s_part[wid] = part;
+        __syncthreads();
+        if (tid == 0) {
+            const unsigned long long excl = a.run[0] + s_part[0] + s_part[1] + s_part[2] + s_part[3];
+            s_excl = excl;
+            if (vid == gridDim.x - 1) {
+                const unsigned long long end = excl + T;
+                a.run[1] = end;
+                if (a.stop_on_overflow && end > a.cap) atomicOr(&a.ctl[0], 1u);
+            }
+            if (a.alive) {
+                const uint32_t al = s_alive[0] + s_alive[1] + s_alive[2] + s_alive[3];
+                if (al) atomicAdd(a.alive, (unsigned long long)al);
+            }
+        }
+    } else if (wid == 0) {
         unsigned long long excl = 0;
         if (vid == 0) {
             excl = a.run[0];
@@ -1200,6 +1252,7 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
         }
     }
     __syncthreads();
+    if (a.dbg & 2) return;  // measurement only: no entries
     const unsigned long long bex = s_excl;
     const int esz = a.format == kFlipFormatXY ? 8 : 4;
     const bool staged = T <= (uint32_t)(kFtLdsBytes / esz);
@@ -1245,6 +1298,13 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
 }
 
 int64_t flip_turn_blocks(int64_t nwords) { return (nwords + kFtWords - 1) / kFtWords; }
+
+int flip_turn_blocks_per_cu(bool contig) {
+    int b = 0;
+    const hipError_t e = contig ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_flip_turn_kernel<true>, kFtThreads, 0)
+                                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_flip_turn_kernel<false>, kFtThreads, 0);
+    return e == hipSuccess ? b : 0;
+}
 
 hipError_t launch_flip_turn(const FlipTurnArgs &a, hipStream_t s) {
     const int64_t nb = flip_turn_blocks((int64_t)a.rows * a.Ww);

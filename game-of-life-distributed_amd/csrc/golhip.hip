@@ -155,6 +155,10 @@ struct golhip {
     void *d_ev = nullptr;                      // entries of a batch
     int64_t ev_cap_bytes = 0;
     unsigned flip_epoch = 0;
+    int flip_debug = 0;  // option "flip_debug" (measurement only: wrong lists)
+    bool ft_ticket = false;       // K5 block order by ticket (set after a co-residency failure)
+    uint64_t ft_est = 0;          // most entries of one turn in the last batch (launch sizing)
+    int64_t flip_fallbacks = 0;
     int64_t flip_launches = 0, flip_entries = 0;
     double flip_ms = 0;
     uint8_t *d_stage = nullptr;  // byte staging for load/snapshot
@@ -961,8 +965,16 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
     if (int rc = set_layout(h, 0)) return rc;
     void *direct = mapped_device_ptr(out, (size_t)dcap * esz);
     const int64_t nb = golk::flip_turn_blocks(nw);
+    const bool contig = h->Ww % 4 == 0;
+    const int bpc = std::min(golk::flip_turn_blocks_per_cu(contig), 4);
+    // every block resident at once (with a 10 % margin): block order = blockIdx
+    const bool coresident = !h->ft_ticket && bpc > 0 && nb * 10 <= (int64_t)h->cu_count * bpc * 9;
+    // launch the turns the buffer probably holds (the last batch's largest
+    // list); turns past an overflow would only return at once
+    int64_t nlaunch = nturns;
+    if (stop && h->ft_est > 0) nlaunch = std::min<int64_t>(nturns, (int64_t)(dcap / h->ft_est) + 1);
     if (int rc = ensure_dev(h, &h->d_ftstatus, &h->ftstatus_cap, nb, true)) return rc;
-    if (int rc = ensure_dev(h, &h->d_ftticket, &h->ftticket_cap, nturns)) return rc;
+    if (int rc = ensure_dev(h, &h->d_ftticket, &h->ftticket_cap, nlaunch)) return rc;
     int64_t ctl_cap = h->d_ftctl ? 2 : 0;
     if (int rc = ensure_dev(h, &h->d_ftctl, &ctl_cap, 2)) return rc;
     if (!direct) {
@@ -972,14 +984,20 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
         h->d_ev = p;
         h->ev_cap_bytes = bytes_cap;
     }
+    if (coresident) {  // keep the batch recoverable (see the error check below)
+        const size_t bytes = (size_t)h->local_words() * 4;
+        int64_t bcap = h->backup ? (int64_t)bytes : 0;
+        if (int rc = ensure_dev(h, &h->backup, &bcap, h->local_words())) return rc;
+        HIP_OR_FAIL(hipMemcpyAsync(h->backup, h->cur_rows(), bytes, hipMemcpyDeviceToDevice, h->stream));
+    }
     HIP_OR_FAIL(hipMemsetAsync(h->d_run, 0, sizeof(unsigned long long), h->stream));
-    HIP_OR_FAIL(hipMemsetAsync(h->d_ftticket, 0, (size_t)nturns * sizeof(unsigned), h->stream));
+    HIP_OR_FAIL(hipMemsetAsync(h->d_ftticket, 0, (size_t)nlaunch * sizeof(unsigned), h->stream));
     HIP_OR_FAIL(hipMemsetAsync(h->d_ftctl, 0, 2 * sizeof(unsigned), h->stream));
     golk::StepArgs sa = step_args(h, nullptr, halo);
-    for (int64_t t = 0; t < nturns; ++t) {
+    for (int64_t t = 0; t < nlaunch; ++t) {
         if (halo)
             if (int rc = exchange_rccl(h, 1, h->stream)) return rc;
-        const bool last = t == nturns - 1;
+        const bool last = t == nlaunch - 1;
         if (last) HIP_OR_FAIL(hipMemsetAsync(h->d_scalars, 0, sizeof(unsigned long long), h->stream));
         golk::FlipTurnArgs a{};
         a.src = h->buf[h->cur];
@@ -1001,6 +1019,8 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
         a.epoch = h->flip_epoch;
         a.ctl = h->d_ftctl;
         a.stop_on_overflow = stop ? 1 : 0;
+        a.dbg = h->flip_debug;
+        a.coresident = coresident ? 1 : 0;
         a.alive = last ? h->d_scalars : nullptr;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (h->flags & GOLHIP_FLAG_TIMING) {
@@ -1018,28 +1038,46 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
         h->cur ^= 1;
         h->turns += 1;
     }
-    HIP_OR_FAIL(hipMemcpyAsync(run.data(), h->d_run, run.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                               h->stream));
+    HIP_OR_FAIL(hipMemcpyAsync(run.data(), h->d_run, (size_t)(nlaunch + 1) * sizeof(unsigned long long),
+                               hipMemcpyDeviceToHost, h->stream));
     HIP_OR_FAIL(hipMemcpyAsync(ctl, h->d_ftctl, sizeof ctl, hipMemcpyDeviceToHost, h->stream));
     if (int rc = sync_stream(h)) return rc;
-    if (ctl[1]) return fail(GOLHIP_EHIP, "flip stream: look-back spin bound exceeded (board undefined)");
-    int64_t done = nturns;
+    if (ctl[1]) {
+        if (!coresident) return fail(GOLHIP_EHIP, "flip stream: look-back spin bound exceeded (board undefined)");
+        // a block waited on a predecessor that never ran (a co-tenant kernel
+        // held CUs): restore the batch's first board, re-run it in ticket order
+        HIP_OR_FAIL(hipMemcpyAsync(h->buf[c0] + (int64_t)kHalo * h->Ww, h->backup, (size_t)h->local_words() * 4,
+                                   hipMemcpyDeviceToDevice, h->stream));
+        h->cur = c0;
+        h->turns = t0;
+        h->alive_turn = -1;
+        h->ft_ticket = true;
+        h->flip_fallbacks++;
+        h->flip_debug &= ~4;
+        return flip_stream_locked(h, nturns, format, out, cap, counts, done_out, total_out, stop);
+    }
+    int64_t done = nlaunch;
     if (stop)
-        for (int64_t t = 0; t < nturns; ++t)
+        for (int64_t t = 0; t < nlaunch; ++t)
             if (run[t + 1] > dcap) {
                 done = t;
                 break;
             }
-    if (done < nturns) {  // turn `done` overflowed and the later launches returned at once
+    if (done < nlaunch) {  // turn `done` overflowed and the later launches returned at once
         h->cur = (c0 + (int)(done & 1)) & 1;
         h->turns = t0 + done;
         h->alive_turn = -1;
     } else {
         h->alive_turn = h->turns;
     }
-    for (int64_t t = 0; t < done; ++t) counts[t] = run[t + 1] - run[t];
-    const uint64_t total = done < nturns ? (done == 0 ? run[1] : run[done]) : run[nturns];
-    const uint64_t got = done == 0 && nturns > 0 && stop ? 0 : std::min<uint64_t>(run[done], cap);
+    uint64_t most_one = 0;
+    for (int64_t t = 0; t < done; ++t) {
+        counts[t] = run[t + 1] - run[t];
+        most_one = std::max<uint64_t>(most_one, counts[t]);
+    }
+    if (done > 0) h->ft_est = most_one;
+    const uint64_t total = done < nlaunch ? (done == 0 ? run[1] : run[done]) : run[nlaunch];
+    const uint64_t got = done == 0 && stop ? 0 : std::min<uint64_t>(run[done], cap);
     if (got > 0 && !direct) {
         HIP_OR_FAIL(hipMemcpyAsync(out, h->d_ev, got * esz, hipMemcpyDeviceToHost, h->stream));
         if (int rc = sync_stream(h)) return rc;
@@ -1236,6 +1274,13 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     if (!strcmp(key, "persist_timeout_us")) {
         if (value < 1 || value > 60000000) return fail(GOLHIP_EINVAL, "persist_timeout_us %lld", (long long)value);
         h->persist_timeout_ticks = value * 100;  // s_memrealtime: 100 MHz
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "flip_debug")) {
+        // 1 no look-back, 2 no entries (measurement only: wrong lists); 4 report a
+        // co-residency failure once (tests the ticket-order fallback; lists exact)
+        if (value < 0 || value > 7) return fail(GOLHIP_EINVAL, "flip_debug %lld", (long long)value);
+        h->flip_debug = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "force_halo")) {
@@ -1709,6 +1754,7 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     out->flip_launches = h->flip_launches;
     out->flip_kernel_ms = h->flip_ms;
     out->flip_entries = h->flip_entries;
+    out->flip_fallbacks = h->flip_fallbacks;
     out->cell_updates = (int64_t)h->W * h->rows * (h->step_turns + h->persist_turns + h->flip_launches);
     out->alg_bytes = out->cell_updates / 4;
     out->halo_bytes = h->halo_bytes;

@@ -51,6 +51,7 @@ class Perf(ctypes.Structure):
         ("flip_launches", ctypes.c_int64),
         ("flip_entries", ctypes.c_int64),
         ("flip_kernel_ms", ctypes.c_double),
+        ("flip_fallbacks", ctypes.c_int64),
     ]
 
     def as_dict(self) -> dict:

@@ -76,6 +76,8 @@ typedef struct golhip_perf {
     int64_t flip_launches;    /* fused turn + flip-list kernels (one turn each)  */
     int64_t flip_entries;     /* flip-list entries copied to the caller          */
     double flip_kernel_ms;    /* their summed device time (GOLHIP_FLAG_TIMING)   */
+    int64_t flip_fallbacks;   /* flip batches re-run in ticket order (a block waited on a
+                                 predecessor that was not resident)                */
 } golhip_perf_t;
 
 /* ---- library ---------------------------------------------------------- */

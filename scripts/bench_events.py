@@ -39,6 +39,22 @@ HBM_PEAK = 8.0e12
 out = {"workload": "configs[4]: 5120^2 random 25%, seed 0x5EED0005, turns 2065..2264", "board": [N, N]}
 
 
+# the host link itself: one 64 MiB device -> host copy, pageable vs page-locked
+# (torch first: its HIP runtime must initialise before libgolhip's does)
+import torch
+src = torch.empty(16 << 20, dtype=torch.int32, device="cuda")
+for label, dst in (("pageable", torch.empty(16 << 20, dtype=torch.int32)),
+                   ("pinned", torch.empty(16 << 20, dtype=torch.int32, pin_memory=True))):
+    dst.copy_(src)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        dst.copy_(src)
+    torch.cuda.synchronize()
+    out[f"d2h_{label}_GBps"] = 5 * (64 << 20) / (time.perf_counter() - t0) / 1e9
+
+
+
 def reset(b):
     b.fill_random(SEED)
     b.step(64)
@@ -90,8 +106,8 @@ with golhip.Board(N, N, timing=True) as b:
     for name, fmt, esz, pinned in legs:
         reset(b)
         cap = 32 << 20
-        shape, dt = ((cap, 2), np.int32) if esz == 8 else ((cap,), np.uint32)
-        buf = golhip.host_array(shape, dt) if pinned else np.empty(shape, dtype=dt)
+        shape, dty = ((cap, 2), np.int32) if esz == 8 else ((cap,), np.uint32)
+        buf = golhip.host_array(shape, dty) if pinned else np.empty(shape, dtype=dty)
         buf.fill(0)
         b.perf_reset()
         done, flips_s, calls = 0, 0, 0
@@ -112,19 +128,6 @@ with golhip.Board(N, N, timing=True) as b:
                      "kernel_GBps": alg / (kus * 1e-6) / 1e9 if kus > 0 else None,
                      "kernel_hbm_frac": alg / (kus * 1e-6) / HBM_PEAK if kus > 0 else None,
                      "copy_and_host_us_per_turn": (dt / TURNS) * 1e6 - kus}
-
-    # the host link itself: one 64 MiB device -> host copy, pageable vs page-locked
-    import torch
-    src = torch.empty(16 << 20, dtype=torch.int32, device="cuda")
-    for label, dst in (("pageable", torch.empty(16 << 20, dtype=torch.int32)),
-                       ("pinned", torch.empty(16 << 20, dtype=torch.int32, pin_memory=True))):
-        dst.copy_(src)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(5):
-            dst.copy_(src)
-        torch.cuda.synchronize()
-        out[f"d2h_{label}_GBps"] = 5 * (64 << 20) / (time.perf_counter() - t0) / 1e9
 
     t0 = time.perf_counter()
     snap = b.snapshot_bytes()

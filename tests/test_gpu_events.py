@@ -176,6 +176,31 @@ def test_flip_stream_dense_blocks(coracle):
         assert int(counts[0]) > 16384
 
 
+@pytest.mark.parametrize("fmt", [0, 1])
+def test_flip_stream_coresidency_fallback(fixtures, coracle, fmt):
+    """A batch whose blockIdx-ordered prefix sums report a missing
+    predecessor (forced by the test hook flip_debug 4) is restored and re-run
+    in ticket order with the decoupled look-back: the lists stay exact."""
+    board = unpack_bits(fixtures["image_512"], 512)
+    cur, want = board, []
+    for _ in range(12):
+        nxt = step_np(cur)
+        want.append(flips_np(cur, nxt))
+        cur = nxt
+    with golhip.Board(512, 512) as b:
+        b.load_bytes(board)
+        b.set_option("flip_debug", 4)
+        ent, counts, done = b.flip_stream(12, cap=12 * 512 * 512, fmt=fmt)
+        assert done == 12 and b.perf()["flip_fallbacks"] == 1
+        xy = ent if fmt == 0 else idx_to_xy(ent, 512)
+        assert np.array_equal(xy, np.concatenate(want))
+        assert np.array_equal(b.snapshot_bytes(), cur)
+        ent, counts, done = b.flip_stream(5, cap=5 * 512 * 512, fmt=fmt)  # ticket order from now on
+        xy = ent if fmt == 0 else idx_to_xy(ent, 512)
+        assert np.array_equal(xy, np.concatenate([flips_np(coracle.run(cur, i), coracle.run(cur, i + 1))
+                                                  for i in range(5)]))
+
+
 def test_step_flips_truncates_and_advances(fixtures):
     """golhip_step_flips keeps its contract on the fused kernel: lists cut at
     cap, ERANGE with the total, the board advanced every turn."""
