@@ -1151,8 +1151,8 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
         }
     }
 
-    if (wid == 0 && (a.dbg & 1)) {  // measurement only: no look-back (entries overlap)
-        if (lane == 0) {
+    if (a.dbg & 1) {  // measurement only: no look-back (entries overlap)
+        if (tid == 0) {
             s_excl = a.run[0];
             if (vid == gridDim.x - 1) a.run[1] = a.run[0];
         }
@@ -1286,15 +1286,22 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
     if (!staged) return;
     __syncthreads();
     const unsigned long long lim = bex >= a.cap ? 0ull : (a.cap - bex < T ? a.cap - bex : (unsigned long long)T);
-    if (a.format == kFlipFormatXY) {
-        const unsigned long long *sb = reinterpret_cast<const unsigned long long *>(s_buf);
-        unsigned long long *d = reinterpret_cast<unsigned long long *>(a.out) + bex;
-        for (unsigned long long e = tid; e < lim; e += kFtThreads) d[e] = sb[e];
-    } else {
-        const uint32_t *sb = reinterpret_cast<const uint32_t *>(s_buf);
-        uint32_t *d = reinterpret_cast<uint32_t *>(a.out) + bex;
-        for (unsigned long long e = tid; e < lim; e += kFtThreads) d[e] = sb[e];
+    // copy out in 16-byte stores (4 indices or 2 pairs a lane: wider writes
+    // when `out` is host memory across PCIe), with 4-byte-word heads and tails
+    // up to the 16-byte boundaries of the destination
+    const unsigned wpe = (unsigned)esz / 4;                  // 32-bit words per entry
+    uint32_t *d = reinterpret_cast<uint32_t *>(a.out) + bex * wpe;
+    const uint32_t *sb = reinterpret_cast<const uint32_t *>(s_buf);
+    const unsigned long long nw = lim * wpe;                 // words to copy
+    const unsigned long long head = min(nw, (unsigned long long)((4u - (unsigned)(((uintptr_t)d >> 2) & 3u)) & 3u));
+    const unsigned long long nq = (nw - head) / 4;           // whole 16-byte groups
+    if ((unsigned long long)tid < head) d[tid] = sb[tid];
+    for (unsigned long long q = tid; q < nq; q += kFtThreads) {
+        const unsigned long long w = head + 4 * q;
+        *reinterpret_cast<uint4 *>(d + w) = make_uint4(sb[w], sb[w + 1], sb[w + 2], sb[w + 3]);
     }
+    const unsigned long long t0 = head + 4 * nq;
+    if (t0 + (unsigned long long)tid < nw) d[t0 + tid] = sb[t0 + tid];
 }
 
 int64_t flip_turn_blocks(int64_t nwords) { return (nwords + kFtWords - 1) / kFtWords; }
