@@ -41,7 +41,7 @@ std::string Event::String() const {
 // ---------------------------------------------------------------- PGM io
 // readPgmImage (io.go:90-126): whitespace-separated fields P5, W, H, 255;
 // the raster follows the single whitespace byte after maxval.
-std::vector<uint8_t> ReadPgm(const std::string &path, int width, int height) {
+std::vector<uint8_t> ReadPgm(const std::string &path, int64_t width, int64_t height) {
     std::ifstream f(path, std::ios::binary);
     if (!f) throw std::runtime_error("open " + path + ": no such file or directory");
     std::vector<uint8_t> data((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
@@ -54,16 +54,16 @@ std::vector<uint8_t> ReadPgm(const std::string &path, int width, int height) {
     }
     ++pos;
     if (fields[0] != "P5") throw std::runtime_error("Not a pgm file");
-    if (std::atoi(fields[1].c_str()) != width) throw std::runtime_error("Incorrect width");
-    if (std::atoi(fields[2].c_str()) != height) throw std::runtime_error("Incorrect height");
-    if (std::atoi(fields[3].c_str()) != 255) throw std::runtime_error("Incorrect maxval/bit depth");
+    if (std::atoll(fields[1].c_str()) != width) throw std::runtime_error("Incorrect width");
+    if (std::atoll(fields[2].c_str()) != height) throw std::runtime_error("Incorrect height");
+    if (std::atoll(fields[3].c_str()) != 255) throw std::runtime_error("Incorrect maxval/bit depth");
     const size_t n = (size_t)width * height;
     if (data.size() < pos + n) throw std::runtime_error("short raster in " + path);
     return std::vector<uint8_t>(data.begin() + pos, data.begin() + pos + n);
 }
 
 // writePgmImage (io.go:42-87): "P5\n" W " " H "\n" "255\n" + raster, one bulk write.
-void WritePgm(const std::string &path, int width, int height, const uint8_t *raster) {
+void WritePgm(const std::string &path, int64_t width, int64_t height, const uint8_t *raster) {
     std::ofstream f(path, std::ios::binary | std::ios::trunc);
     if (!f) throw std::runtime_error("create " + path + " failed");
     f << "P5\n" << width << " " << height << "\n" << 255 << "\n";
@@ -80,8 +80,28 @@ void check(int rc) {
 
 struct Board {
     golhip_t h = nullptr;
-    Board(int w, int hgt, int dev) { check(golhip_create(w, hgt, dev, 0, &h)); }
+    Board(int64_t w, int64_t hgt, int dev) { check(golhip_create((int32_t)w, (int32_t)hgt, dev, 0, &h)); }
     ~Board() { golhip_destroy(h); }
+};
+
+// Page-locked flip-list buffer the engine's flip kernel writes directly
+// (golhip_host_alloc): 4-byte cell indices y * W + x.
+struct FlipBuffer {
+    uint32_t *p = nullptr;
+    uint64_t cap = 0;  // entries
+    void grow(uint64_t n) {
+        if (n <= cap) return;
+        if (p) golhip_host_free(p);
+        p = nullptr;
+        cap = 0;
+        void *q = nullptr;
+        check(golhip_host_alloc(n * sizeof(uint32_t), &q));
+        p = static_cast<uint32_t *>(q);
+        cap = n;
+    }
+    ~FlipBuffer() {
+        if (p) golhip_host_free(p);
+    }
 };
 
 std::vector<util::Cell> cells_of(golhip_t h, int (*fn)(golhip_t, int32_t *, uint64_t, uint64_t *), bool transpose) {
@@ -101,8 +121,8 @@ std::vector<util::Cell> cells_of(golhip_t h, int (*fn)(golhip_t, int32_t *, uint
 }  // namespace
 
 void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOptions &opt) {
-    const int W = p.ImageWidth, H = p.ImageHeight;
-    if (W <= 0 || H <= 0 || p.Turns < 0) throw std::runtime_error("bad Params");
+    const int64_t W = p.ImageWidth, H = p.ImageHeight;
+    if (W <= 0 || H <= 0 || W > INT32_MAX || H > INT32_MAX || p.Turns < 0) throw std::runtime_error("bad Params");
     const std::string name = std::to_string(W) + "x" + std::to_string(H);
     const bool quirks = opt.ref_quirks;
 
@@ -117,13 +137,13 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
     auto send = [&](Event e) {
         if (events) events->send(std::move(e));
     };
-    auto write_snapshot = [&](int turn, bool transposed) -> std::string {
+    auto write_snapshot = [&](int64_t turn, bool transposed) -> std::string {
         std::vector<uint8_t> snap((size_t)W * H);
         check(golhip_snapshot_bytes(board.h, snap.data()));
         if (transposed) {  // the reference streams (*world)[x][y] for s/q (distributor.go:234-238)
             std::vector<uint8_t> t((size_t)W * H);
-            for (int y = 0; y < H; ++y)
-                for (int x = 0; x < W; ++x) t[(size_t)x * H + y] = snap[(size_t)y * W + x];
+            for (int64_t y = 0; y < H; ++y)
+                for (int64_t x = 0; x < W; ++x) t[(size_t)x * H + y] = snap[(size_t)y * W + x];
             snap.swap(t);
         }
         const std::string fname = name + "x" + std::to_string(turn);
@@ -146,7 +166,7 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
 
     std::mutex mu;                 // the reference's `mu`: held by the turn loop and by pause
     std::atomic<int> waiters{0};   // helpers queued for `mu` (std::mutex is not fair)
-    std::atomic<int> turn{0};      // completed turns
+    std::atomic<int64_t> turn{0};  // completed turns
     // helpers take `mu` through this, so the turn loop can step aside for them
     auto lock_mu = [&]() {
         ++waiters;
@@ -187,8 +207,8 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
             }
             Event e;
             e.kind = EventKind::AliveCellsCount;
-            e.CompletedTurns = (int)at;
-            e.CellsCount = (int)n;
+            e.CompletedTurns = at;
+            e.CellsCount = (int64_t)n;
             send(e);
         }
     }));
@@ -206,7 +226,7 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
             }
             if (k == U's' || k == U'q') {
                 std::string fname;
-                int t;
+                int64_t t;
                 {
                     auto g = lock_mu();  // snapshot at a turn boundary
                     t = turn.load();
@@ -223,7 +243,7 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
                 }
             } else if (k == U'p') {
                 auto g = lock_mu();
-                std::printf("%d\n", turn.load());
+                std::printf("%lld\n", (long long)turn.load());
                 std::fflush(stdout);
                 if (!quirks) {
                     Event e;
@@ -264,35 +284,64 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
     };
 
     try {
-        const bool per_turn = opt.cell_events || opt.turn_events;
-        int t = 0;
+        // The turn loop in batches (distributor.go:93-173): each engine call
+        // runs up to `batch` turns; with cell events it is the fused flip
+        // stream (golhip_flip_stream: every turn's CellFlipped list, written
+        // by the device straight into a page-locked buffer as cell indices),
+        // otherwise fused step launches.  `mu` is held only for the call, so
+        // the ticker, s/q snapshots and p (which takes `mu`, as the
+        // reference's pause does) act between batches, at a turn boundary.
+        const int64_t batch = opt.batch_turns > 0 ? opt.batch_turns : (opt.cell_events ? 64 : 256);
+        FlipBuffer fb;
+        if (opt.cell_events) fb.grow((uint64_t)std::min<int64_t>(W * H * std::min<int64_t>(batch, 4), 64ll << 20));
+        std::vector<uint64_t> counts((size_t)batch);
+        int64_t t = 0;
         while (t < p.Turns && !quit.load()) {
-            // per-turn events need one turn per step; otherwise fuse up to
-            // 256 turns per call (bounded key/pause latency)
-            const int n = per_turn ? 1 : std::min(256, p.Turns - t);
-            std::vector<util::Cell> flips;
+            const int64_t want = std::min<int64_t>(batch, p.Turns - t);
+            int64_t done = want;
+            uint64_t n = 0;
             {
                 std::lock_guard<std::mutex> g(mu);
-                check(golhip_step(board.h, n, opt.cell_events ? 1 : 0));
-                if (opt.cell_events) flips = cells_of(board.h, golhip_flips, quirks);
-                else check(golhip_sync(board.h));
-                t += n;
+                if (opt.cell_events) {
+                    int rc = golhip_flip_stream(board.h, want, GOLHIP_FLIPS_INDEX, fb.p, fb.cap, counts.data(), &done,
+                                                &n);
+                    if (rc == GOLHIP_ERANGE) {  // one turn needs more than the buffer: grow, nothing advanced
+                        fb.grow(n);
+                        rc = golhip_flip_stream(board.h, want, GOLHIP_FLIPS_INDEX, fb.p, fb.cap, counts.data(), &done,
+                                                &n);
+                    }
+                    check(rc);
+                } else {
+                    check(golhip_step(board.h, want, 0));
+                    check(golhip_sync(board.h));
+                }
+                t += done;
                 turn = t;
             }
-            // let a queued ticker / key handler take `mu` before the next turn
+            // let a queued ticker / key handler take `mu` before the next batch
             while (waiters.load() > 0) std::this_thread::sleep_for(std::chrono::microseconds(20));
-            for (const util::Cell &c : flips) {  // initializeAliveCells (:212-220)
-                Event e;
-                e.kind = EventKind::CellFlipped;
-                e.CompletedTurns = quirks ? t - 1 : t;
-                e.Cell = c;
-                send(e);
-            }
-            if (opt.turn_events) {  // :113 / :171 (the reference sends the 0-based turn)
-                Event e;
-                e.kind = EventKind::TurnComplete;
-                e.CompletedTurns = quirks ? t - 1 : t;
-                send(e);
+            const int64_t t0 = t - done;
+            uint64_t off = 0;
+            for (int64_t i = 0; i < done; ++i) {
+                const int64_t completed = t0 + i + 1;  // quirks: the reference's 0-based turn (:113, :171, :216)
+                if (opt.cell_events) {
+                    for (uint64_t e = off; e < off + counts[(size_t)i]; ++e) {  // initializeAliveCells (:212-220)
+                        const uint64_t idx = fb.p[e];
+                        Event ev;
+                        ev.kind = EventKind::CellFlipped;
+                        ev.CompletedTurns = quirks ? completed - 1 : completed;
+                        ev.Cell.X = quirks ? (int64_t)(idx / W) : (int64_t)(idx % W);
+                        ev.Cell.Y = quirks ? (int64_t)(idx % W) : (int64_t)(idx / W);
+                        send(ev);
+                    }
+                    off += counts[(size_t)i];
+                }
+                if (opt.turn_events) {
+                    Event ev;
+                    ev.kind = EventKind::TurnComplete;
+                    ev.CompletedTurns = quirks ? completed - 1 : completed;
+                    send(ev);
+                }
             }
         }
         stop_helpers();
@@ -362,7 +411,7 @@ extern "C" {
 
 const char *golrun_last_error(void) { return g_run_err.c_str(); }
 
-int golrun_start(int32_t turns, int32_t threads, int32_t width, int32_t height, const char *root, int32_t device,
+int golrun_start(int64_t turns, int64_t threads, int64_t width, int64_t height, const char *root, int32_t device,
                  uint32_t flags, int32_t events_cap, int32_t ticker_ms, golrun_t *out) {
     if (!out || !root || events_cap < 0) return run_fail("bad arguments");
     gol::Params p;
@@ -415,7 +464,19 @@ int golrun_next_event(golrun_t r, golrun_event_t *ev, int32_t timeout_ms) {
     return 1;
 }
 
-int golrun_event_cells(golrun_t r, int32_t *xy, uint64_t cap) {
+int golrun_event_string(const golrun_event_t *ev, char *out, uint64_t cap) {
+    if (!ev || !out || cap == 0) return run_fail("bad arguments");
+    gol::Event e;
+    e.kind = (gol::EventKind)ev->kind;
+    e.CompletedTurns = ev->completed_turns;
+    e.CellsCount = ev->cells_count;
+    e.NewState = (gol::State)ev->new_state;
+    e.Filename = std::string(ev->filename, strnlen(ev->filename, sizeof ev->filename));
+    std::snprintf(out, cap, "%s", e.String().c_str());
+    return GOLHIP_OK;
+}
+
+int golrun_event_cells(golrun_t r, int64_t *xy, uint64_t cap) {
     if (!r) return run_fail("bad arguments");
     const auto &a = r->current.Alive;
     if (cap < a.size() || (!xy && !a.empty())) return run_fail("buffer too small");

@@ -23,9 +23,12 @@
 #include <string>
 #include <vector>
 
+// Go's int is 64-bit (gol.go:4-9, event.go:19-68, util/cell.go:4-6): every
+// integer of the mirror's API is int64_t, so a 262144^2 board's ~6.5e9 alive
+// cells and the CLI's 10^10 default turns (main.go:37-41) pass through intact.
 namespace util {
 struct Cell {
-    int X = 0, Y = 0;
+    int64_t X = 0, Y = 0;
     bool operator==(const Cell &o) const { return X == o.X && Y == o.Y; }
 };
 }  // namespace util
@@ -33,10 +36,10 @@ struct Cell {
 namespace gol {
 
 struct Params {
-    int Turns = 0;
-    int Threads = 1;  // accepted for API parity; the GPU engine ignores it
-    int ImageWidth = 0;
-    int ImageHeight = 0;
+    int64_t Turns = 0;
+    int64_t Threads = 1;  // accepted for API parity; the GPU engine ignores it
+    int64_t ImageWidth = 0;
+    int64_t ImageHeight = 0;
 };
 
 enum class State { Paused = 0, Executing = 1, Quitting = 2 };
@@ -54,14 +57,14 @@ enum class EventKind {
 // One tagged struct for the six event types; unused fields stay default.
 struct Event {
     EventKind kind = EventKind::TurnComplete;
-    int CompletedTurns = 0;
-    int CellsCount = 0;               // AliveCellsCount
+    int64_t CompletedTurns = 0;
+    int64_t CellsCount = 0;           // AliveCellsCount
     std::string Filename;             // ImageOutputComplete
     State NewState = State::Executing;  // StateChange
     util::Cell Cell;                  // CellFlipped
     std::vector<util::Cell> Alive;    // FinalTurnComplete
     std::string String() const;       // event.go:72-131 text
-    int GetCompletedTurns() const { return CompletedTurns; }
+    int64_t GetCompletedTurns() const { return CompletedTurns; }
 };
 
 // Go channel: capacity 0 is a rendezvous (send returns once received).
@@ -130,11 +133,13 @@ struct RunOptions {
     bool cell_events = true;      // per-cell CellFlipped events (the SDL feed)
     bool turn_events = true;      // TurnComplete every turn
     double ticker_seconds = 2.0;  // AliveCellsCount period (distributor.go:285)
+    int64_t batch_turns = 0;      // turns per engine call (0: 64 with cell events, 256 without);
+                                  // keys, pause and the ticker are served between calls
 };
 
 // The PGM goroutine's file formats (io.go:42-126).
-std::vector<uint8_t> ReadPgm(const std::string &path, int width, int height);
-void WritePgm(const std::string &path, int width, int height, const uint8_t *raster);
+std::vector<uint8_t> ReadPgm(const std::string &path, int64_t width, int64_t height);
+void WritePgm(const std::string &path, int64_t width, int64_t height, const uint8_t *raster);
 
 // gol.Run: blocks until the run finishes (events closed) or `q` stops it.
 // Throws std::runtime_error where the reference panics / log.Fatal-s.

@@ -61,11 +61,11 @@ int main(int argc, char **argv) {
             return argv[++i];
         };
         if (key == "-t") {
-            params.Threads = (int)parse_int(value(), "t");
+            params.Threads = parse_int(value(), "t");
         } else if (key == "-w") {
-            params.ImageWidth = (int)parse_int(value(), "w");
+            params.ImageWidth = parse_int(value(), "w");
         } else if (key == "-h") {
-            params.ImageHeight = (int)parse_int(value(), "h");
+            params.ImageHeight = parse_int(value(), "h");
         } else if (key == "-turns") {
             turns = parse_int(value(), "turns");
         } else if (key == "-noVis") {
@@ -78,11 +78,10 @@ int main(int argc, char **argv) {
             usage(("flag provided but not defined: " + key).c_str());
         }
     }
-    // Params.Turns is a Go int (64-bit); the mirror counts in int, so the
-    // reference's "forever" default is clamped to INT_MAX turns.
-    params.Turns = (int)std::min<long long>(turns, INT_MAX);
+    params.Turns = turns;  // a Go int (64-bit): the reference's 10^10 default passes through
 
-    std::printf("Threads: %d\nWidth: %d\nHeight: %d\n", params.Threads, params.ImageWidth, params.ImageHeight);
+    std::printf("Threads: %lld\nWidth: %lld\nHeight: %lld\n", (long long)params.Threads, (long long)params.ImageWidth,
+                (long long)params.ImageHeight);
     std::fflush(stdout);
     if (!no_vis) std::fprintf(stderr, "golrun: no SDL window in this build; running headless (keys s/q/p/k on stdin)\n");
 

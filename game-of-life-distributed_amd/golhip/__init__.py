@@ -410,8 +410,8 @@ EVENT_NAMES = ["AliveCellsCount", "ImageOutputComplete", "StateChange", "CellFli
 
 class RunEvent(ctypes.Structure):
     _fields_ = [
-        ("kind", ctypes.c_int32), ("completed_turns", ctypes.c_int32), ("cells_count", ctypes.c_int32),
-        ("new_state", ctypes.c_int32), ("cell_x", ctypes.c_int32), ("cell_y", ctypes.c_int32),
+        ("kind", ctypes.c_int32), ("new_state", ctypes.c_int32), ("completed_turns", ctypes.c_int64),
+        ("cells_count", ctypes.c_int64), ("cell_x", ctypes.c_int64), ("cell_y", ctypes.c_int64),
         ("alive_len", ctypes.c_int64), ("filename", ctypes.c_char * 256), ("text", ctypes.c_char * 288),
     ]
 
@@ -428,10 +428,11 @@ def load_host(path: str = HOST_LIB_PATH) -> ctypes.CDLL:
         raise FileNotFoundError(f"{path} not built")
     lib = ctypes.CDLL(path)
     P = ctypes.POINTER
-    i32, u32, u64 = ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64
+    i32, i64, u32, u64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32, ctypes.c_uint64
     sig = {
         "golrun_last_error": ([], ctypes.c_char_p),
-        "golrun_start": ([i32, i32, i32, i32, ctypes.c_char_p, i32, u32, i32, i32, P(ctypes.c_void_p)], ctypes.c_int),
+        "golrun_start": ([i64, i64, i64, i64, ctypes.c_char_p, i32, u32, i32, i32, P(ctypes.c_void_p)], ctypes.c_int),
+        "golrun_event_string": ([P(RunEvent), ctypes.c_char_p, u64], ctypes.c_int),
         "golrun_next_event": ([ctypes.c_void_p, P(RunEvent), i32], ctypes.c_int),
         "golrun_event_cells": ([ctypes.c_void_p, ctypes.c_void_p, u64], ctypes.c_int),
         "golrun_send_key": ([ctypes.c_void_p, u32], ctypes.c_int),
@@ -486,7 +487,7 @@ class Run:
         elif e.kind == CELL_FLIPPED:
             ev["Cell"] = (e.cell_x, e.cell_y)
         elif e.kind == FINAL_TURN_COMPLETE:
-            xy = np.zeros((max(e.alive_len, 1), 2), dtype=np.int32)
+            xy = np.zeros((max(e.alive_len, 1), 2), dtype=np.int64)
             rc = lib.golrun_event_cells(self._h, _ptr(xy), e.alive_len)
             if rc != 0:
                 raise GolHipError(rc, lib.golrun_last_error().decode())

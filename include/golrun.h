@@ -39,12 +39,13 @@ extern "C" {
 typedef struct golrun golrun;
 typedef golrun *golrun_t;
 
+/* Go's int is 64-bit (event.go:19-68, util/cell.go:4-6): so are these. */
 typedef struct golrun_event {
     int32_t kind;
-    int32_t completed_turns;   /* GetCompletedTurns()                      */
-    int32_t cells_count;       /* AliveCellsCount.CellsCount               */
     int32_t new_state;         /* StateChange.NewState                     */
-    int32_t cell_x, cell_y;    /* CellFlipped.Cell                         */
+    int64_t completed_turns;   /* GetCompletedTurns()                      */
+    int64_t cells_count;       /* AliveCellsCount.CellsCount               */
+    int64_t cell_x, cell_y;    /* CellFlipped.Cell                         */
     int64_t alive_len;         /* len(FinalTurnComplete.Alive)             */
     char filename[256];        /* ImageOutputComplete.Filename             */
     char text[288];            /* String()                                 */
@@ -54,12 +55,14 @@ const char *golrun_last_error(void);
 /* root: directory with images/<W>x<H>.pgm; output goes to root/out/.
  * events_cap: 0 = unbuffered (as in the tests), 1000 as in main.go:53.
  * ticker_ms: AliveCellsCount period (<= 0: 2000 as distributor.go:285). */
-int golrun_start(int32_t turns, int32_t threads, int32_t width, int32_t height, const char *root, int32_t device,
+int golrun_start(int64_t turns, int64_t threads, int64_t width, int64_t height, const char *root, int32_t device,
                  uint32_t flags, int32_t events_cap, int32_t ticker_ms, golrun_t *out);
 /* 1 = event received, 0 = channel closed and drained, 2 = timeout (timeout_ms >= 0). */
 int golrun_next_event(golrun_t r, golrun_event_t *ev, int32_t timeout_ms);
 /* Alive list of the last FinalTurnComplete received (alive_len pairs X, Y). */
-int golrun_event_cells(golrun_t r, int32_t *xy, uint64_t cap);
+int golrun_event_cells(golrun_t r, int64_t *xy, uint64_t cap);
+/* String() of an event's fields (event.go:72-131); needs no run or device. */
+int golrun_event_string(const golrun_event_t *ev, char *out, uint64_t cap);
 int golrun_send_key(golrun_t r, uint32_t key);
 /* Drains unread events, joins the run; 0 or the panic message in err. */
 int golrun_wait(golrun_t r, char *err, uint64_t err_cap);
