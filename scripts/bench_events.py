@@ -10,8 +10,9 @@ Prints one JSON object with:
   stream_index    turns per call as a 32 M-entry caller buffer holds, pairs
   (_pinned)       (8 B) / cell indices (4 B), in a pageable numpy buffer
                   (device list + one copy) or a golhip_host_alloc buffer
-                  (the kernel writes the host memory): turns/s, flips/s, the K5
-                  kernel alone (HIP events): us per turn, algorithmic bytes
+                  (the kernel writes the host memory): turns/s, flips/s (no
+                  HIP timing events), the K5 kernel alone (HIP events on a
+                  second run): us per launch, algorithmic bytes
                   per turn (board read + board written + entries) and their
                   rate against the 8 TB/s HBM peak
   snapshot_s      one 's' snapshot (golhip_snapshot_bytes + PGM write), ms
@@ -103,31 +104,39 @@ with golhip.Board(N, N, timing=True) as b:
 
     legs = (("stream_xy", golhip.FLIPS_XY, 8, False), ("stream_index", golhip.FLIPS_INDEX, 4, False),
             ("stream_xy_pinned", golhip.FLIPS_XY, 8, True), ("stream_index_pinned", golhip.FLIPS_INDEX, 4, True))
+    # turns/s on a board without per-launch HIP timing events (they cost the
+    # pinned legs ~2x in host time), the K5 kernel time on the timed board
+    plain = golhip.Board(N, N)
     for name, fmt, esz, pinned in legs:
-        reset(b)
         cap = 32 << 20
         shape, dty = ((cap, 2), np.int32) if esz == 8 else ((cap,), np.uint32)
         buf = golhip.host_array(shape, dty) if pinned else np.empty(shape, dtype=dty)
         buf.fill(0)
-        b.perf_reset()
-        done, flips_s, calls = 0, 0, 0
-        t0 = time.perf_counter()
-        while done < TURNS:
-            ent, counts, k = b.flip_stream(TURNS - done, cap=cap, fmt=fmt, out=buf)
-            done += k
-            flips_s += len(ent)
-            calls += 1
-        dt = time.perf_counter() - t0
-        p = b.perf()
-        kus = p["flip_kernel_ms"] * 1e3 / max(1, p["flip_launches"])
-        alg = 2 * N * N / 8 + flips_s / TURNS * esz  # board in + board out + entries, per turn
-        out[name] = {"turns": TURNS, "calls": calls, "seconds": dt, "turns_per_s": TURNS / dt, "flips": flips_s,
-                     "flips_per_s": flips_s / dt, "gcups": N * N * TURNS / dt / 1e9,
-                     "same_flips_as_events_on": flips_s == flips_total,
-                     "kernel_us_per_turn": kus, "alg_bytes_per_turn": alg,
-                     "kernel_GBps": alg / (kus * 1e-6) / 1e9 if kus > 0 else None,
-                     "kernel_hbm_frac": alg / (kus * 1e-6) / HBM_PEAK if kus > 0 else None,
-                     "copy_and_host_us_per_turn": (dt / TURNS) * 1e6 - kus}
+        rec = {"turns": TURNS}
+        for bb, timed in ((plain, False), (b, True)):
+            reset(bb)
+            bb.perf_reset()
+            done, flips_s, calls = 0, 0, 0
+            t0 = time.perf_counter()
+            while done < TURNS:
+                ent, counts, k = bb.flip_stream(TURNS - done, cap=cap, fmt=fmt, out=buf)
+                done += k
+                flips_s += len(ent)
+                calls += 1
+            dt = time.perf_counter() - t0
+            if not timed:
+                rec.update({"calls": calls, "seconds": dt, "turns_per_s": TURNS / dt, "flips": flips_s,
+                            "flips_per_s": flips_s / dt, "gcups": N * N * TURNS / dt / 1e9,
+                            "same_flips_as_events_on": flips_s == flips_total})
+            else:
+                p = bb.perf()
+                kus = p["flip_kernel_ms"] * 1e3 / max(1, p["flip_launches"])
+                alg = 2 * N * N / 8 + flips_s / TURNS * esz  # board in + board out + entries, per turn
+                rec.update({"kernel_us_per_launch": kus, "launches": p["flip_launches"], "alg_bytes_per_turn": alg,
+                            "kernel_GBps": alg / (kus * 1e-6) / 1e9 if kus > 0 else None,
+                            "kernel_hbm_frac": alg / (kus * 1e-6) / HBM_PEAK if kus > 0 else None})
+        out[name] = rec
+    plain.close()
 
     t0 = time.perf_counter()
     snap = b.snapshot_bytes()
