@@ -203,10 +203,11 @@ int golhip_flips(golhip_t h, int32_t *xy, uint64_t cap, uint64_t *n);
  * initializeAliveCells :212-220): advance nturns turns one at a time and
  * return every turn's flip list, concatenated in turn order (row-major within
  * a turn, same pairs as golhip_flips), with counts[t] = flips of turn t.
- * One host round trip for the whole batch.  The board always advances
- * nturns; if the lists exceed cap pairs, xy holds the first cap, *n the
- * total and the call returns GOLHIP_ERANGE.  Reserves cap pairs on the
- * device. */
+ * One host round trip for the whole batch, on the fused turn + list kernel
+ * (K5).  The board always advances nturns; if the lists exceed cap pairs, xy
+ * holds the first cap, *n the total and the call returns GOLHIP_ERANGE.
+ * Reserves min(cap, nturns x cells) pairs on the device.  Works in a
+ * multi-rank ring; golhip_flip_stream (below) never drops a flip. */
 int golhip_step_flips(golhip_t h, int64_t nturns, int32_t *xy, uint64_t cap, uint64_t *counts, uint64_t *n);
 /* The CellFlipped stream without loss: advance UP TO nturns turns, one at a
  * time, each fused with its flip list on the device (initializeAliveCells,
