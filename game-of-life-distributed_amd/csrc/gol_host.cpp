@@ -487,6 +487,34 @@ int golrun_event_cells(golrun_t r, int64_t *xy, uint64_t cap) {
     return GOLHIP_OK;
 }
 
+int golrun_drain(golrun_t r, golrun_drain_stats_t *st, uint64_t *flips, uint64_t *digests, int64_t turns_cap,
+                 int64_t width) {
+    if (!r || !st || turns_cap < 0 || ((flips || digests) && width <= 0)) return run_fail("bad arguments");
+    memset(st, 0, sizeof *st);
+    for (int64_t t = 0; t < turns_cap; ++t) {
+        if (flips) flips[t] = 0;
+        if (digests) digests[t] = 0;
+    }
+    auto mix = [](uint64_t x) {
+        uint64_t z = x + 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    };
+    gol::Event e;
+    while (r->events.recv(e)) {  // main.go:59-66, until close
+        const int k = (int)e.kind;
+        if (k >= 0 && k < 6) st->count[k]++;
+        if (e.kind == gol::EventKind::TurnComplete) st->last_turn = e.CompletedTurns;
+        if (e.kind == gol::EventKind::FinalTurnComplete) st->final_alive = (int64_t)e.Alive.size();
+        if (e.kind != gol::EventKind::CellFlipped || e.CompletedTurns < 1 || e.CompletedTurns > turns_cap) continue;
+        const int64_t t = e.CompletedTurns - 1;
+        const uint64_t i = flips ? ++flips[t] : 0;
+        if (digests) digests[t] += mix(i) * ((uint64_t)e.Cell.Y * (uint64_t)width + (uint64_t)e.Cell.X + 1);
+    }
+    return GOLHIP_OK;
+}
+
 int golrun_send_key(golrun_t r, uint32_t key) {
     if (!r || !r->use_keys) return run_fail("run has no key channel");
     return r->keys.send((char32_t)key) ? GOLHIP_OK : run_fail("key channel closed");

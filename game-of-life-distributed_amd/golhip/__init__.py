@@ -416,6 +416,10 @@ class RunEvent(ctypes.Structure):
     ]
 
 
+class DrainStats(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_uint64 * 6), ("last_turn", ctypes.c_int64), ("final_alive", ctypes.c_int64)]
+
+
 _host = None
 
 
@@ -436,6 +440,7 @@ def load_host(path: str = HOST_LIB_PATH) -> ctypes.CDLL:
         "golrun_next_event": ([ctypes.c_void_p, P(RunEvent), i32], ctypes.c_int),
         "golrun_event_cells": ([ctypes.c_void_p, ctypes.c_void_p, u64], ctypes.c_int),
         "golrun_send_key": ([ctypes.c_void_p, u32], ctypes.c_int),
+        "golrun_drain": ([ctypes.c_void_p, P(DrainStats), ctypes.c_void_p, ctypes.c_void_p, i64, i64], ctypes.c_int),
         "golrun_wait": ([ctypes.c_void_p, ctypes.c_char_p, u64], ctypes.c_int),
         "golrun_destroy": ([ctypes.c_void_p], ctypes.c_int),
     }
@@ -500,6 +505,21 @@ class Run:
             if ev is None:
                 return
             yield ev
+
+    def drain(self, turns_cap: int = 0, width: int = 0):
+        """main.go's headless drain loop in C++ (golrun_drain): consume every
+        event until close.  Returns (counts by event name, last TurnComplete,
+        len(FinalTurnComplete.Alive), per-turn CellFlipped counts, per-turn
+        ordered digests)."""
+        st = DrainStats()
+        flips = np.zeros(max(turns_cap, 1), dtype=np.uint64)
+        dig = np.zeros(max(turns_cap, 1), dtype=np.uint64)
+        rc = load_host().golrun_drain(self._h, ctypes.byref(st), _ptr(flips) if turns_cap else None,
+                                      _ptr(dig) if turns_cap else None, turns_cap, width)
+        if rc != 0:
+            raise GolHipError(rc, load_host().golrun_last_error().decode())
+        counts = {EVENT_NAMES[k]: int(st.count[k]) for k in range(6)}
+        return counts, st.last_turn, st.final_alive, flips[:turns_cap], dig[:turns_cap]
 
     def send_key(self, key: str) -> None:
         lib = load_host()

@@ -63,6 +63,20 @@ int golrun_next_event(golrun_t r, golrun_event_t *ev, int32_t timeout_ms);
 int golrun_event_cells(golrun_t r, int64_t *xy, uint64_t cap);
 /* String() of an event's fields (event.go:72-131); needs no run or device. */
 int golrun_event_string(const golrun_event_t *ev, char *out, uint64_t cap);
+/* main.go's headless drain loop (main.go:59-66) on the run's own events, for
+ * runs whose event streams are too large to hand over one by one: receives
+ * until the channel closes and tallies count[kind].  For CellFlipped of
+ * completed turn t in 1..turns_cap (documented contract: 1-based turns):
+ * flips[t-1] events and digests[t-1] = sum over them, in arrival order, of
+ * splitmix64(i) * (Y * width + X + 1), i = 1, 2, ... within the turn
+ * (tests/golden/make_fullsize.py ordered_digest).  flips / digests nullable. */
+typedef struct golrun_drain_stats {
+    uint64_t count[6];     /* events received, by GOLRUN_* kind              */
+    int64_t last_turn;     /* CompletedTurns of the last TurnComplete        */
+    int64_t final_alive;   /* len(FinalTurnComplete.Alive), 0 if none         */
+} golrun_drain_stats_t;
+int golrun_drain(golrun_t r, golrun_drain_stats_t *st, uint64_t *flips, uint64_t *digests, int64_t turns_cap,
+                 int64_t width);
 int golrun_send_key(golrun_t r, uint32_t key);
 /* Drains unread events, joins the run; 0 or the panic message in err. */
 int golrun_wait(golrun_t r, char *err, uint64_t err_cap);

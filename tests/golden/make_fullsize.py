@@ -16,7 +16,9 @@ check/alive counts) and to the per-cell restatement oracle/gol_oracle.c:
   c4  configs[4]  5120^2,   seed 0x5EED0005, the CellFlipped stream of turns
                   1..50: per-turn flip counts and the SHA-256 of the
                   concatenated (x = col, y = row) int32 pairs, row-major within
-                  a turn (initializeAliveCells, distributor.go:212-220)
+                  a turn (initializeAliveCells, distributor.go:212-220), and
+                  per turn an order-dependent digest (ordered_digest) that the
+                  host mirror's C++ drain can recompute
 
 For each checkpoint: the board digest of golhip_board_hash (include/golhip.h,
 restated by fastcpu_hash) and the alive count; for the last checkpoint also
@@ -81,21 +83,36 @@ def make_board(o: COracle, key: str, c: dict, th: int, arrays: dict) -> dict:
     return rec
 
 
+def ordered_digest(xy: np.ndarray, W: int) -> int:
+    """Order-dependent digest of one turn's list, cheap in C++ too (the host
+    mirror's golrun_drain): sum over positions i of
+    splitmix64(i + 1) * (y * W + x + 1) mod 2^64."""
+    i = np.arange(1, len(xy) + 1, dtype=np.uint64)
+    e = xy[:, 1].astype(np.uint64) * np.uint64(W) + xy[:, 0].astype(np.uint64) + np.uint64(1)
+    with np.errstate(over="ignore"):
+        z = i + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+        return int((z * e).sum(dtype=np.uint64))
+
+
 def make_events(o: COracle, th: int) -> dict:
     N, seed, T = EVENTS["N"], EVENTS["seed"], EVENTS["turns"]
     w = o.fill_random64(N, N, seed, th)
     init = flips_xy(np.zeros_like(w), w, N)  # the CellFlipped of every alive cell at load (:72-80)
-    sha, counts = hashlib.sha256(), []
+    sha, counts, digests = hashlib.sha256(), [], []
     for _ in range(T):
         nxt = w.copy()
         o.run_fast_words(nxt, N, 1, th)
         xy = flips_xy(w, nxt, N)
         sha.update(xy.tobytes())
         counts.append(int(len(xy)))
+        digests.append(f"{ordered_digest(xy, N):016x}")
         w = nxt
     rec = {"config": EVENTS["config"], "width": N, "height": N, "seed": seed, "turns": T,
            "initial_alive": int(len(init)), "initial_sha256": hashlib.sha256(init.tobytes()).hexdigest(),
-           "flip_counts": counts, "flips_sha256": sha.hexdigest(),
+           "flip_counts": counts, "flips_sha256": sha.hexdigest(), "flip_digests": digests,
            "final": {"hash": f"{o.hash64(w, N, th):016x}", "alive": o.popcount64(w, N, th)}}
     print(f"c4: {T} turns, {sum(counts)} flips, sha {rec['flips_sha256'][:16]}", flush=True)
     return rec

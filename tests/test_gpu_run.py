@@ -202,3 +202,34 @@ def test_cli_quit_key(root):
                          text=True, timeout=120)
     assert res.returncode == 0, res.stderr
     assert any(p.name.startswith("64x64x") for p in (root / "out").iterdir())
+
+
+def test_config4_5120_event_stream_through_run(tmp_path):
+    """BASELINE configs[4] through the whole gol.Run mirror: the 5120^2 board
+    as images/5120x5120.pgm, every CellFlipped of turns 1..T through an events
+    channel of capacity 1000 (main.go:53) into main.go's headless drain loop
+    (golrun_drain, C++): per-turn counts and order-dependent digests equal the
+    oracle fixture (tests/golden/fullsize.json c4); then the final PGM and
+    FinalTurnComplete."""
+    import json
+    from oracle.oracle import COracle
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "fullsize.json")) as f:
+        rec = json.load(f)["c4"]
+    N, T = rec["width"], 6
+    board = COracle().fill_random(N, N, rec["seed"])
+    (tmp_path / "images").mkdir()
+    (tmp_path / "images" / f"{N}x{N}.pgm").write_bytes(pgm_bytes(board))
+    r = golhip.Run(T, 8, N, N, str(tmp_path), events_cap=1000)
+    t0 = time.time()
+    counts, last, final_alive, flips, digests = r.drain(T, N)
+    dt = time.time() - t0
+    assert r.wait() == ""
+    r.close()
+    assert counts["TurnComplete"] == T and last == T and counts["FinalTurnComplete"] == 1
+    assert counts["CellFlipped"] == rec["initial_alive"] + sum(rec["flip_counts"][:T])
+    assert [int(x) for x in flips] == rec["flip_counts"][:T]
+    assert [f"{int(x):016x}" for x in digests] == rec["flip_digests"][:T]
+    out = read_pgm(str(tmp_path / "out" / f"{N}x{N}x{T}.pgm"), N, N)
+    assert int((out == 255).sum()) == final_alive
+    print(f"gol.Run 5120^2 with every CellFlipped: {T} turns, {counts['CellFlipped']} events in {dt:.1f} s")
