@@ -309,13 +309,30 @@ __device__ __forceinline__ Lanes<WPL> vmov(const Lanes<WPL> &v) {
 // Output stores (STORE): kStoreDeferred = masked, one group late (K1);
 // kStoreMasked = masked, right after the group; kStoreDummy = unconditional,
 // masked rows to a dummy row (wave_id % dummy_rows of dst).
-[[maybe_unused]] constexpr int kStoreDeferred = 0, kStoreMasked = 1, kStoreDummy = 2;
+// kStoreAfterLoads = one group late like kStoreDeferred, but unconditional
+// (masked rows / lanes to the dummy row) and issued AFTER the next group's
+// prefetch loads: vmcnt counts in issue order, so the wait for those loads
+// at the bottom of the body no longer waits for the stores' acks too.
+// kStoreMaskedAfterLoads = the same, but masked stores (no dummy row).
+// kStoreBufAfterLoads = after the loads, as buffer stores whose masked lanes
+// carry an out-of-range offset (the hardware drops them): no branch, no dummy
+// row, and a static vmcnt.  Needs each wave's band < 2 GiB (host-checked).
+// kStoreBufImmediate = buffer stores right after the group (no deferral).
+[[maybe_unused]] constexpr int kStoreDeferred = 0, kStoreMasked = 1, kStoreDummy = 2, kStoreAfterLoads = 3,
+                               kStoreMaskedAfterLoads = 4, kStoreBufAfterLoads = 5, kStoreBufImmediate = 6;
 #ifndef GOL_PERSIST_STORE
-#define GOL_PERSIST_STORE 2
+#define GOL_PERSIST_STORE 6  // immediate buffer stores: 16384^2 58.5 -> 59.0 TCUPS vs dummy-row stores (profiles/r2n)
 #endif
 #ifndef GOL_PAIR_STORE
-#define GOL_PAIR_STORE 0
+#define GOL_PAIR_STORE -1  // -1: by words per lane (A/B builds override)
 #endif
+// K1's stores, measured per words per lane (profiles/r2m, same box): buffer
+// stores after the loads 65536^2 114.6 -> 116.5 TCUPS (WPL 2); quads keep the
+// deferred masked stores (262144^2: 129.0 vs 116.0 with buffer stores).
+template <int WPL>
+constexpr int pair_store() {
+    return GOL_PAIR_STORE >= 0 ? GOL_PAIR_STORE : (WPL == 4 ? kStoreDeferred : kStoreBufAfterLoads);
+}
 
 template <int D, bool SKIP, int WPL, int STORE = kStoreDeferred, bool LATE_CLAIM = true>
 __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int rows_here, int t0, int wave_id,
@@ -373,6 +390,12 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
     int lim = claim ? 0 : rows_here;  // output rows [0, lim) of this wave's order are its own
     uint32_t *const dummy = a.dst + (size_t)(wave_id % a.dummy_rows) * Ww + col;
     uint32_t cnt = 0;
+    // kStoreBufAfterLoads: one buffer resource over the wave's output rows
+    // [r0, r0 + rows_here) of dst (wave-uniform), a byte offset per lane
+    const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+        a.dst + (size_t)(a.dst_base + r0) * Ww, (short)0,
+        (STORE == kStoreBufAfterLoads || STORE == kStoreBufImmediate) ? rows_here * Ww * 4 : 0,
+        0x00020000);
     // output rows counted into the popcount, in this wave's out_idx order
     const int clo = dir > 0 ? a.count_lo - r0 : r0 + rows_here - a.count_hi;
     const int chi = dir > 0 ? a.count_hi - r0 : r0 + rows_here - a.count_lo;
@@ -387,7 +410,18 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
             else
                 *reinterpret_cast<uint2 *>(p) = make_uint2(y.w[0], y.w[1]);
         };
-        if constexpr (STORE == kStoreDummy)
+        if constexpr (STORE == kStoreBufAfterLoads || STORE == kStoreBufImmediate) {
+            const int rel = dir > 0 ? out_idx : rows_here - 1 - out_idx;
+            const int off = ok ? (rel * Ww + col) * 4 : INT_MAX;  // out of range: dropped
+            if constexpr (WPL == 1)
+                __builtin_amdgcn_raw_buffer_store_b32(y.w[0], brs, off, 0, 0);
+            else if constexpr (WPL == 2)
+                __builtin_amdgcn_raw_buffer_store_b64((__attribute__((ext_vector_type(2))) unsigned)
+                                                      {y.w[0], y.w[1]}, brs, off, 0, 0);
+            else
+                __builtin_amdgcn_raw_buffer_store_b128((__attribute__((ext_vector_type(4))) unsigned)
+                                                       {y.w[0], y.w[1], y.w[2], y.w[3]}, brs, off, 0, 0);
+        } else if constexpr (STORE == kStoreDummy || STORE == kStoreAfterLoads)
             put(ok ? dst_row0 + (ptrdiff_t)out_idx * dst_step : dummy);
         else if (ok)
             put(dst_row0 + (ptrdiff_t)out_idx * dst_step);
@@ -451,6 +485,11 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
     bool more = true, pend = false;
     Lanes<WPL> q0, q1, q2;  // the previous group's output rows (stored one body late)
     int qoi = 0;
+    if constexpr (STORE == kStoreAfterLoads || STORE == kStoreBufAfterLoads) {  // the first body stores nothing real
+#pragma unroll
+        for (int k = 0; k < WPL; ++k) q0.w[k] = q1.w[k] = q2.w[k] = 0u;
+        qoi = -8;
+    }
     for (; claim ? more : oi < rows_here; oi += 3) {
         if (STORE == kStoreDeferred && pend) {
             emit(q0, qoi);
@@ -458,6 +497,15 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
             emit(q2, qoi + 2);
         }
         const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
+        if constexpr (STORE == kStoreAfterLoads || STORE == kStoreBufAfterLoads) {
+            emit(q0, qoi);
+            emit(q1, qoi + 1);
+            emit(q2, qoi + 2);
+        } else if (STORE == kStoreMaskedAfterLoads && pend) {
+            emit(q0, qoi);
+            emit(q1, qoi + 1);
+            emit(q2, qoi + 2);
+        }
         // claim this group's rows >= 0; the LDS round trip hides under the group
         const int need = claim ? min(3, max(0, oi + 3)) : 0;
         // LATE_CLAIM: wait for the LDS round trip after the group rather than
@@ -482,7 +530,8 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
             lim = max(oi, 0) + min(need, max(0, old));
             more = old > need;
         }
-        if constexpr (STORE == kStoreDeferred) {
+        if constexpr (STORE == kStoreDeferred || STORE == kStoreAfterLoads || STORE == kStoreMaskedAfterLoads ||
+                      STORE == kStoreBufAfterLoads) {
             q0 = y0;
             q1 = y1;
             q2 = y2;
@@ -498,7 +547,8 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
         x1 = vmov(n1);
         x2 = vmov(n2);
     }
-    if (STORE == kStoreDeferred && pend) {
+    if ((STORE == kStoreDeferred || STORE == kStoreAfterLoads || STORE == kStoreMaskedAfterLoads ||
+         STORE == kStoreBufAfterLoads) && pend) {
         emit(q0, qoi);
         emit(q1, qoi + 1);
         emit(q2, qoi + 2);
@@ -548,7 +598,7 @@ __global__ __launch_bounds__(512) void gol_tb_pair_kernel(StepArgs a) {
     if (CNT && threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
     if (len == 0) return;  // wave-uniform, after the only barrier
-    const uint32_t cnt = stream_band<D, true, WPL, GOL_PAIR_STORE, true>(a, r0, len, tile * tile_words(WPL), blockIdx.x * 8 + w,
+    const uint32_t cnt = stream_band<D, true, WPL, pair_store<WPL>(), true>(a, r0, len, tile * tile_words(WPL), blockIdx.x * 8 + w,
                                                    w < 4 ? 1 : -1, &s_claim[w & 3]);
     if constexpr (!CNT) {
         if (a.alive) {

@@ -535,6 +535,8 @@ int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int
         a.rows_per_wave = golk::auto_rows_per_wave(h->Ww, a.rows_out, depth, std::max(slots, 1), h->fill_skip, wpl,
                                                      tb_paired(h));
     }
+    // a wave's buffer-store range (two bands of a paired region) must stay < 2 GiB
+    a.rows_per_wave = (int)std::min<int64_t>(a.rows_per_wave, ((1ll << 31) - 1) / (8ll * h->Ww));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->flags & GOLHIP_FLAG_TIMING) {
         e0 = take_event(h);
@@ -653,6 +655,7 @@ bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int w
     const int age_split = h->age_split >= 0 ? h->age_split : (nw == 8 ? 65 : 0);
     const bool split = age_split > 0 && age_split < 100;
     if (!golk::plan_persist(h->Ww, base.rows_out, depth, h->cu_count, wpl, nw, &p, h->persist_wg_tx)) return false;
+    if (2ll * p.S * h->Ww * 4 >= (1ll << 31)) return false;  // a band's buffer-store range
     // every workgroup must be resident at once (they wait on their neighbours):
     // the grid may not exceed what the occupancy query admits on this device
     if ((int64_t)p.cols * p.wg_y > (int64_t)golk::persist_blocks_per_cu(depth, wpl, nw) * h->cu_count) return false;
