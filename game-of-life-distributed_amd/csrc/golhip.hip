@@ -368,7 +368,11 @@ int wpl_for(golhip_t h) {
         const int def = golk::persist_waves_for(d, wpl);
         return std::max(plan_rate(h, wpl, def, d), def == 16 ? plan_rate(h, wpl, 8, d) : 0.0);
     };
-    return best(2) >= best(1) ? 2 : 1;
+    // The model charges WPL 2's halved bands too much fill: at 16384^2 it
+    // prefers WPL 1 by 4 %, but WPL 2 (8 waves) measured 61.7 vs 59.0 TCUPS
+    // on the same box (profiles/r2p/persist_wpl_16384.txt), so WPL 2 wins
+    // unless the model puts it more than 5 % behind.
+    return best(2) >= 0.95 * best(1) ? 2 : 1;
 }
 
 // The wpl = 2 step kernels run on the interleaved pair layout; every other
