@@ -333,8 +333,17 @@ template <int WPL>
 constexpr int pair_store() {
     return GOL_PAIR_STORE >= 0 ? GOL_PAIR_STORE : (WPL == 4 ? kStoreDeferred : kStoreBufAfterLoads);
 }
+#ifndef GOL_PAIR_G2
+#define GOL_PAIR_G2 0
+#endif
+template <int WPL>
+constexpr bool pair_g2() {
+    return GOL_PAIR_G2 && pair_store<WPL>() == kStoreBufAfterLoads;
+}
 
-template <int D, bool SKIP, int WPL, int STORE = kStoreDeferred, bool LATE_CLAIM = true>
+// G2 (kStoreBufAfterLoads only): the main loop takes two 3-row groups per
+// body, so each body's prefetch loads have two groups of compute to land.
+template <int D, bool SKIP, int WPL, int STORE = kStoreDeferred, bool LATE_CLAIM = true, bool G2 = false>
 __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int rows_here, int t0, int wave_id,
                                                 int dir = 1, int *claim = nullptr) {
     const int lane = threadIdx.x & 63;
@@ -490,6 +499,59 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
         for (int k = 0; k < WPL; ++k) q0.w[k] = q1.w[k] = q2.w[k] = 0u;
         qoi = -8;
     }
+    if constexpr (G2) {
+        static_assert(STORE == kStoreBufAfterLoads, "G2 needs static store counts");
+        Lanes<WPL> x3 = vmov(load_next()), x4 = vmov(load_next()), x5 = vmov(load_next());
+        Lanes<WPL> q3 = q0, q4 = q0, q5 = q0;
+        for (; claim ? more : oi < rows_here; oi += 6) {
+            const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
+            const Lanes<WPL> n3 = load_next(), n4 = load_next(), n5 = load_next();
+            emit(q0, qoi);
+            emit(q1, qoi + 1);
+            emit(q2, qoi + 2);
+            emit(q3, qoi + 3);
+            emit(q4, qoi + 4);
+            emit(q5, qoi + 5);
+            const int need = claim ? min(6, max(0, oi + 6)) : 0;
+            int old = 0, o = 0;
+            if (need > 0 && lane == 0)
+                o = __hip_atomic_fetch_add(claim, -need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __builtin_amdgcn_sched_barrier(0);
+            Lanes<WPL> y0 = x0, y1 = x1, y2 = x2, y3 = x3, y4 = x4, y5 = x5;
+            push_group<D, D, WPL>(y0, y1, y2, h0, h1, cc);
+            push_group<D, D, WPL>(y3, y4, y5, h0, h1, cc);
+            if (need > 0) {
+                asm volatile("" : "+v"(o));  // the LDS wait after both groups
+                old = __builtin_amdgcn_readfirstlane(o);
+                lim = max(oi, 0) + min(need, max(0, old));
+                more = old > need;
+            }
+            q0 = y0;
+            q1 = y1;
+            q2 = y2;
+            q3 = y3;
+            q4 = y4;
+            q5 = y5;
+            qoi = oi;
+            pend = true;
+            __builtin_amdgcn_sched_barrier(0);
+            x0 = vmov(n0);
+            x1 = vmov(n1);
+            x2 = vmov(n2);
+            x3 = vmov(n3);
+            x4 = vmov(n4);
+            x5 = vmov(n5);
+        }
+        if (pend) {
+            emit(q0, qoi);
+            emit(q1, qoi + 1);
+            emit(q2, qoi + 2);
+            emit(q3, qoi + 3);
+            emit(q4, qoi + 4);
+            emit(q5, qoi + 5);
+        }
+        return cnt;
+    }
     for (; claim ? more : oi < rows_here; oi += 3) {
         if (STORE == kStoreDeferred && pend) {
             emit(q0, qoi);
@@ -598,7 +660,7 @@ __global__ __launch_bounds__(512) void gol_tb_pair_kernel(StepArgs a) {
     if (CNT && threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
     if (len == 0) return;  // wave-uniform, after the only barrier
-    const uint32_t cnt = stream_band<D, true, WPL, pair_store<WPL>(), true>(a, r0, len, tile * tile_words(WPL), blockIdx.x * 8 + w,
+    const uint32_t cnt = stream_band<D, true, WPL, pair_store<WPL>(), true, pair_g2<WPL>()>(a, r0, len, tile * tile_words(WPL), blockIdx.x * 8 + w,
                                                    w < 4 ? 1 : -1, &s_claim[w & 3]);
     if constexpr (!CNT) {
         if (a.alive) {
