@@ -73,7 +73,7 @@ def parse():
     ap.add_argument("--workload", type=int, default=65536, choices=sorted(WORKLOADS))
     ap.add_argument("--turns-per-step", type=int, default=None,
                     help="default: the config's turns (parity is only checked then)")
-    ap.add_argument("--tb-depth", type=int, default=16)
+    ap.add_argument("--tb-depth", type=int, default=20)
     ap.add_argument("--rows-per-wave", type=int, default=0, help="0 = automatic")
     ap.add_argument("--option", action="append", default=[], help="engine option key=value (A/B runs)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
@@ -166,9 +166,11 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str) 
     if perf["persist_kernel_ms"] >= perf["step_kernel_ms"]:
         kname, launches, kms, kturns = "gol_persist_kernel", perf["persist_launches"], perf["persist_kernel_ms"], \
             perf["persist_turns"]
+        depth = perf["persist_depth"]
     else:
         kname, launches, kms, kturns = "gol_tb_pair_kernel", perf["step_launches"], perf["step_kernel_ms"], \
             perf["step_turns"]
+        depth = perf["tb_depth"]
     launches = max(1, launches)
     avg_s = kms / launches * 1e-3
     wpl = max(1, perf["words_per_lane"])
@@ -185,7 +187,7 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str) 
         "unit": "Gslot/s (wave64 VALU issue slots)",
         "frac": round(achieved / VALU_PEAK_GSLOTS, 4) if achieved else None,
         "traffic": None,
-        "kernel": f"{kname}<{perf['tb_depth']}, {wpl}>",
+        "kernel": f"{kname}<{depth}, {wpl}>",
         "avg_launch_ms": round(avg_s * 1e3, 5),
         "launches": launches,
         "turns_per_launch": tpl,

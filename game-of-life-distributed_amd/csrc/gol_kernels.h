@@ -44,6 +44,7 @@ struct StepArgs {
 // stage-rows that only see padding.  wpl: words per lane (1 or 2).
 hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s, bool fill_skip, int wpl, bool paired = false);
 int max_depth_for(int wpl);
+int persist_max_depth(int wpl);
 int tb_tiles(int Ww, int wpl);
 // One turn for any width (W % 32 != 0 boards such as 16x16).
 hipError_t launch_step_generic(const StepArgs &a, hipStream_t s);

@@ -62,6 +62,28 @@ __device__ __forceinline__ uint32_t from_left_lane(uint32_t v) {
 __device__ __forceinline__ uint32_t from_right_lane(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xF, 0xF, true);
 }
+// The stencil's lane shifts: DPP (VALU, half rate) or ds_bpermute through the
+// LDS crossbar (no VALU slot; the edge lanes receive the wrapped lane, which
+// is tile halo either way).
+#ifndef GOL_XLANE_BPERM
+#define GOL_XLANE_BPERM 0
+#endif
+__device__ __forceinline__ uint32_t stencil_left(uint32_t v) {
+    if constexpr (GOL_XLANE_BPERM) {
+        const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        return (uint32_t)__builtin_amdgcn_ds_bpermute((lane - 1) << 2, (int)v);
+    } else {
+        return from_left_lane(v);
+    }
+}
+__device__ __forceinline__ uint32_t stencil_right(uint32_t v) {
+    if constexpr (GOL_XLANE_BPERM) {
+        const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        return (uint32_t)__builtin_amdgcn_ds_bpermute((lane + 1) << 2, (int)v);
+    } else {
+        return from_right_lane(v);
+    }
+}
 
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
@@ -213,9 +235,18 @@ struct Lanes {
 };
 
 // One stage (turn t) for the row entering with role R (R = input index % 3).
+// el / er: the edge words from the adjacent lanes (left lane's last word,
+// right lane's first).  With the ds_bpermute shifts they are fetched at the
+// end of the previous stage (`last` = the row's last stage here), so the LDS
+// latency overlaps the two other rows' stages in between.
 template <int D, int R, int WPL>
-__device__ __forceinline__ void stage(int t, Lanes<WPL> &x, uint32_t (&h0)[3][D][WPL], uint32_t (&h1)[3][D][WPL],
+__device__ __forceinline__ void stage(int t, Lanes<WPL> &x, uint32_t &el, uint32_t &er, int last,
+                                      uint32_t (&h0)[3][D][WPL], uint32_t (&h1)[3][D][WPL],
                                       uint32_t (&cc)[3][D][WPL]) {
+    if (t == 0 || !GOL_XLANE_BPERM) {
+        el = stencil_left(x.w[WPL - 1]);
+        er = stencil_right(x.w[0]);
+    }
     constexpr int N = R;            // slot of the row entering now
     constexpr int C = (R + 2) % 3;  // previous row (the one we emit)
     constexpr int P = (R + 1) % 3;  // the row before it
@@ -227,15 +258,15 @@ __device__ __forceinline__ void stage(int t, Lanes<WPL> &x, uint32_t (&h0)[3][D]
     // one word per side needs a one-bit funnel shift with the edge lane's bit.
     uint32_t west[WPL], east[WPL];
     if constexpr (WPL == 1) {
-        const uint32_t l = from_left_lane(x.w[0]);
-        const uint32_t r = from_right_lane(x.w[0]);
+        const uint32_t l = el;
+        const uint32_t r = er;
         west[0] = __builtin_amdgcn_alignbit(x.w[0], l, 31);  // bit b = cell b-1
         east[0] = __builtin_amdgcn_alignbit(r, x.w[0], 1);   // bit b = cell b+1
     } else if constexpr (WPL == 4) {
         // interleaved quads: word j holds cells 4k + j, so every neighbour
         // word but two is another word of the lane as is
-        const uint32_t l3 = from_left_lane(x.w[3]);   // left chunk's cells 4k + 3 (bit 31 = its cell 127)
-        const uint32_t r0 = from_right_lane(x.w[0]);  // right chunk's cells 4k (bit 0 = its cell 0)
+        const uint32_t l3 = el;                       // left chunk's cells 4k + 3 (bit 31 = its cell 127)
+        const uint32_t r0 = er;                       // right chunk's cells 4k (bit 0 = its cell 0)
         west[0] = __builtin_amdgcn_alignbit(x.w[3], l3, 31);  // cell 4k - 1
         west[1] = x.w[0];
         west[2] = x.w[1];
@@ -245,8 +276,8 @@ __device__ __forceinline__ void stage(int t, Lanes<WPL> &x, uint32_t (&h0)[3][D]
         east[2] = x.w[3];
         east[3] = __builtin_amdgcn_alignbit(r0, x.w[0], 1);   // cell 4k + 4
     } else {
-        const uint32_t l1 = from_left_lane(x.w[1]);   // left chunk's odd cells (bit 31 = its cell 63)
-        const uint32_t r0 = from_right_lane(x.w[0]);  // right chunk's even cells (bit 0 = its cell 0)
+        const uint32_t l1 = el;                       // left chunk's odd cells (bit 31 = its cell 63)
+        const uint32_t r0 = er;                       // right chunk's even cells (bit 0 = its cell 0)
         west[0] = __builtin_amdgcn_alignbit(x.w[1], l1, 31);  // cell 2k-1
         east[0] = x.w[1];                                     // cell 2k+1
         west[1] = x.w[0];                                     // cell 2k
@@ -270,6 +301,10 @@ __device__ __forceinline__ void stage(int t, Lanes<WPL> &x, uint32_t (&h0)[3][D]
         cc[N][t][k] = x.w[k];
         x.w[k] = nx[k];
     }
+    if (GOL_XLANE_BPERM && t < last) {
+        el = stencil_left(nx[WPL - 1]);
+        er = stencil_right(nx[0]);
+    }
 }
 
 // A group of 3 consecutive input rows through the first A of the D stages.
@@ -282,11 +317,12 @@ template <int D, int A, int WPL>
 __device__ __forceinline__ void push_group(Lanes<WPL> &x0, Lanes<WPL> &x1, Lanes<WPL> &x2,
                                            uint32_t (&h0)[3][D][WPL], uint32_t (&h1)[3][D][WPL],
                                            uint32_t (&cc)[3][D][WPL]) {
+    uint32_t e[3][2];
 #pragma unroll
     for (int s = 0; s < A + 2; ++s) {
-        if (s < A) stage<D, 0, WPL>(s, x0, h0, h1, cc);
-        if (s >= 1 && s - 1 < A) stage<D, 1, WPL>(s - 1, x1, h0, h1, cc);
-        if (s >= 2 && s - 2 < A) stage<D, 2, WPL>(s - 2, x2, h0, h1, cc);
+        if (s < A) stage<D, 0, WPL>(s, x0, e[0][0], e[0][1], A - 1, h0, h1, cc);
+        if (s >= 1 && s - 1 < A) stage<D, 1, WPL>(s - 1, x1, e[1][0], e[1][1], A - 1, h0, h1, cc);
+        if (s >= 2 && s - 2 < A) stage<D, 2, WPL>(s - 2, x2, e[2][0], e[2][1], A - 1, h0, h1, cc);
     }
 }
 
@@ -853,9 +889,9 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
 }
 
 // ---- host-side dispatch over (depth, fill skip, words per lane) ----------
-// Depths 1, 2, 4, 6, 8, 12, 16 (and 24, 32 for WPL = 1: depth 32 at WPL = 2
-// would exceed 256 VGPRs; WPL = 4 stops at 8); the host's depth_plan picks
-// among them.
+// Depths 1, 2, 4, 6, 8, 12, 16, 20 (and 24, 32 for WPL = 1: depth 24 at
+// WPL = 2 would exceed 256 VGPRs; WPL = 4 stops at 8); the host's depth_plan
+// picks among them.
 template <typename F>
 static hipError_t dispatch(int depth, bool skip, int wpl, F &&f) {
 #define GOL_CASE(D, SK, WP) \
@@ -871,11 +907,15 @@ static hipError_t dispatch(int depth, bool skip, int wpl, F &&f) {
     GOL_CASE(6, true, 4) GOL_CASE(6, false, 4)
     GOL_CASE(1, true, 2) GOL_CASE(2, true, 2) GOL_CASE(4, true, 2) GOL_CASE(8, true, 2) GOL_CASE(16, true, 2)
     GOL_CASE(1, false, 2) GOL_CASE(2, false, 2) GOL_CASE(4, false, 2) GOL_CASE(8, false, 2) GOL_CASE(16, false, 2)
+    GOL_CASE(20, true, 1) GOL_CASE(20, false, 1) GOL_CASE(20, true, 2) GOL_CASE(20, false, 2)
 #undef GOL_CASE
     return hipErrorInvalidValue;
 }
 
-int max_depth_for(int wpl) { return wpl == 4 ? 8 : wpl == 2 ? 16 : 32; }
+// Per-launch kernels: WPL 2 fits 20 stages in 242 VGPRs (two waves per SIMD,
+// no scratch); the resident kernel keeps 16 (its instantiations).
+int max_depth_for(int wpl) { return wpl == 4 ? 8 : wpl == 2 ? 20 : 32; }
+int persist_max_depth(int wpl) { return wpl == 4 ? 8 : wpl == 2 ? 16 : 32; }
 
 int tb_tiles(int Ww, int wpl) { return (Ww + tile_words(wpl) - 1) / tile_words(wpl); }
 
@@ -891,7 +931,7 @@ static hipError_t dispatch_pair(int depth, int wpl, F &&f, bool cnt = false) {
     GOL_QCASE(1, 1) GOL_QCASE(2, 1) GOL_QCASE(4, 1) GOL_QCASE(8, 1) GOL_QCASE(16, 1) GOL_QCASE(32, 1)
     GOL_QCASE(1, 2) GOL_QCASE(2, 2) GOL_QCASE(4, 2) GOL_QCASE(8, 2) GOL_QCASE(16, 2)
     GOL_QCASE(12, 1) GOL_QCASE(24, 1) GOL_QCASE(12, 2) GOL_QCASE(1, 4) GOL_QCASE(2, 4) GOL_QCASE(4, 4) GOL_QCASE(8, 4)
-    GOL_QCASE(6, 1) GOL_QCASE(6, 2) GOL_QCASE(6, 4)
+    GOL_QCASE(6, 1) GOL_QCASE(6, 2) GOL_QCASE(6, 4) GOL_QCASE(20, 1) GOL_QCASE(20, 2)
 #undef GOL_QCASE
     return hipErrorInvalidValue;
 }

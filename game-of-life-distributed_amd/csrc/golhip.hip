@@ -86,7 +86,7 @@ int fail(int code, const char *fmt, ...) {
 
 // Turns per launch with an instantiated step kernel (24: one word per lane
 // only, as 32; see max_depth_for).
-constexpr int kDepths[] = {32, 24, 16, 12, 8, 6, 4, 2, 1};
+constexpr int kDepths[] = {32, 24, 20, 16, 12, 8, 6, 4, 2, 1};
 constexpr int kNumDepths = sizeof(kDepths) / sizeof(kDepths[0]);
 // trace buffer: 8 totals + (start, end) per (workgroup < 1024, wave < 64)
 constexpr int64_t kTraceWords = 8 + 2 * 1024 * 64;
@@ -106,7 +106,7 @@ struct golhip {
     int cur = 0;
     int64_t phys_rows = 0;
 
-    int tb_depth = 16;
+    int tb_depth = 20;          // per-launch WPL-2 kernels fuse up to 20, the resident kernel 16
     int rows_per_wave = 0;      // 0 = automatic (per depth, from occupancy)
     int cu_count = 0;
     bool fill_skip = true;      // option "fill_skip"
@@ -312,7 +312,7 @@ double plan_rate(golhip_t h, int wpl, int nw, int depth) {
     return util * S / (S + 1.75 * depth) * occ / slots_per_word(wpl);
 }
 
-int default_depth(golhip_t h, int wpl) { return largest_depth(std::min(h->tb_depth, golk::max_depth_for(wpl))); }
+int default_depth(golhip_t h, int wpl) { return largest_depth(std::min(h->tb_depth, golk::persist_max_depth(wpl))); }
 
 // Waves per workgroup of the persistent kernel: the option, or the better of
 // 16 (4 per SIMD: hides VALU latency) and 8 (taller bands: less fill).
@@ -396,7 +396,9 @@ int loaded_canonical(golhip_t h) {
 // all come from one neighbour strip, so depth <= strip rows.
 int depth_cap(golhip_t h, bool halo) {
     if (h->W % 32 != 0) return 1;  // generic kernel: one turn per launch
-    int cap = std::min(h->tb_depth, golk::max_depth_for(wpl_for(h)));
+    // a strip between exchanges runs the resident kernel (its depths) when on
+    const int wpl = wpl_for(h);
+    int cap = std::min(h->tb_depth, (halo && persist_on(h)) ? golk::persist_max_depth(wpl) : golk::max_depth_for(wpl));
     if (halo) cap = std::min(cap, sched_rows(h));
     return cap;
 }
@@ -728,7 +730,7 @@ bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int w
 }
 
 int persist_depth_for(golhip_t h, int wpl) {
-    return largest_depth(std::min(h->persist_depth > 0 ? h->persist_depth : h->tb_depth, golk::max_depth_for(wpl)));
+    return largest_depth(std::min(h->persist_depth > 0 ? h->persist_depth : h->tb_depth, golk::persist_max_depth(wpl)));
 }
 
 // Torus: J super-steps of `depth` turns in one resident launch; returns the
@@ -1770,6 +1772,7 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     out->rows_per_wave = rows_per_wave_for(h, next_depth(h, h->tb_depth, halo));
     out->kernel_variant = h->W % 32 == 0 ? 1 : 0;
     out->words_per_lane = h->W % 32 == 0 ? wpl_for(h) : 0;
+    out->persist_depth = h->W % 32 == 0 ? persist_depth_for(h, wpl_for(h)) : 0;
     return GOLHIP_OK;
 }
 

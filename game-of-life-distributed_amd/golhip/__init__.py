@@ -52,6 +52,8 @@ class Perf(ctypes.Structure):
         ("flip_entries", ctypes.c_int64),
         ("flip_kernel_ms", ctypes.c_double),
         ("flip_fallbacks", ctypes.c_int64),
+        ("persist_depth", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
     ]
 
     def as_dict(self) -> dict:

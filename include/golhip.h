@@ -78,6 +78,9 @@ typedef struct golhip_perf {
     double flip_kernel_ms;    /* their summed device time (GOLHIP_FLAG_TIMING)   */
     int64_t flip_fallbacks;   /* flip batches re-run in ticket order (a block waited on a
                                  predecessor that was not resident)                */
+    int32_t persist_depth;    /* turns per super-step of the resident kernel (its
+                                 depths stop at 16 for two words per lane)       */
+    int32_t reserved0;
 } golhip_perf_t;
 
 /* ---- library ---------------------------------------------------------- */
@@ -109,7 +112,9 @@ int golhip_destroy(golhip_t h);
 int golhip_set_stream(golhip_t h, void *hip_stream);
 void *golhip_stream(golhip_t h);
 
-/* Tuning: turns fused per launch (1..GOLHIP_MAX_TB_DEPTH) and rows streamed
+/* Tuning: turns fused per launch (1..GOLHIP_MAX_TB_DEPTH, default 20; capped
+ * per kernel: 32 at one word per lane, 20 at two (16 for the resident
+ * kernel), 8 at four) and rows streamed
  * per wavefront (0 = automatic, the default: sized from the CU count and the
  * kernel's occupancy).  Results never depend on them. */
 int golhip_set_tb_depth(golhip_t h, int32_t turns);

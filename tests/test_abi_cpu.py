@@ -79,7 +79,8 @@ def test_halo_schedule(rows, tb, left, want):
 @pytest.mark.parametrize("rows,tb,left,want", [
     (65536, 16, 100, [(16, 4), (12, 3)]),          # not 6 x 16 + 4: no short tail launch
     (16384, 16, 40, [(16, 1), (12, 2)]),
-    (16384, 32, 100, [(32, 2), (24, 1), (12, 1)]),
+    (16384, 32, 100, [(32, 1), (24, 2), (20, 1)]),
+    (65536, 20, 1000, [(20, 6)] * 8 + [(20, 2)]),
     (16384, 16, 20, [(12, 1), (8, 1)]),
     (16384, 16, 7, [(6, 1), (1, 1)]),
     (65536, 8, 100, [(8, 11), (6, 2)]),              # quads: no 4-turn tail

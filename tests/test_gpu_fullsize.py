@@ -81,9 +81,9 @@ def test_config1_16384_10k_turns(full, opts):
 
 
 # ---------------------------------------------------------------- configs[2]
-@pytest.mark.parametrize("opts", [{}, {"wpl": 4}, {"persistent": 1}, {"wpl": 1, "tb_depth": 32}])
+@pytest.mark.parametrize("opts", [{}, {"tb_depth": 16}, {"wpl": 4}, {"persistent": 1}, {"wpl": 1, "tb_depth": 32}])
 def test_config2_65536_1k_turns(full, opts):
-    """configs[2]: 65536^2, 1,000 turns (default: per-launch kernels, 16-turn launches)."""
+    """configs[2]: 65536^2, 1,000 turns (default: per-launch kernels, 20-turn launches)."""
     run_checkpoints(full, "c2", **opts)
 
 

@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 golhip = pytest.importorskip("golhip")
 
 CHECKS = [(16, 0), (16, 1), (16, 100), (64, 0), (64, 1), (64, 100), (512, 0), (512, 1), (512, 100)]
-DEPTHS = [1, 2, 4, 6, 8, 12, 16, 24, 32]
+DEPTHS = [1, 2, 4, 6, 8, 12, 16, 20, 24, 32]
 
 
 @pytest.fixture(scope="module")
@@ -223,7 +223,7 @@ def test_depth_and_strip_height_invariance(fixtures, depth, rpw, fill_skip, wpl)
 
 @pytest.mark.parametrize("W,H", [(32, 1), (32, 3), (64, 2), (96, 7), (2016, 9), (1984, 33), (4000 - 4000 % 32, 40),
                                  (8192, 5), (320, 1000), (6272, 70), (7936, 20), (8064, 12), (128, 64)])
-@pytest.mark.parametrize("depth", [1, 8, 12, 32])
+@pytest.mark.parametrize("depth", [1, 8, 12, 20, 32])
 @pytest.mark.parametrize("wpl", [1, 2, 4])
 def test_random_shapes(W, H, depth, wpl):
     """Widths that are 1..many tiles (62 x wpl stored words/tile), heights below the depth."""
@@ -637,7 +637,7 @@ def test_persistent_paired_bands(coracle, N, rows, depth, wpl, nw, tx):
 
 @pytest.mark.parametrize("N,rows,depth,wpl,rpw", [(2048, 1024, 16, 1, 0), (4096, 2048, 16, 2, 0), (1984, 999, 8, 2, 37),
                                                   (3968, 1001, 4, 1, 5), (2048, 77, 2, 1, 3), (1024, 513, 32, 1, 50),
-                                                  (4096, 300, 1, 2, 7)])
+                                                  (4096, 300, 1, 2, 7), (4096, 2048, 20, 2, 0), (2048, 999, 20, 1, 37)])
 @pytest.mark.parametrize("paired", [1, 0])
 def test_per_launch_paired_bands(coracle, N, rows, depth, wpl, rpw, paired):
     """Per-launch kernel with SIMD mates meeting inside a two-band region (gol_tb_pair_kernel) vs the C oracle."""
