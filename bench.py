@@ -168,8 +168,9 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str) 
             perf["persist_turns"]
         depth = perf["persist_depth"]
     else:
-        kname, launches, kms, kturns = "gol_tb_pair_kernel", perf["step_launches"], perf["step_kernel_ms"], \
-            perf["step_turns"]
+        # split tiling (kernel_variant 2): a step launch is kernel A + kernel B
+        kname = "gol_split" if perf["kernel_variant"] == 2 else "gol_tb_pair_kernel"
+        launches, kms, kturns = perf["step_launches"], perf["step_kernel_ms"], perf["step_turns"]
         depth = perf["tb_depth"]
     launches = max(1, launches)
     avg_s = kms / launches * 1e-3
@@ -187,7 +188,8 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str) 
         "unit": "Gslot/s (wave64 VALU issue slots)",
         "frac": round(achieved / VALU_PEAK_GSLOTS, 4) if achieved else None,
         "traffic": None,
-        "kernel": f"{kname}<{depth}, {wpl}>",
+        "kernel": (f"gol_split_pair_kernel<{depth}, {wpl}> + gol_split_tri_kernel<{depth}, {wpl}>"
+                   if kname == "gol_split" else f"{kname}<{depth}, {wpl}>"),
         "avg_launch_ms": round(avg_s * 1e3, 5),
         "launches": launches,
         "turns_per_launch": tpl,

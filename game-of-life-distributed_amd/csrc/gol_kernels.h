@@ -55,6 +55,25 @@ int tb_wave_slots_per_cu(int depth, int wpl, bool paired);  // resident waves pe
 // Rows per wavefront minimising (rounds of waves) x (rows streamed per wave).
 int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_skip, int wpl, bool paired = false);
 
+// Split tiling (torus, per launch; gol_kernels.hip K1s): kernel A streams
+// regions of input rows from both ends and exports the edge rows of every
+// generation, kernel B computes the triangles between the bands.  Region q is
+// input rows [q H / nreg, (q + 1) H / nreg), each at least 2 P0 rows.
+struct SplitArgs {
+    StepArgs base;   // torus step: src, dst, W, Ww, rows_out = H, dst_base, in, alive
+    int nreg;        // regions
+    int tiles_x;
+    int P0;          // split_prefix_rows(depth)
+    uint32_t *exp;   // split_exp_words() words
+    int *meet;       // 2 * nreg * tiles_x: input rows each wave of a region streamed (U, L)
+};
+bool split_supported(int depth, int wpl);
+int split_prefix_rows(int depth);
+inline int64_t split_exp_words(int nreg, int tiles_x, int depth, int wpl) {
+    return (int64_t)nreg * tiles_x * 4 * (depth - 1) * 3 * 64 * wpl;
+}
+hipError_t launch_split(const SplitArgs &p, int depth, int wpl, hipStream_t s);
+
 // Persistent multi-super-step step kernel (torus, or a strip's extended rows
 // between two deep-halo exchanges); see gol_kernels.hip K1p.
 struct PersistArgs {

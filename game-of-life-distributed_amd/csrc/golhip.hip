@@ -110,6 +110,13 @@ struct golhip {
     int rows_per_wave = 0;      // 0 = automatic (per depth, from occupancy)
     int cu_count = 0;
     bool fill_skip = true;      // option "fill_skip"
+    int split = 1;              // option "split": split tiling (K1s) for per-launch torus steps
+                                // (65536^2 +1.3 %, 262144^2 +4.4 %, profiles/r2t/split_ab.jsonl)
+    uint32_t *split_exp = nullptr;  // K1s export rows
+    int64_t split_exp_cap = 0;      // words
+    int *split_meet = nullptr;      // K1s per-region wave row counts
+    int64_t split_meet_cap = 0;
+    bool last_split = false;        // the last step launch ran K1s
     int persistent = -1;        // option "persistent": K1p for long torus runs (1 on, 0 off, -1 auto)
     int wpl_opt = 0;            // option "wpl": words per lane (0 = auto, 1, 2, 4)
     int persist_depth = 0;      // option "persist_depth" (0: tb_depth)
@@ -524,6 +531,47 @@ void shift_rows(golk::StepArgs &a, int lo, int hi) {
     a.count_hi = -lo + rows;
 }
 
+// Split tiling (K1s, option "split"): whole-torus launches whose depth and
+// words per lane have an instance.  Regions of input rows, two waves each,
+// sized to fill the CUs' wave slots once (two per SIMD); each region needs
+// 2 (P0 + 3) rows (both waves' own prefix) plus a little to share.
+bool split_plan(golhip_t h, int depth, int wpl, golk::SplitArgs *sp) {
+    if (!h->split || h->W % 32 != 0 || !h->torus() || !golk::split_supported(depth, wpl)) return false;
+    const int tiles = golk::tb_tiles(h->Ww, wpl);
+    const int P0 = golk::split_prefix_rows(depth);
+    const int minlen = 2 * (P0 + 3) + 3;
+    const int pairs = std::max(1, h->cu_count * 4);  // two waves per SIMD
+    int nreg = std::max(1, pairs / tiles);
+    nreg = std::min(nreg, h->rows / minlen);
+    if (nreg < 1) return false;
+    sp->nreg = nreg;
+    sp->tiles_x = tiles;
+    sp->P0 = P0;
+    return true;
+}
+
+int split_buffers(golhip_t h, golk::SplitArgs &sp, int depth, int wpl) {
+    const int64_t words = golk::split_exp_words(sp.nreg, sp.tiles_x, depth, wpl);
+    if (words > h->split_exp_cap) {
+        HIP_OR_FAIL(hipFree(h->split_exp));
+        h->split_exp = nullptr;
+        h->split_exp_cap = 0;
+        HIP_OR_FAIL(hipMalloc(&h->split_exp, (size_t)words * 4));
+        h->split_exp_cap = words;
+    }
+    const int64_t nm = 2ll * sp.nreg * sp.tiles_x;
+    if (nm > h->split_meet_cap) {
+        HIP_OR_FAIL(hipFree(h->split_meet));
+        h->split_meet = nullptr;
+        h->split_meet_cap = 0;
+        HIP_OR_FAIL(hipMalloc(&h->split_meet, (size_t)nm * sizeof(int)));
+        h->split_meet_cap = nm;
+    }
+    sp.exp = h->split_exp;
+    sp.meet = h->split_meet;
+    return GOLHIP_OK;
+}
+
 // Launch the step kernel for output rows [lo, hi) of this handle (halos, if
 // used, already in place); `alive` (nullable) accumulates their popcount.
 // No bookkeeping: see finish_launch.
@@ -551,10 +599,18 @@ int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int
         HIP_OR_FAIL(hipEventRecord(e0, st));
     }
     hipError_t e;
-    if (h->W % 32 == 0)
+    golk::SplitArgs sp{};
+    const bool split = !halo && a.rows_out == h->rows && split_plan(h, depth, wpl, &sp);
+    if (split) {
+        sp.base = a;
+        if (int rc = split_buffers(h, sp, depth, wpl)) return rc;
+        e = golk::launch_split(sp, depth, wpl, st);
+    } else if (h->W % 32 == 0) {
         e = golk::launch_step_tb(a, depth, st, h->fill_skip, wpl, tb_paired(h));
-    else
+    } else {
         e = golk::launch_step_generic(a, st);
+    }
+    h->last_split = split;
     if (e != hipSuccess) return fail(GOLHIP_EHIP, "step launch: %s", hipGetErrorString(e));
     if (e1) {
         HIP_OR_FAIL(hipEventRecord(e1, st));
@@ -1182,6 +1238,8 @@ int golhip_destroy(golhip_t h) {
     HIP_RC(hipFree(h->d_sync));
     HIP_RC(hipFree(h->d_trace));
     HIP_RC(hipFree(h->backup));
+    HIP_RC(hipFree(h->split_exp));
+    HIP_RC(hipFree(h->split_meet));
     if (h->h_err) HIP_RC(hipHostFree(h->h_err));
     if (h->own_stream && h->stream) HIP_RC(hipStreamDestroy(h->stream));
     delete h;
@@ -1299,6 +1357,11 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     if (!strcmp(key, "fill_skip")) {
         h->fill_skip = value != 0;
         for (int &c : h->auto_rpw) c = 0;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "split")) {
+        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "split %lld", (long long)value);
+        h->split = (int)value;
         return GOLHIP_OK;
     }
     return fail(GOLHIP_EINVAL, "unknown option %s", key);
@@ -1770,7 +1833,7 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     const bool halo = h->comm && (h->nranks > 1 || h->force_halo);
     out->tb_depth = depth_cap(h, halo);
     out->rows_per_wave = rows_per_wave_for(h, next_depth(h, h->tb_depth, halo));
-    out->kernel_variant = h->W % 32 == 0 ? 1 : 0;
+    out->kernel_variant = h->W % 32 != 0 ? 0 : h->last_split ? 2 : 1;
     out->words_per_lane = h->W % 32 == 0 ? wpl_for(h) : 0;
     out->persist_depth = h->W % 32 == 0 ? persist_depth_for(h, wpl_for(h)) : 0;
     return GOLHIP_OK;

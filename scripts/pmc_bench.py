@@ -22,7 +22,7 @@ import sys
 
 src, dst = sys.argv[1], sys.argv[2]
 out = json.load(open(dst)) if os.path.exists(dst) else {}
-FAMILIES = ("gol_persist_kernel", "gol_tb_pair_kernel")
+FAMILIES = ("gol_persist_kernel", "gol_tb_pair_kernel", "gol_split_pair_kernel", "gol_split_tri_kernel")
 
 for d in sorted(glob.glob(os.path.join(src, "pmc_*_*"))):
     if not os.path.isdir(d):
@@ -45,7 +45,7 @@ for d in sorted(glob.glob(os.path.join(src, "pmc_*_*"))):
             rec = out.setdefault(f"{wl}:{fam}", {"_vals": {}, "_durs": []})
             rec.setdefault("_vals", {}).setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
             rec.setdefault("_durs", []).append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
-            if bench and bench["roofline"]["kernel"].startswith(fam):
+            if bench and fam in bench["roofline"]["kernel"]:
                 rec["turns_per_launch"] = bench["roofline"]["turns_per_launch"]
                 rec["bench_kernel"] = bench["roofline"]["kernel"]
 
@@ -71,5 +71,20 @@ for key, rec in list(out.items()):
             rec["clock_ghz_est"] = statistics.mean(vals["GRBM_GUI_ACTIVE"]) / 8 / dur / 1e9
     rec["note"] = ("rocprofv3 --pmc passes of bench.py (scripts/pmc_bench.sh), one counter group per pass; "
                    "FETCH_SIZE x2 per the gfx950 correction; Infinity-Cache hits are counted")
+# split tiling: one step launch is kernel A + kernel B (one dispatch of each)
+for key in [k for k in out if k.endswith(":gol_split_pair_kernel")]:
+    wl = key.split(":")[0]
+    a, b = out[key], out.get(f"{wl}:gol_split_tri_kernel")
+    if not b:
+        continue
+    rec = {"parts": ["gol_split_pair_kernel", "gol_split_tri_kernel"], "note": a.get("note"),
+           "turns_per_launch": a.get("turns_per_launch"), "bench_kernel": a.get("bench_kernel")}
+    for f in ("hbm_bytes_per_launch", "fetch_bytes_corrected", "write_bytes", "sq_insts_valu", "sq_insts_salu"):
+        if f in a and f in b:
+            rec[f] = a[f] + b[f]
+    if "valu_active_frac" in a:
+        rec["valu_active_frac"] = a["valu_active_frac"]
+        rec["clock_ghz_est"] = a.get("clock_ghz_est")
+    out[f"{wl}:gol_split"] = rec
 json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
 print(json.dumps(out, indent=1))

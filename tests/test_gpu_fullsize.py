@@ -81,9 +81,11 @@ def test_config1_16384_10k_turns(full, opts):
 
 
 # ---------------------------------------------------------------- configs[2]
-@pytest.mark.parametrize("opts", [{}, {"tb_depth": 16}, {"wpl": 4}, {"persistent": 1}, {"wpl": 1, "tb_depth": 32}])
+@pytest.mark.parametrize("opts", [{}, {"split": 0}, {"tb_depth": 16}, {"wpl": 4}, {"persistent": 1},
+                                  {"wpl": 1, "tb_depth": 32}])
 def test_config2_65536_1k_turns(full, opts):
-    """configs[2]: 65536^2, 1,000 turns (default: per-launch kernels, 20-turn launches)."""
+    """configs[2]: 65536^2, 1,000 turns (default: split tiling, 20-turn launches; split 0: the
+    overlapped paired-band kernel)."""
     run_checkpoints(full, "c2", **opts)
 
 
@@ -130,7 +132,7 @@ def test_config2_rccl_ring_one_rank(full, persistent):
 
 # ---------------------------------------------------------------- configs[3]
 @pytest.mark.parametrize("opts", [{}, {"wpl": 2}])
-def test_config3_262144_100_turns(full, opts):
+def test_config3_262144_100_turns(full, opts):  # default: split tiling
     """configs[3]: the whole 262144^2 board on one GPU, 100 turns (default:
     four words per lane, 8-turn launches)."""
     run_checkpoints(full, "c3", **opts)
