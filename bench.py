@@ -168,8 +168,10 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str) 
             perf["persist_turns"]
         depth = perf["persist_depth"]
     else:
-        # split tiling (kernel_variant 2): a step launch is kernel A + kernel B
-        kname = "gol_split" if perf["kernel_variant"] == 2 else "gol_tb_pair_kernel"
+        # split tiling: a step launch is kernel A + kernel B; named after the
+        # family that ran most of the step launches (262144^2 x 100 turns =
+        # 11 split launches of 8 turns + 2 paired-band launches of 6)
+        kname = "gol_split" if 2 * perf.get("split_launches", 0) > perf["step_launches"] else "gol_tb_pair_kernel"
         launches, kms, kturns = perf["step_launches"], perf["step_kernel_ms"], perf["step_turns"]
         depth = perf["tb_depth"]
     launches = max(1, launches)
@@ -192,6 +194,7 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str) 
                    if kname == "gol_split" else f"{kname}<{depth}, {wpl}>"),
         "avg_launch_ms": round(avg_s * 1e3, 5),
         "launches": launches,
+        "split_launches": perf.get("split_launches", 0),
         "turns_per_launch": tpl,
         "slots_per_word_turn": spw,
         "alg_bytes_per_launch": alg_bytes,

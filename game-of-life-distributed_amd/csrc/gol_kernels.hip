@@ -19,6 +19,9 @@
 #include <type_traits>
 
 namespace golk {
+#ifndef GOL_LOOP_PAD
+#define GOL_LOOP_PAD 0  // code-layout experiments: 4-byte s_nop pads ahead of the main loops (profiles/r2la)
+#endif
 
 // ---------------------------------------------------------------------------
 // bit-sliced helpers
@@ -321,6 +324,31 @@ __device__ __forceinline__ void stage(int t, Lanes<WPL> &x, uint32_t (&h0)[3][D]
     }
 }
 
+// Code layout.  On gfx950 the step kernels' 8-byte VALU instructions issue
+// ~20 % faster at addresses = 4 (mod 8) than at 0 (mod 8): the same kernel
+// shifted by one 4-byte instruction runs 65536^2 at 97 instead of 120 TCUPS,
+// 262144^2 110 vs 133, 16384^2 52.5 vs 61.9 (profiles/r2la, same box).  The
+// compiler does not track this, and every odd run of 4-byte instructions
+// (SALU, s_waitcnt, s_nop hazard pads, VOP1/VOP2) flips the parity of all
+// code after it.  parity_fix re-anchors it: `.p2align 3` then one s_nop puts
+// the next instruction at 4 (mod 8) whatever came before (one or two
+// s_nops executed), once per 3-row group (pinned by sched barriers; 2 =
+// every pipeline step as well, which the hazard pads then mis-anchor).  The
+// tree before it happened to sit on the fast parity in every main loop; the
+// fix keeps it there whatever changes upstream of a loop (scripts/
+// loop_parity.py reports the parity of every hot loop of a build).
+#ifndef GOL_PARITY_FIX
+#define GOL_PARITY_FIX 1  // profiles/r2lc: 16384^2 +1.2 %, the others within 0.6 % of the lucky layout
+#endif
+template <int LEVEL>
+__device__ __forceinline__ void parity_fix() {
+    if constexpr (GOL_PARITY_FIX >= LEVEL) {  // pinned: nothing is scheduled across it
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile(".p2align 3\n\ts_nop 0");
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // A group of 3 consecutive input rows through the first A of the D stages.
 // Stage t of row i+1 needs stage t of row i (its row sum), so the rows run
 // skewed by one stage: (row0, t), (row1, t-1), (row2, t-2) are independent and
@@ -331,8 +359,10 @@ template <int D, int A, int WPL>
 __device__ __forceinline__ void push_group(Lanes<WPL> &x0, Lanes<WPL> &x1, Lanes<WPL> &x2,
                                            uint32_t (&h0)[3][D][WPL], uint32_t (&h1)[3][D][WPL],
                                            uint32_t (&cc)[3][D][WPL]) {
+    parity_fix<1>();
 #pragma unroll
     for (int s = 0; s < A + 2; ++s) {
+        parity_fix<2>();
         if (s < A) stage<D, 0, WPL>(s, x0, h0, h1, cc);
         if (s >= 1 && s - 1 < A) stage<D, 1, WPL>(s - 1, x1, h0, h1, cc);
         if (s >= 2 && s - 2 < A) stage<D, 2, WPL>(s - 2, x2, h0, h1, cc);
@@ -604,6 +634,7 @@ __device__ __forceinline__ uint32_t stream_band(const StepArgs &a, int r0, int r
         }
         return cnt;
     }
+    for (int i = 0; i < GOL_LOOP_PAD; ++i) asm volatile("s_nop 0");
     for (; claim ? more : oi < rows_here; oi += 3) {
         if (STORE == kStoreDeferred && pend) {
             emit(q0, qoi);
@@ -844,8 +875,10 @@ template <int D, int A, int WPL, typename Hook>
 __device__ __forceinline__ void push_group_exp(Lanes<WPL> &x0, Lanes<WPL> &x1, Lanes<WPL> &x2,
                                                uint32_t (&h0)[3][D][WPL], uint32_t (&h1)[3][D][WPL],
                                                uint32_t (&cc)[3][D][WPL], int ii0, Hook &&hook) {
+    parity_fix<1>();
 #pragma unroll
     for (int s = 0; s < A + 2; ++s) {
+        parity_fix<2>();
         if (s < A) {
             hook(s, ii0, x0);
             stage<D, 0, WPL>(s, x0, h0, h1, cc);
@@ -989,6 +1022,7 @@ __device__ __forceinline__ uint32_t stream_split(const SplitArgs &p, int region,
 #pragma unroll
     for (int k = 0; k < WPL; ++k) q0.w[k] = q1.w[k] = q2.w[k] = 0u;
     int qoi = -8;  // the first body stores nothing real
+    for (int i = 0; i < GOL_LOOP_PAD; ++i) asm volatile("s_nop 0");
     for (;;) {
         const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
         emit(q0, qoi);

@@ -187,7 +187,7 @@ struct golhip {
     };
     std::vector<Timed> ev_pending;
     double step_ms = 0, persist_ms = 0;
-    int64_t step_launches = 0, step_turns = 0, halo_bytes = 0;
+    int64_t step_launches = 0, step_turns = 0, halo_bytes = 0, split_launches = 0;
     int64_t persist_turns = 0;
 
     std::mutex mu;
@@ -621,6 +621,7 @@ int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int
         }
     }
     h->step_launches++;
+    h->split_launches += split;
     return GOLHIP_OK;
 }
 
@@ -1817,6 +1818,7 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     memset(out, 0, sizeof *out);
     out->turns = h->turns;
     out->step_launches = h->step_launches;
+    out->split_launches = h->split_launches;
     out->step_turns = h->step_turns;
     out->step_kernel_ms = h->step_ms;
     out->persist_launches = h->persist_launches;
@@ -1869,7 +1871,7 @@ int golhip_perf_reset(golhip_t h) {
     if (int rc = set_dev(h)) return rc;
     if (int rc = drain_events(h)) return rc;
     h->step_ms = h->persist_ms = 0;
-    h->step_launches = h->step_turns = h->halo_bytes = 0;
+    h->step_launches = h->step_turns = h->halo_bytes = h->split_launches = 0;
     h->persist_launches = h->persist_turns = 0;
     h->flip_launches = h->flip_entries = 0;
     h->flip_ms = 0;

@@ -54,6 +54,7 @@ class Perf(ctypes.Structure):
         ("flip_fallbacks", ctypes.c_int64),
         ("persist_depth", ctypes.c_int32),
         ("reserved0", ctypes.c_int32),
+        ("split_launches", ctypes.c_int64),
     ]
 
     def as_dict(self) -> dict:

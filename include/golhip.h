@@ -81,6 +81,8 @@ typedef struct golhip_perf {
     int32_t persist_depth;    /* turns per super-step of the resident kernel (its
                                  depths stop at 16 for two words per lane)       */
     int32_t reserved0;
+    int64_t split_launches;   /* of step_launches, those that ran split tiling
+                                 (gol_split_pair_kernel + gol_split_tri_kernel) */
 } golhip_perf_t;
 
 /* ---- library ---------------------------------------------------------- */
