@@ -46,6 +46,45 @@ def kernels(lines):
         yield name, body
 
 
+def loops(body):
+    """(start, end, Counter) of every loop (backward branch) in a kernel's disassembly."""
+    ins = []
+    for l in body:
+        m = re.search(r"// ([0-9A-F]+): [0-9A-F]+( [0-9A-F]+)?", l)
+        if m:
+            ins.append((int(m.group(1), 16), 8 if m.group(2) else 4, l.split("//")[0].strip()))
+    out = []
+    for addr, size, txt in ins:
+        m = re.match(r"(s_cbranch_\w+|s_branch)\s+(\d+)", txt)
+        if not m:
+            continue
+        off = int(m.group(2))
+        off = off - 65536 if off >= 32768 else off
+        if off >= 0:
+            continue
+        tgt = addr + 4 + 4 * off
+        out.append((tgt, addr, collections.Counter(f"b8@{x % 8}" if s == 8 else "b4"
+                                                   for x, s, _ in ins if tgt <= x <= addr)))
+    return ins, out
+
+
+def main_loop_parity(lines, kernel):
+    """Good-parity fraction of the kernel's main loop: the last innermost loop
+    (no loop of >= 100 dwords inside it) with >= 500 8-byte instructions (the
+    stream loops' main loop follows their fill loops)."""
+    for name, body in kernels(lines):
+        if kernel not in name:
+            continue
+        ins, lps = loops(body)
+        inner = [l for l in lps if not any(o is not l and l[0] <= o[0] and o[1] <= l[1] and (o[1] - o[0]) >= 400
+                                           for o in lps)]
+        big = [l for l in inner if l[2]["b8@4"] + l[2]["b8@0"] >= 500]
+        best = max(big, key=lambda l: l[0])
+        c = best[2]
+        return c["b8@4"] / max(1, c["b8@4"] + c["b8@0"]), c["b8@4"] + c["b8@0"]
+    raise KeyError(kernel)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("lib")
