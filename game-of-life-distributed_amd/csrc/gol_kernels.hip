@@ -1403,8 +1403,8 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
 
 // ---- host-side dispatch over (depth, fill skip, words per lane) ----------
 // Depths 1, 2, 4, 6, 8, 12, 16, 20 (and 24, 32 for WPL = 1: depth 24 at
-// WPL = 2 would exceed 256 VGPRs; WPL = 4 stops at 8); the host's depth_plan
-// picks among them.
+// WPL = 2 would exceed 256 VGPRs; WPL = 4 stops at 9, an extra depth of its
+// own); the host's depth_plan picks among them.
 template <typename F>
 static hipError_t dispatch(int depth, bool skip, int wpl, F &&f) {
 #define GOL_CASE(D, SK, WP) \
@@ -1414,8 +1414,8 @@ static hipError_t dispatch(int depth, bool skip, int wpl, F &&f) {
     GOL_CASE(16, false, 1) GOL_CASE(32, false, 1)
     GOL_CASE(12, true, 1) GOL_CASE(24, true, 1) GOL_CASE(12, false, 1) GOL_CASE(24, false, 1)
     GOL_CASE(12, true, 2) GOL_CASE(12, false, 2)
-    GOL_CASE(1, true, 4) GOL_CASE(2, true, 4) GOL_CASE(4, true, 4) GOL_CASE(8, true, 4)
-    GOL_CASE(1, false, 4) GOL_CASE(2, false, 4) GOL_CASE(4, false, 4) GOL_CASE(8, false, 4)
+    GOL_CASE(1, true, 4) GOL_CASE(2, true, 4) GOL_CASE(4, true, 4) GOL_CASE(8, true, 4) GOL_CASE(9, true, 4)
+    GOL_CASE(1, false, 4) GOL_CASE(2, false, 4) GOL_CASE(4, false, 4) GOL_CASE(8, false, 4) GOL_CASE(9, false, 4)
     GOL_CASE(6, true, 1) GOL_CASE(6, false, 1) GOL_CASE(6, true, 2) GOL_CASE(6, false, 2)
     GOL_CASE(6, true, 4) GOL_CASE(6, false, 4)
     GOL_CASE(1, true, 2) GOL_CASE(2, true, 2) GOL_CASE(4, true, 2) GOL_CASE(8, true, 2) GOL_CASE(16, true, 2)
@@ -1426,8 +1426,10 @@ static hipError_t dispatch(int depth, bool skip, int wpl, F &&f) {
 }
 
 // Per-launch kernels: WPL 2 fits 20 stages in 242 VGPRs (two waves per SIMD,
-// no scratch); the resident kernel keeps 16 (its instantiations).
-int max_depth_for(int wpl) { return wpl == 4 ? 8 : wpl == 2 ? 20 : 32; }
+// no scratch), WPL 4 nine in 248-250 (depth 9 exists for quads only: the host
+// plans it only under a cap of exactly 9, see depth_cap); the resident kernel
+// keeps 16 / 8 (its instantiations).
+int max_depth_for(int wpl) { return wpl == 4 ? 9 : wpl == 2 ? 20 : 32; }
 int persist_max_depth(int wpl) { return wpl == 4 ? 8 : wpl == 2 ? 16 : 32; }
 
 int tb_tiles(int Ww, int wpl) { return (Ww + tile_words(wpl) - 1) / tile_words(wpl); }
@@ -1444,7 +1446,7 @@ static hipError_t dispatch_pair(int depth, int wpl, F &&f, bool cnt = false) {
     GOL_QCASE(1, 1) GOL_QCASE(2, 1) GOL_QCASE(4, 1) GOL_QCASE(8, 1) GOL_QCASE(16, 1) GOL_QCASE(32, 1)
     GOL_QCASE(1, 2) GOL_QCASE(2, 2) GOL_QCASE(4, 2) GOL_QCASE(8, 2) GOL_QCASE(16, 2)
     GOL_QCASE(12, 1) GOL_QCASE(24, 1) GOL_QCASE(12, 2) GOL_QCASE(1, 4) GOL_QCASE(2, 4) GOL_QCASE(4, 4) GOL_QCASE(8, 4)
-    GOL_QCASE(6, 1) GOL_QCASE(6, 2) GOL_QCASE(6, 4) GOL_QCASE(20, 1) GOL_QCASE(20, 2)
+    GOL_QCASE(6, 1) GOL_QCASE(6, 2) GOL_QCASE(6, 4) GOL_QCASE(9, 4) GOL_QCASE(20, 1) GOL_QCASE(20, 2)
 #undef GOL_QCASE
     return hipErrorInvalidValue;
 }
@@ -1474,7 +1476,7 @@ hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s, bool fill
 }
 
 bool split_supported(int depth, int wpl) {
-    return (wpl == 2 && (depth == 8 || depth == 12 || depth == 16 || depth == 20)) || (wpl == 4 && depth == 8) ||
+    return (wpl == 2 && (depth == 8 || depth == 12 || depth == 16 || depth == 20)) || (wpl == 4 && (depth == 8 || depth == 9)) ||
            (wpl == 1 && (depth == 16 || depth == 32));
 }
 int split_prefix_rows(int depth) { return split_prefix(depth); }
@@ -1490,7 +1492,7 @@ hipError_t launch_split(const SplitArgs &p, int depth, int wpl, hipStream_t s) {
         hipLaunchKernelGGL((gol_split_tri_kernel<D, WP>), gb, dim3(256), 0, s, p); \
         return hipGetLastError();                                           \
     }
-    GOL_SCASE(8, 2) GOL_SCASE(12, 2) GOL_SCASE(16, 2) GOL_SCASE(20, 2) GOL_SCASE(8, 4) GOL_SCASE(16, 1)
+    GOL_SCASE(8, 2) GOL_SCASE(12, 2) GOL_SCASE(16, 2) GOL_SCASE(20, 2) GOL_SCASE(8, 4) GOL_SCASE(9, 4) GOL_SCASE(16, 1)
     GOL_SCASE(32, 1)
 #undef GOL_SCASE
     return hipErrorInvalidValue;

@@ -85,8 +85,9 @@ int fail(int code, const char *fmt, ...) {
     } while (0)
 
 // Turns per launch with an instantiated step kernel (24: one word per lane
-// only, as 32; see max_depth_for).
-constexpr int kDepths[] = {32, 24, 20, 16, 12, 8, 6, 4, 2, 1};
+// only, as 32; 9: four words per lane only, planned only under a cap of
+// exactly 9 (depth_cap); see max_depth_for).
+constexpr int kDepths[] = {32, 24, 20, 16, 12, 9, 8, 6, 4, 2, 1};
 constexpr int kNumDepths = sizeof(kDepths) / sizeof(kDepths[0]);
 // trace buffer: 8 totals + (start, end) per (workgroup < 1024, wave < 64)
 constexpr int64_t kTraceWords = 8 + 2 * 1024 * 64;
@@ -250,9 +251,11 @@ int64_t stage_rows(golhip_t h) {
     return std::min<int64_t>(per, h->rows);
 }
 
+// Depth 9 (quads only) is never a "largest depth": the resident kernels and
+// the other word widths have no 9.
 int largest_depth(int64_t want) {
     for (int d : kDepths)
-        if (d <= want) return d;
+        if (d <= want && d != 9) return d;
     return 1;
 }
 
@@ -268,7 +271,7 @@ struct DepthRun {
     int64_t n;
 };
 DepthRun depth_plan(int cap, int64_t left) {
-    const int M = largest_depth(std::max(1, cap));
+    const int M = cap == 9 ? 9 : largest_depth(std::max(1, cap));  // 9: quads (depth_cap)
     if (left <= 0) return {M, 0};
     const int64_t head = std::max<int64_t>(0, left / M - 3);  // launches of M before the planned tail
     const int t = (int)(left - head * M);                     // < 4 M <= 128
@@ -278,7 +281,7 @@ DepthRun depth_plan(int cap, int64_t left) {
     mn[0] = INT_MAX;
     for (int v = 1; v <= t; ++v)
         for (int d : kDepths) {  // descending: ties keep the larger depth
-            if (d > M || d > v || nl[v - d] == INT_MAX) continue;
+            if (d > M || d > v || nl[v - d] == INT_MAX || (d == 9 && M != 9)) continue;
             const int n = nl[v - d] + 1, m = std::min(mn[v - d], d);
             if (n < nl[v] || (n == nl[v] && m > mn[v])) {
                 nl[v] = n;
@@ -407,6 +410,7 @@ int depth_cap(golhip_t h, bool halo) {
     const int wpl = wpl_for(h);
     int cap = std::min(h->tb_depth, (halo && persist_on(h)) ? golk::persist_max_depth(wpl) : golk::max_depth_for(wpl));
     if (halo) cap = std::min(cap, sched_rows(h));
+    if (cap == 9 && (wpl != 4 || (halo && persist_on(h)))) cap = 8;  // only per-launch quads have 9
     return cap;
 }
 

@@ -44,7 +44,7 @@ def run_split(board, turns, depth, wpl, rows_per_wave=0):
         return out, p
 
 
-SPLIT = [(8, 2), (12, 2), (16, 2), (20, 2), (8, 4), (16, 1), (32, 1)]
+SPLIT = [(8, 2), (12, 2), (16, 2), (20, 2), (8, 4), (9, 4), (16, 1), (32, 1)]
 
 
 @pytest.mark.parametrize("depth,wpl", SPLIT)
@@ -73,7 +73,7 @@ def test_split_single_region(coracle, depth, wpl):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("depth,wpl", [(16, 2), (20, 2), (8, 4)])
+@pytest.mark.parametrize("depth,wpl", [(16, 2), (20, 2), (8, 4), (9, 4)])
 @pytest.mark.parametrize("H", [4096 + 1, 4096 + 2, 4096 + 3, 5000])
 def test_split_many_regions_every_remainder(coracle, depth, wpl, H):
     """Region lengths of every residue mod 3 (the meeting claims end in 1-, 2- and 3-row grants)."""
