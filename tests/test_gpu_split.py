@@ -57,6 +57,7 @@ def test_split_matches_oracle(coracle, depth, wpl, W, H):
     want = coracle.run(board, turns)
     got, p = run_split(board, turns, depth, wpl)
     assert p["kernel_variant"] in (1, 2)
+    assert 1 <= p["split_launches"] <= p["step_launches"]  # the full-depth launches split, the remainder may not
     assert np.array_equal(got, want)
 
 
@@ -90,7 +91,7 @@ def test_split_falls_back_below_one_region(coracle):
     board = coracle.fill_random(1024, 40, 0x5EED0024)
     want = coracle.run(board, 60)
     got, p = run_split(board, 60, 20, 2)
-    assert p["kernel_variant"] == 1
+    assert p["kernel_variant"] == 1 and p["split_launches"] == 0
     assert np.array_equal(got, want)
 
 
