@@ -67,9 +67,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--warmup-seconds", type=float, default=0.5,
+    ap.add_argument("--warmup-seconds", type=float, default=3.0,
                     help="keep warming up (untimed) until this much wall time has passed: a first run on an idle "
-                         "GPU is ~4 %% slower for its first second (clock ramp, first touch of the buffers)")
+                         "GPU is ~4 %% slower for its first second (clock ramp, first touch of the buffers); 3 s "
+                         "also keeps the GPU visibly busy for an outside utilisation sampler (BENCH_r01: 0/3 "
+                         "samples saw the 0.6 s of GPU work beside the 10 s CPU baseline)")
     ap.add_argument("--workload", type=int, default=65536, choices=sorted(WORKLOADS))
     ap.add_argument("--turns-per-step", type=int, default=None,
                     help="default: the config's turns (parity is only checked then)")
