@@ -878,7 +878,9 @@ __device__ __forceinline__ void push_group_exp(Lanes<WPL> &x0, Lanes<WPL> &x1, L
     parity_fix<1>();
 #pragma unroll
     for (int s = 0; s < A + 2; ++s) {
-        parity_fix<2>();
+        // every step: the hook's export stores (4-byte SALU address work) flip
+        // the parity; 65536^2 +0.5 %, quads -0.5 % (profiles/r2pf), so pairs only
+        if constexpr (WPL <= 2) parity_fix<1>();
         if (s < A) {
             hook(s, ii0, x0);
             stage<D, 0, WPL>(s, x0, h0, h1, cc);
