@@ -173,7 +173,8 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str) 
         # split tiling: a step launch is kernel A + kernel B; named after the
         # family that ran most of the step launches (262144^2 x 100 turns =
         # 11 split launches of 8 turns + 2 paired-band launches of 6)
-        kname = "gol_split" if 2 * perf.get("split_launches", 0) > perf["step_launches"] else "gol_tb_pair_kernel"
+        kname = ("gol_skew_kernel" if 2 * perf.get("skew_launches", 0) > perf["step_launches"] else
+                 "gol_split" if 2 * perf.get("split_launches", 0) > perf["step_launches"] else "gol_tb_pair_kernel")
         launches, kms, kturns = perf["step_launches"], perf["step_kernel_ms"], perf["step_turns"]
         depth = perf["tb_depth"]
     launches = max(1, launches)
@@ -197,6 +198,7 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str) 
         "avg_launch_ms": round(avg_s * 1e3, 5),
         "launches": launches,
         "split_launches": perf.get("split_launches", 0),
+        "skew_launches": perf.get("skew_launches", 0),
         "turns_per_launch": tpl,
         "slots_per_word_turn": spw,
         "alg_bytes_per_launch": alg_bytes,

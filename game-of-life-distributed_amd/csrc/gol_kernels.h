@@ -74,6 +74,29 @@ inline int64_t split_exp_words(int nreg, int tiles_x, int depth, int wpl) {
 }
 hipError_t launch_split(const SplitArgs &p, int depth, int wpl, hipStream_t s);
 
+// Skewed band stacks (K1w, gol_kernels.hip; torus and row strips, per
+// launch).  Output rows [0, base.rows_out) of the StepArgs frame come from
+// input rows [-D, rows_out + D) through base.in.  The input rows
+// [-D, rows_out - D) split into nst stacks per tile column, one workgroup of
+// 8 waves each = tx tiles x (8 / tx) bands; a band [a, e) of input rows owns
+// generation g of the rows [a + g, e + g) (a parallelogram), so only the
+// band below it feeds it (through LDS, from the top of that band's pipeline
+// fill) and the stack's bottom band computes its own drain from the board.
+struct SkewArgs {
+    StepArgs base;
+    int tiles_x;
+    int tx;           // tiles per workgroup: 1 (stacks of 8 bands) or 2 (stacks of 4)
+    int nst;          // stacks per tile column
+    int wgt[8];       // band heights by stack position (relative weights)
+    int hcap;         // rows the stack's bottom band gives up (its drain is computed in full)
+    int prio_young;   // 1: s_setprio 1 for waves 4..7 (the SIMD arbiter's age losers)
+    unsigned *error;  // nullable, host-mapped: set if a band's imports never arrived (spin bound)
+    unsigned long long *trace;  // nullable diagnostics: per wave (start, end) s_memrealtime at 8 + 2 (block * 64 + wave)
+};
+bool skew_supported(int depth, int wpl);
+int skew_blocks_per_cu(int depth, int wpl);
+hipError_t launch_skew(const SkewArgs &p, int depth, int wpl, hipStream_t s);
+
 // Persistent multi-super-step step kernel (torus, or a strip's extended rows
 // between two deep-halo exchanges); see gol_kernels.hip K1p.
 struct PersistArgs {

@@ -1240,6 +1240,298 @@ __global__ __launch_bounds__(256) void gol_split_tri_kernel(SplitArgs p) {
 }
 
 // ---------------------------------------------------------------------------
+// K1w: skewed band stacks (round 3; torus and row strips, per launch).
+//
+// K1 computes the D-turn trapezoid at both ends of every band (~1.25 D^2
+// extra stage-rows a band); K1s computes every stage-row once but leaves the
+// triangles between bands to a second, latency-bound kernel.  K1w skews
+// the bands instead: band [a, e) of input rows owns generation g of the rows
+// [a + g, e + g).  Generation g + 1 of its rows needs generation g of
+// [a + g, e + g + 1]: its own rows and, at the bottom, the first two rows of
+// the band below it -- rows that band computes first, in its pipeline fill.
+// So no band needs anything from above, the band below hands over its top
+// rows early, and nobody computes a triangle.
+//
+// Pipeline (as stream_band): at push j (generation-0 row j entering), stage s
+// receives generation s of row j - s and emits generation s + 1 of row
+// j - s - 1; the band needs stage s at the pushes j in [a + 2 s + 2,
+// e + 2 s + 2), gen D goes out at j in [a + 2 D, e + 2 D).  Pushes run in
+// groups of 3 rows from a:
+//  * fill (j - a < 2 D): stages [0, A) only (phases A = D/4, D/2, 3D/4, D),
+//    exporting to LDS generation P of the rows a + P + m (the input of stage
+//    P at push a + 2 P + m) for the drain phases P = D/4, D/2, 3D/4 of the
+//    band above;
+//  * main: all stages on board rows, until the drain;
+//  * drain (d = j - e in [2 P, 2 P')): only stages [P, D) are needed; their
+//    input is generation P of row e + d - P, the band below's export (its
+//    rows a' + P + m, a' = e).  A group runs in the phase of its first row,
+//    so each phase exports 2 rows beyond its pushes.  The drain computes
+//    1.25 D^2 stage-rows instead of the exact D^2 (the triangle).
+// A stack of bands is one workgroup of one tile column (LDS hand-offs only,
+// no cross-workgroup wait); its bottom band has no band below in the
+// workgroup and computes its drain in full from board rows (2 D^2), so it
+// is shorter by `hcap` rows.  Torus: the input rows [-D, H - D) produce
+// generation D of [0, H) without wrapping the output; row strips: the
+// halo rows feed the top band's first D rows and the bottom band's drain.
+// ---------------------------------------------------------------------------
+template <int D>
+struct SkewPlan {
+    static constexpr int P1 = D / 4, P2 = D / 2, P3 = 3 * D / 4;
+    // import rows per drain phase: a group starting in phase 1 or 2 may end
+    // two rows into the next one; phase 3 clamps (rows past the drain)
+    static constexpr int N1 = 2 * (P2 - P1) + 2, N2 = 2 * (P3 - P2) + 2, N3 = 2 * (D - P3);
+    static constexpr int B1 = 0, B2 = N1, B3 = N1 + N2;
+    static constexpr int NEXP = N1 + N2 + N3;  // row NEXP of a wave's LDS slot = dummy (fill rows not exported)
+    static_assert(P1 >= 1, "skew depth >= 4");
+};
+
+// push_group for the last stages only: the group's rows enter stage LO.
+template <int D, int LO, int WPL>
+__device__ __forceinline__ void push_group_hi(Lanes<WPL> &x0, Lanes<WPL> &x1, Lanes<WPL> &x2,
+                                              uint32_t (&h0)[3][D][WPL], uint32_t (&h1)[3][D][WPL],
+                                              uint32_t (&cc)[3][D][WPL]) {
+    parity_fix<1>();
+#pragma unroll
+    for (int s = LO; s < D + 2; ++s) {
+        parity_fix<2>();
+        if (s < D) stage<D, 0, WPL>(s, x0, h0, h1, cc);
+        if (s - 1 >= LO && s - 1 < D) stage<D, 1, WPL>(s - 1, x1, h0, h1, cc);
+        if (s - 2 >= LO) stage<D, 2, WPL>(s - 2, x2, h0, h1, cc);
+    }
+}
+
+// One band [ab, eb) of input rows (StepArgs frame) of tile `tile`.  self: no
+// band below in the workgroup (compute the drain from board rows).  Exports
+// go to exp_mine (LDS slot of this wave), imports come from exp_next.
+template <int D, int WPL>
+__device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int eb, int tile, bool self,
+                                                uint32_t *exp_mine, const uint32_t *exp_next, int *flag_mine,
+                                                int *flag_next, unsigned *error) {
+    using SP = SkewPlan<D>;
+    constexpr int ROW = 64 * WPL;  // words of one LDS row
+    const int lane = threadIdx.x & 63;
+    const int Ww = a.Ww;
+    const int S = eb - ab;
+    const int t0 = tile * kTileValid * WPL;
+    int col = (t0 + WPL * (lane - 1)) % Ww;
+    if (col < 0) col += Ww;
+    const bool keep = lane >= 1 && lane <= kTileValid && (t0 + WPL * (lane - 1)) < Ww;
+    // input rows ab, ab + 1, ... through the row map (torus wrap or halo clamp)
+    int r = ab + a.in.off;
+    const int wrap = a.in.wrap > 0 ? a.in.wrap : INT_MAX;
+    if (a.in.wrap > 0) {
+        r %= a.in.wrap;
+        if (r < 0) r += a.in.wrap;
+    }
+    const uint32_t *__restrict__ src = a.src + col;
+    auto load_next = [&]() -> Lanes<WPL> {
+        const Lanes<WPL> v = load_row<WPL>(src + (size_t)(a.in.base + min(r, a.in.rmax)) * Ww);
+        r = (r + 1 == wrap) ? 0 : r + 1;
+        return v;
+    };
+    // generation D of row ab + D + oi leaves at push ab + 2 D + oi
+    // (buffer stores for every width: a masked store's branch and EXEC writes
+    // put hazard s_nops between parity_fix and the group's first DPP)
+    const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+        a.dst + (size_t)(a.dst_base + ab + D) * Ww, (short)0, S * Ww * 4, 0x00020000);
+    const int clo = a.count_lo - (ab + D), chi = a.count_hi - (ab + D);
+    uint32_t cnt = 0;
+    auto emit = [&](const Lanes<WPL> &y, int oi) {
+        const bool ok = keep && (unsigned)oi < (unsigned)S;
+        const int off = ok ? (oi * Ww + col) * 4 : INT_MAX;  // out of range: dropped
+        if constexpr (WPL == 1)
+            __builtin_amdgcn_raw_buffer_store_b32(y.w[0], brs, off, 0, 0);
+        else if constexpr (WPL == 2)
+            __builtin_amdgcn_raw_buffer_store_b64((__attribute__((ext_vector_type(2))) unsigned){y.w[0], y.w[1]}, brs,
+                                                  off, 0, 0);
+        else
+            __builtin_amdgcn_raw_buffer_store_b128(
+                (__attribute__((ext_vector_type(4))) unsigned){y.w[0], y.w[1], y.w[2], y.w[3]}, brs, off, 0, 0);
+        uint32_t pc = 0;
+#pragma unroll
+        for (int k = 0; k < WPL; ++k) pc += __builtin_popcount(y.w[k]);
+        cnt += (ok && oi >= clo && oi < chi) ? pc : 0u;
+    };
+    // fill exports: the input of stage P (generation P of row ab + P + m) at
+    // fill push 2 P + m, for the band above's drain phase P
+    auto hook = [&](int s, int k, const Lanes<WPL> &x) {
+        int row;
+        if (s == SP::P1)
+            row = (unsigned)(k - 2 * SP::P1) < (unsigned)SP::N1 ? SP::B1 + k - 2 * SP::P1 : SP::NEXP;
+        else if (s == SP::P2)
+            row = (unsigned)(k - 2 * SP::P2) < (unsigned)SP::N2 ? SP::B2 + k - 2 * SP::P2 : SP::NEXP;
+        else if (s == SP::P3)
+            row = (unsigned)(k - 2 * SP::P3) < (unsigned)SP::N3 ? SP::B3 + k - 2 * SP::P3 : SP::NEXP;
+        else
+            return;
+        put_lanes<WPL>(exp_mine + row * ROW, x.w);
+    };
+
+    uint32_t h0[3][D][WPL], h1[3][D][WPL], cc[3][D][WPL];
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int t = 0; t < D; ++t)
+#pragma unroll
+            for (int k = 0; k < WPL; ++k) h0[s][t][k] = h1[s][t][k] = cc[s][t][k] = 0u;
+
+    Lanes<WPL> x0 = vmov(load_next()), x1 = vmov(load_next()), x2 = vmov(load_next());
+    int k = 0;  // push index of x0, from ab
+    auto fill = [&](auto a_tag) {
+        constexpr int A = decltype(a_tag)::value;
+        for (; A == D ? k <= 2 * D - 1 : (k + 2) / 2 <= A - 1; k += 3) {
+            const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
+            __builtin_amdgcn_sched_barrier(0);
+            Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
+            push_group_exp<D, A, WPL>(y0, y1, y2, h0, h1, cc, k, hook);
+            if constexpr (A == D) {
+                emit(y0, k - 2 * D);
+                emit(y1, k + 1 - 2 * D);
+                emit(y2, k + 2 - 2 * D);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            x0 = vmov(n0);
+            x1 = vmov(n1);
+            x2 = vmov(n2);
+        }
+    };
+    fill(std::integral_constant<int, SP::P1>());
+    fill(std::integral_constant<int, SP::P2>());
+    fill(std::integral_constant<int, SP::P3>());
+    fill(std::integral_constant<int, D>());
+    // exports done: this wave's LDS writes complete before the flag (LDS
+    // operations of a wave complete in order; no wait on its global loads)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(flag_mine, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+
+    Lanes<WPL> q0, q1, q2;
+#pragma unroll
+    for (int i = 0; i < WPL; ++i) q0.w[i] = q1.w[i] = q2.w[i] = 0u;
+    int qoi = -8;  // the first body stores nothing real
+    // main: every stage on board rows (the bottom band of a stack to the end)
+    const int kmain = S + (self ? 2 * D : 2 * SP::P1);
+    for (int i = 0; i < GOL_LOOP_PAD; ++i) asm volatile("s_nop 0");
+    for (; k < kmain; k += 3) {
+        const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
+        emit(q0, qoi);
+        emit(q1, qoi + 1);
+        emit(q2, qoi + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
+        push_group<D, D, WPL>(y0, y1, y2, h0, h1, cc);
+        q0 = y0;
+        q1 = y1;
+        q2 = y2;
+        qoi = k - 2 * D;
+        __builtin_amdgcn_sched_barrier(0);
+        x0 = vmov(n0);
+        x1 = vmov(n1);
+        x2 = vmov(n2);
+    }
+    if (!self) {
+        // the band below has exported its top rows (almost always long ago)
+        if (__hip_atomic_load(flag_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+            const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(flag_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > 200000000ll) {  // 2 s: never
+                    if (error && lane == 0) __hip_atomic_store(error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the flag read before the imports
+        // the imports of the group at push kg: generation P of rows e + d - P
+        // (d = kg - S + row), P the phase of the group's first row
+        auto imports = [&](int kg, Lanes<WPL> &y0, Lanes<WPL> &y1, Lanes<WPL> &y2) {
+            const int d = kg - S;
+            const int base = d < 2 * SP::P2 ? SP::B1 - 2 * SP::P1 : d < 2 * SP::P3 ? SP::B2 - 2 * SP::P2
+                                                                                   : SP::B3 - 2 * SP::P3;
+            const int top = SP::NEXP - 1;  // phase 3 clamps (rows past the drain)
+            y0 = get_lanes<WPL>(exp_next + min(base + d, top) * ROW);
+            y1 = get_lanes<WPL>(exp_next + min(base + d + 1, top) * ROW);
+            y2 = get_lanes<WPL>(exp_next + min(base + d + 2, top) * ROW);
+        };
+        {
+            Lanes<WPL> n0, n1, n2;
+            imports(k, n0, n1, n2);
+            x0 = vmov(n0);  // waited here, not at the loop head (keeps parity_fix next to the group)
+            x1 = vmov(n1);
+            x2 = vmov(n2);
+        }
+        auto drain = [&](auto lo_tag, int kend) {
+            constexpr int LO = decltype(lo_tag)::value;
+            for (; k < kend; k += 3) {
+                Lanes<WPL> n0, n1, n2;
+                imports(k + 3, n0, n1, n2);
+                emit(q0, qoi);
+                emit(q1, qoi + 1);
+                emit(q2, qoi + 2);
+                __builtin_amdgcn_sched_barrier(0);
+                Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
+                push_group_hi<D, LO, WPL>(y0, y1, y2, h0, h1, cc);
+                q0 = y0;
+                q1 = y1;
+                q2 = y2;
+                qoi = k - 2 * D;
+                __builtin_amdgcn_sched_barrier(0);
+                x0 = vmov(n0);
+                x1 = vmov(n1);
+                x2 = vmov(n2);
+            }
+        };
+        drain(std::integral_constant<int, SP::P1>(), S + 2 * SP::P2);
+        drain(std::integral_constant<int, SP::P2>(), S + 2 * SP::P3);
+        drain(std::integral_constant<int, SP::P3>(), S + 2 * D);
+    }
+    emit(q0, qoi);
+    emit(q1, qoi + 1);
+    emit(q2, qoi + 2);
+    return cnt;
+}
+
+// K1w: one workgroup = one stack = tx tiles x (8 / tx) bands; wave w takes
+// tile w % tx and stack position w / tx (top to bottom).
+template <int D, int WPL>
+__global__ __launch_bounds__(512) void gol_skew_kernel(SkewArgs p) {
+    using SP = SkewPlan<D>;
+    constexpr int ROW = 64 * WPL;
+    __shared__ uint32_t s_exp[8][(SP::NEXP + 1) * ROW];
+    __shared__ int s_flag[8];
+    __shared__ unsigned long long s_cnt;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int sy = 8 / p.tx;
+    const int tcols = (p.tiles_x + p.tx - 1) / p.tx;
+    const int stack = blockIdx.x / tcols, tc = blockIdx.x - stack * tcols;
+    const int tile = tc * p.tx + w % p.tx, pos = w / p.tx;
+    if (lane == 0) s_flag[w] = 0;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    if (tile >= p.tiles_x) return;  // wave-uniform, after the only barrier (its stack's waves all leave)
+    if (p.prio_young && w >= 4) __builtin_amdgcn_s_setprio(1);
+    const int L = p.base.rows_out;
+    const int A0 = (int)((int64_t)stack * L / p.nst) - D, E0 = (int)((int64_t)(stack + 1) * L / p.nst) - D;
+    const int64_t Ls = (int64_t)(E0 - A0) + p.hcap;
+    int cum = 0, tot = 0;
+    for (int q = 0; q < sy; ++q) {
+        tot += p.wgt[q];
+        cum += q < pos ? p.wgt[q] : 0;
+    }
+    const bool bottom = pos == sy - 1;
+    const int ab = A0 + (int)(Ls * cum / tot);
+    const int eb = bottom ? E0 : A0 + (int)(Ls * (cum + p.wgt[pos]) / tot);
+    const long long t_start = p.trace ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
+    const uint32_t cnt = stream_skew<D, WPL>(p.base, ab, eb, tile, bottom, s_exp[w], bottom ? nullptr : s_exp[w + p.tx],
+                                             &s_flag[w], bottom ? nullptr : &s_flag[w + p.tx], p.error);
+    if (p.trace && lane == 0 && blockIdx.x < 1024) {
+        p.trace[8 + 2 * (blockIdx.x * 64 + w)] = (unsigned long long)t_start;
+        p.trace[8 + 2 * (blockIdx.x * 64 + w) + 1] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
+    }
+    if (p.base.alive) wg_count(p.base.alive, &s_cnt, cnt, sy * min(p.tx, p.tiles_x - tc * p.tx));
+}
+
+// ---------------------------------------------------------------------------
 // K1p: persistent multi-super-step kernel (torus mode, one device).
 //
 // One workgroup of NW wavefronts per CU stays resident for J super-steps of
@@ -1498,6 +1790,36 @@ hipError_t launch_split(const SplitArgs &p, int depth, int wpl, hipStream_t s) {
     GOL_SCASE(32, 1)
 #undef GOL_SCASE
     return hipErrorInvalidValue;
+}
+
+template <typename F>
+static hipError_t dispatch_skew(int depth, int wpl, F &&f) {
+#define GOL_WCASE(D, WP) \
+    if (depth == D && wpl == WP) return f(gol_skew_kernel<D, WP>);
+    GOL_WCASE(8, 2) GOL_WCASE(12, 2) GOL_WCASE(16, 2) GOL_WCASE(20, 2) GOL_WCASE(8, 4) GOL_WCASE(9, 4)
+    GOL_WCASE(16, 1) GOL_WCASE(32, 1)
+#undef GOL_WCASE
+    return hipErrorInvalidValue;
+}
+
+bool skew_supported(int depth, int wpl) {
+    return dispatch_skew(depth, wpl, [](auto) { return hipSuccess; }) == hipSuccess;
+}
+
+int skew_blocks_per_cu(int depth, int wpl) {
+    int b = 0;
+    hipError_t e = dispatch_skew(depth, wpl, [&](auto kern) {
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 512, 0);
+    });
+    return e == hipSuccess ? b : 0;
+}
+
+hipError_t launch_skew(const SkewArgs &p, int depth, int wpl, hipStream_t s) {
+    const int tcols = (p.tiles_x + p.tx - 1) / p.tx;
+    return dispatch_skew(depth, wpl, [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(tcols * p.nst), dim3(512), 0, s, p);
+        return hipGetLastError();
+    });
 }
 
 int tb_blocks_per_cu(int depth, int wpl) {

@@ -117,7 +117,16 @@ struct golhip {
     int64_t split_exp_cap = 0;      // words
     int *split_meet = nullptr;      // K1s per-region wave row counts
     int64_t split_meet_cap = 0;
-    bool last_split = false;        // the last step launch ran K1s
+    int last_variant = 1;           // kernel family of the last step launch (golhip_perf kernel_variant)
+    int skew = 1;                   // option "skew": skewed band stacks (K1w) for per-launch steps
+    int skew_young = 100;           // option "skew_young": band height of waves 4..7, % of waves 0..3's
+    int skew_hcap = -1;             // option "skew_hcap": rows a stack's bottom band gives up (-1: 3 D / 4)
+    int skew_prio = 0;              // option "skew_prio": s_setprio 1 for waves 4..7
+    int skew_tx = 0;                // option "skew_tx": tiles per K1w workgroup (0: plan, 1 or 2)
+    int skew_bpc[kNumDepths][3] = {};  // K1w workgroups per CU by (depth, wpl) (0: not queried)
+    unsigned *skew_err = nullptr;      // host-mapped spin-bound flag of the K1w kernels
+    unsigned *skew_err_dev = nullptr;
+    int64_t skew_launches = 0;
     int persistent = -1;        // option "persistent": K1p for long torus runs (1 on, 0 off, -1 auto)
     int wpl_opt = 0;            // option "wpl": words per lane (0 = auto, 1, 2, 4)
     int persist_depth = 0;      // option "persist_depth" (0: tb_depth)
@@ -345,6 +354,7 @@ int persist_nw_for(golhip_t h, int depth, int wpl) {
 constexpr int64_t kPersistAutoMaxBytes = 64ll << 20;
 bool persist_on(golhip_t h) {
     if (h->persistent >= 0) return h->persistent != 0;
+    if (h->skew) return false;  // K1w per launch (round 3)
     return (int64_t)sched_rows(h) * h->Ww * 4 <= kPersistAutoMaxBytes;
 }
 
@@ -576,6 +586,71 @@ int split_buffers(golhip_t h, golk::SplitArgs &sp, int depth, int wpl) {
     return GOLHIP_OK;
 }
 
+// Skewed band stacks (K1w, option "skew"): any per-launch step (whole torus
+// or a strip's extended rows) whose depth and words per lane have an
+// instance.  One workgroup of 8 waves per stack, sized to fill every CU once:
+// as many stacks per tile column as the CUs allow, with bands of at least
+// D + 3 rows (any height is exact; shorter bands would mostly wait for the
+// band below's exports) and the stack's bottom band `hcap` rows shorter (it
+// computes its drain in full).  tx = 2 (stacks of 4
+// bands, two tiles a workgroup) when the tile count fits the CUs better.
+int skew_bpc(golhip_t h, int depth, int wpl) {
+    int &c = h->skew_bpc[depth_index(depth)][wpl == 4 ? 2 : wpl - 1];
+    if (c == 0) {
+        const int b = golk::skew_blocks_per_cu(depth, wpl);
+        c = b > 0 ? b : -1;
+    }
+    return c;
+}
+
+bool skew_plan(golhip_t h, int depth, int wpl, const golk::StepArgs &a, golk::SkewArgs *sk) {
+    if (!h->skew || h->W % 32 != 0 || !golk::skew_supported(depth, wpl)) return false;
+    const int bpc = skew_bpc(h, depth, wpl);
+    if (bpc < 1) return false;
+    const int tiles = golk::tb_tiles(h->Ww, wpl);
+    const int L = a.rows_out;
+    const int hcap = h->skew_hcap >= 0 ? h->skew_hcap : 3 * depth / 4;
+    const int smin = depth + 3;
+    int best_tx = 0, best_nst = 0;
+    double best = 1e300;
+    for (int tx = 1; tx <= 2; ++tx) {
+        if (h->skew_tx && tx != h->skew_tx) continue;
+        const int sy = 8 / tx, tcols = (tiles + tx - 1) / tx;
+        const int nst = std::min(h->cu_count * bpc / tcols, (L + hcap) / (sy * (smin + hcap)));
+        if (nst < 1) continue;
+        const double per_wave = ((double)L / nst + hcap) / sy;  // input rows a wave streams
+        if (per_wave < best * 0.999) {
+            best = per_wave;
+            best_tx = tx;
+            best_nst = nst;
+        }
+    }
+    if (!best_tx) return false;
+    // a wave's buffer-store range (its band) must stay < 2 GiB
+    if (((double)L / best_nst + hcap) * h->Ww * 4 >= 2147483648.0) return false;
+    if (!h->skew_err) {
+        void *p = nullptr, *d = nullptr;
+        if (hipHostMalloc(&p, sizeof(unsigned), hipHostMallocMapped) != hipSuccess) return false;
+        if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+            (void)hipHostFree(p);
+            return false;
+        }
+        h->skew_err = static_cast<unsigned *>(p);
+        h->skew_err_dev = static_cast<unsigned *>(d);
+        *h->skew_err = 0;
+    }
+    sk->tiles_x = tiles;
+    sk->tx = best_tx;
+    sk->nst = best_nst;
+    const int sy = 8 / best_tx;
+    for (int q = 0; q < 8; ++q) sk->wgt[q] = (q < sy && q * best_tx >= 4) ? h->skew_young : 100;
+    sk->hcap = hcap;
+    sk->prio_young = h->skew_prio;
+    sk->error = h->skew_err_dev;
+    sk->trace = h->d_trace;
+    return true;
+}
+
 // Launch the step kernel for output rows [lo, hi) of this handle (halos, if
 // used, already in place); `alive` (nullable) accumulates their popcount.
 // No bookkeeping: see finish_launch.
@@ -604,8 +679,13 @@ int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int
     }
     hipError_t e;
     golk::SplitArgs sp{};
-    const bool split = !halo && a.rows_out == h->rows && split_plan(h, depth, wpl, &sp);
-    if (split) {
+    golk::SkewArgs sk{};
+    const bool skew = skew_plan(h, depth, wpl, a, &sk);
+    const bool split = !skew && !halo && a.rows_out == h->rows && split_plan(h, depth, wpl, &sp);
+    if (skew) {
+        sk.base = a;
+        e = golk::launch_skew(sk, depth, wpl, st);
+    } else if (split) {
         sp.base = a;
         if (int rc = split_buffers(h, sp, depth, wpl)) return rc;
         e = golk::launch_split(sp, depth, wpl, st);
@@ -614,7 +694,7 @@ int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int
     } else {
         e = golk::launch_step_generic(a, st);
     }
-    h->last_split = split;
+    h->last_variant = h->W % 32 != 0 ? 0 : skew ? 3 : split ? 2 : 1;
     if (e != hipSuccess) return fail(GOLHIP_EHIP, "step launch: %s", hipGetErrorString(e));
     if (e1) {
         HIP_OR_FAIL(hipEventRecord(e1, st));
@@ -626,6 +706,7 @@ int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int
     }
     h->step_launches++;
     h->split_launches += split;
+    h->skew_launches += skew;
     return GOLHIP_OK;
 }
 
@@ -705,6 +786,11 @@ int check_persist(golhip_t h) {
 
 int sync_stream(golhip_t h) {
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (h->skew_err && *h->skew_err) {
+        *h->skew_err = 0;
+        return fail(GOLHIP_EHIP, "skewed-band step kernel: a band waited past its spin bound for the band below "
+                                 "(board state is undefined)");
+    }
     return check_persist(h);
 }
 
@@ -1246,6 +1332,7 @@ int golhip_destroy(golhip_t h) {
     HIP_RC(hipFree(h->split_exp));
     HIP_RC(hipFree(h->split_meet));
     if (h->h_err) HIP_RC(hipHostFree(h->h_err));
+    if (h->skew_err) HIP_RC(hipHostFree(h->skew_err));
     if (h->own_stream && h->stream) HIP_RC(hipStreamDestroy(h->stream));
     delete h;
     return rc;
@@ -1362,6 +1449,31 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     if (!strcmp(key, "fill_skip")) {
         h->fill_skip = value != 0;
         for (int &c : h->auto_rpw) c = 0;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "skew")) {
+        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "skew %lld", (long long)value);
+        h->skew = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "skew_young")) {
+        if (value < 10 || value > 400) return fail(GOLHIP_EINVAL, "skew_young %lld not in 10..400", (long long)value);
+        h->skew_young = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "skew_hcap")) {
+        if (value < -1 || value > 256) return fail(GOLHIP_EINVAL, "skew_hcap %lld", (long long)value);
+        h->skew_hcap = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "skew_prio")) {
+        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "skew_prio %lld", (long long)value);
+        h->skew_prio = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "skew_tx")) {
+        if (value < 0 || value > 2) return fail(GOLHIP_EINVAL, "skew_tx %lld", (long long)value);
+        h->skew_tx = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "split")) {
@@ -1839,7 +1951,8 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     const bool halo = h->comm && (h->nranks > 1 || h->force_halo);
     out->tb_depth = depth_cap(h, halo);
     out->rows_per_wave = rows_per_wave_for(h, next_depth(h, h->tb_depth, halo));
-    out->kernel_variant = h->W % 32 != 0 ? 0 : h->last_split ? 2 : 1;
+    out->kernel_variant = h->last_variant;
+    out->skew_launches = h->skew_launches;
     out->words_per_lane = h->W % 32 == 0 ? wpl_for(h) : 0;
     out->persist_depth = h->W % 32 == 0 ? persist_depth_for(h, wpl_for(h)) : 0;
     return GOLHIP_OK;
@@ -1875,7 +1988,7 @@ int golhip_perf_reset(golhip_t h) {
     if (int rc = set_dev(h)) return rc;
     if (int rc = drain_events(h)) return rc;
     h->step_ms = h->persist_ms = 0;
-    h->step_launches = h->step_turns = h->halo_bytes = h->split_launches = 0;
+    h->step_launches = h->step_turns = h->halo_bytes = h->split_launches = h->skew_launches = 0;
     h->persist_launches = h->persist_turns = 0;
     h->flip_launches = h->flip_entries = 0;
     h->flip_ms = 0;

@@ -55,6 +55,7 @@ class Perf(ctypes.Structure):
         ("persist_depth", ctypes.c_int32),
         ("reserved0", ctypes.c_int32),
         ("split_launches", ctypes.c_int64),
+        ("skew_launches", ctypes.c_int64),
     ]
 
     def as_dict(self) -> dict:

@@ -83,6 +83,8 @@ typedef struct golhip_perf {
     int32_t reserved0;
     int64_t split_launches;   /* of step_launches, those that ran split tiling
                                  (gol_split_pair_kernel + gol_split_tri_kernel) */
+    int64_t skew_launches;    /* of step_launches, those that ran skewed band
+                                 stacks (gol_skew_kernel, kernel_variant 3)     */
 } golhip_perf_t;
 
 /* ---- library ---------------------------------------------------------- */

@@ -25,6 +25,7 @@ ap.add_argument("--strips", default="65536x8192,65536x16384,65536x32768,262144x3
 ap.add_argument("--persistent", default="-1,0")
 ap.add_argument("--depths", default="16")
 ap.add_argument("--torus", action="store_true", help="whole-board torus instead of a one-rank ring")
+ap.add_argument("--option", action="append", default=[], help="engine option key=value (every run)")
 a = ap.parse_args()
 for spec in a.strips.split(","):
     W, R = (int(x) for x in spec.split("x"))
@@ -34,6 +35,9 @@ for spec in a.strips.split(","):
                 b.comm_init(golhip.unique_id(), 1, 0)
                 b.set_option("force_halo", 1)
             b.set_option("persistent", pers)
+            for kv in a.option:
+                k, v = kv.split("=")
+                b.set_option(k, int(v))
             b.set_tb_depth(depth)
             b.fill_random(0x5EED0002)
             b.step(min(a.turns, 200))
@@ -47,4 +51,5 @@ for spec in a.strips.split(","):
             print(json.dumps({"strip": [R, W], "torus": a.torus, "persistent": pers, "depth": depth, "turns": a.turns, "seconds": dt,
                               "gcups": W * R * a.turns / dt / 1e9, "persist_launches": p["persist_launches"],
                               "step_launches": p["step_launches"], "words_per_lane": p["words_per_lane"],
-                              "tb_depth": p["tb_depth"], "halo_MB": p["halo_bytes"] / 1e6}), flush=True)
+                              "tb_depth": p["tb_depth"], "halo_MB": p["halo_bytes"] / 1e6,
+                              "skew_launches": p["skew_launches"], "options": a.option}), flush=True)

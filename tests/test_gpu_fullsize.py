@@ -73,19 +73,22 @@ def run_checkpoints(full, key, **options):
 
 
 # ---------------------------------------------------------------- configs[1]
-@pytest.mark.parametrize("opts", [{}, {"persistent": 0}, {"wpl": 2}, {"persistent": 0, "wpl": 4},
-                                  {"tb_depth": 32, "wpl": 1}, {"persistent": 0, "tb_depth": 6}])
+@pytest.mark.parametrize("opts", [{}, {"persistent": 1}, {"skew": 0, "persistent": 0}, {"wpl": 2},
+                                  {"persistent": 0, "wpl": 4}, {"tb_depth": 32, "wpl": 1},
+                                  {"persistent": 0, "tb_depth": 6}, {"tb_depth": 16}])
 def test_config1_16384_10k_turns(full, opts):
-    """configs[1]: 16384^2, 10,000 turns (default: the resident kernel)."""
+    """configs[1]: 16384^2, 10,000 turns (default: skewed band stacks, K1w;
+    persistent 1: the resident kernel K1p; skew 0: the overlapped K1)."""
     run_checkpoints(full, "c1", **opts)
 
 
 # ---------------------------------------------------------------- configs[2]
-@pytest.mark.parametrize("opts", [{}, {"split": 0}, {"tb_depth": 16}, {"wpl": 4}, {"persistent": 1},
-                                  {"wpl": 1, "tb_depth": 32}])
+@pytest.mark.parametrize("opts", [{}, {"skew": 0}, {"skew": 0, "split": 0}, {"tb_depth": 16}, {"wpl": 4},
+                                  {"persistent": 1}, {"wpl": 1, "tb_depth": 32}, {"skew_tx": 2},
+                                  {"skew_young": 70, "skew_prio": 1}])
 def test_config2_65536_1k_turns(full, opts):
-    """configs[2]: 65536^2, 1,000 turns (default: split tiling, 20-turn launches; split 0: the
-    overlapped paired-band kernel)."""
+    """configs[2]: 65536^2, 1,000 turns (default: skewed band stacks, 20-turn launches;
+    skew 0: split tiling; skew 0 split 0: the overlapped paired-band kernel)."""
     run_checkpoints(full, "c2", **opts)
 
 
@@ -114,7 +117,7 @@ def test_config2_strips_in_process(full, nstrips):
             s.close()
 
 
-@pytest.mark.parametrize("persistent", [-1, 0])
+@pytest.mark.parametrize("persistent", [-1, 1, 0])
 def test_config2_rccl_ring_one_rank(full, persistent):
     """configs[2] through the RCCL halo path (a one-rank ring, deep halos)."""
     js, rows = full
@@ -124,6 +127,8 @@ def test_config2_rccl_ring_one_rank(full, persistent):
         b.comm_init(golhip.unique_id(), 1, 0)
         b.set_option("force_halo", 1)
         b.set_option("persistent", persistent)
+        if persistent == 0:
+            b.set_option("skew", 0)
         b.fill_random(rec["seed"])
         b.step(1000)
         assert b.perf()["halo_bytes"] > 0
@@ -131,8 +136,8 @@ def test_config2_rccl_ring_one_rank(full, persistent):
 
 
 # ---------------------------------------------------------------- configs[3]
-@pytest.mark.parametrize("opts", [{}, {"wpl": 2}])
-def test_config3_262144_100_turns(full, opts):  # default: split tiling
+@pytest.mark.parametrize("opts", [{}, {"wpl": 2}, {"skew": 0}])
+def test_config3_262144_100_turns(full, opts):  # default: skewed band stacks
     """configs[3]: the whole 262144^2 board on one GPU, 100 turns (default:
     four words per lane, 8-turn launches)."""
     run_checkpoints(full, "c3", **opts)

@@ -393,6 +393,7 @@ def test_persistent_waves_per_workgroup(coracle, N, depth, wpl, nw):
     turns = 4 * depth + 3
     want = coracle.run(board, turns)
     with golhip.Board(N, N // 2) as b:
+        b.set_option("persistent", 1)
         b.set_option("wpl", wpl)
         b.set_option("persist_waves", nw)
         b.set_tb_depth(depth)
@@ -469,7 +470,7 @@ def test_interleaved_fill_random_and_strips(coracle, wpl):
 @pytest.mark.parametrize("W,H,depth", [(512, 512, 16), (512, 512, 4), (1024, 768, 8), (2048, 1024, 32),
                                        (640, 200, 16), (4096, 96, 16), (4096, 40, 16), (1000, 300, 4),
                                        (2048, 2048, 16), (1984, 1500, 8)])
-@pytest.mark.parametrize("persistent", [-1, 0])
+@pytest.mark.parametrize("persistent", [1, 0, -1])
 def test_rccl_halo_ring_one_rank(coracle, W, H, depth, persistent):
     """The multi-GPU path (RCCL send/recv of deep halo rows, then the resident
     kernel over the extended rows or per-launch kernels on shrinking ranges)
@@ -487,7 +488,7 @@ def test_rccl_halo_ring_one_rank(coracle, W, H, depth, persistent):
         b.step(turns)
         p = b.perf()
         assert p["halo_bytes"] > 0
-        if persistent == 0:
+        if persistent != 1:  # auto: skewed band stacks (K1w) between exchanges
             assert p["persist_launches"] == 0
         elif W % 32 == 0 and depth >= 4 and H >= 4 * depth:
             assert p["persist_launches"] > 0
@@ -605,6 +606,7 @@ def test_persistent_unequal_bands(coracle, N, depth, wpl, nw, split, tx):
         b.set_option("paired_bands", 0)
         b.set_option("age_split", split)
         b.set_option("persist_wg_tx", tx)
+        b.set_option("persistent", 1)
         b.set_tb_depth(depth)
         b.load_bytes(board)
         b.step(turns)
@@ -627,6 +629,7 @@ def test_persistent_paired_bands(coracle, N, rows, depth, wpl, nw, tx):
         b.set_option("persist_waves", nw)
         b.set_option("persist_wg_tx", tx)
         b.set_option("paired_bands", 1)
+        b.set_option("persistent", 1)
         b.set_tb_depth(depth)
         b.load_bytes(board)
         b.step(turns)
@@ -646,6 +649,7 @@ def test_per_launch_paired_bands(coracle, N, rows, depth, wpl, rpw, paired):
     want = coracle.run(board, turns)
     with golhip.Board(N, rows) as b:
         b.set_option("persistent", 0)
+        b.set_option("skew", 0)
         b.set_option("wpl", wpl)
         b.set_option("paired_bands", paired)
         b.set_tb_depth(depth)

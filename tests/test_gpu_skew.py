@@ -1,0 +1,163 @@
+"""GPU parity of skewed band stacks (option "skew", gol_kernels.hip K1w) against the C oracle.
+
+K1w runs a launch as stacks of bands, one workgroup per stack: band [a, e)
+of input rows owns generation g of the rows [a + g, e + g), takes the
+bottom rows it needs from the band below through LDS (exported during that
+band's pipeline fill) and the stack's bottom band computes its drain from
+the board.  Bit-exact against oracle/gol_fastcpu.c (the C restatement pinned
+to the reference's fixtures in tests/test_oracle_golden.py) for every
+instantiated (depth, words per lane), stacks of 8 and of 4 bands, unequal
+band heights, the torus seam inside a band, row strips (one-rank RCCL ring
+and in-process strips, where the launches step extended row ranges) and
+the fused alive count.  The full-size BASELINE fixtures run on K1w by
+default (tests/test_gpu_fullsize.py).
+"""
+import numpy as np
+import pytest
+
+from oracle.oracle import COracle
+
+pytestmark = pytest.mark.gpu
+
+golhip = pytest.importorskip("golhip")
+
+SKEW = [(8, 2), (12, 2), (16, 2), (20, 2), (8, 4), (9, 4), (16, 1), (32, 1)]
+
+
+@pytest.fixture(scope="module")
+def coracle():
+    return COracle()
+
+
+def run_skew(board, turns, depth, wpl, **opts):
+    H, W = board.shape
+    with golhip.Board(W, H) as b:
+        b.set_option("persistent", 0)
+        b.set_option("skew", 1)
+        b.set_option("wpl", wpl)
+        for k, v in opts.items():
+            b.set_option(k, v)
+        b.set_tb_depth(depth)
+        b.load_bytes(board)
+        b.step(turns)
+        p = b.perf()
+        out = b.snapshot_bytes()
+        cnt, at = b.alive_count()
+        assert at == turns
+        assert cnt == int((out == 255).sum())
+        return out, p
+
+
+@pytest.mark.parametrize("depth,wpl", SKEW)
+@pytest.mark.parametrize("W,H", [(2048, 1024), (4096, 777), (8192, 331), (3968, 2500), (16384, 1600)])
+def test_skew_matches_oracle(coracle, depth, wpl, W, H):
+    if W % (32 * wpl):
+        pytest.skip("width not a multiple of the lane chunk")
+    board = coracle.fill_random(W, H, 0x5EED0031 + W + H)
+    turns = 2 * depth + 3  # two skew launches and a remainder on the other kernels
+    want = coracle.run(board, turns)
+    got, p = run_skew(board, turns, depth, wpl)
+    assert p["skew_launches"] >= 1
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("depth,wpl", SKEW)
+@pytest.mark.parametrize("tx", [1, 2])
+def test_skew_single_stack(coracle, depth, wpl, tx):
+    """One stack per tile column (a narrow board, few rows): the torus seam
+    runs through the top band's first rows and the bottom band's drain."""
+    W = 62 * 32 * wpl  # one tile
+    sy = 8 // tx
+    H = sy * (2 * depth + 3) + 5
+    board = coracle.fill_random(W, H, 0x5EED0032 + depth * 8 + wpl)
+    turns = 2 * depth
+    want = coracle.run(board, turns)
+    got, p = run_skew(board, turns, depth, wpl, skew_tx=tx)
+    assert p["skew_launches"] == 2 and p["kernel_variant"] == 3
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("depth,wpl", [(20, 2), (16, 2), (9, 4), (32, 1)])
+@pytest.mark.parametrize("opts", [{"skew_young": 60}, {"skew_young": 150}, {"skew_hcap": 0}, {"skew_hcap": 40},
+                                  {"skew_prio": 1}, {"skew_tx": 2, "skew_young": 80}])
+def test_skew_band_heights(coracle, depth, wpl, opts):
+    """Unequal bands (taller or shorter younger waves, bottom-band handicap,
+    static priority) change only the schedule, never the result."""
+    W, H = 4096, 2000 + depth
+    board = coracle.fill_random(W, H, 0x5EED0033 + depth)
+    turns = 3 * depth
+    want = coracle.run(board, turns)
+    got, p = run_skew(board, turns, depth, wpl, **opts)
+    assert p["skew_launches"] == 3
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("depth,wpl", [(20, 2), (16, 2), (8, 4), (9, 4), (16, 1), (32, 1)])
+@pytest.mark.parametrize("W,H", [(4096, 1500), (8192, 700), (2048, 4096)])
+def test_skew_rccl_ring_one_rank(coracle, depth, wpl, W, H):
+    """The multi-GPU path on K1w: deep-halo exchange, then launches over the
+    extended row ranges [-e, rows + e) (one-rank RCCL ring, force_halo)."""
+    board = coracle.fill_random(W, H, 0x5EED0034 + W)
+    turns = 7 * depth + 2
+    want = coracle.run(board, turns)
+    with golhip.Board(W, H) as b:
+        b.comm_init(golhip.unique_id(), 1, 0)
+        b.set_option("force_halo", 1)
+        b.set_option("persistent", 0)
+        b.set_option("wpl", wpl)
+        b.set_tb_depth(depth)
+        b.load_bytes(board)
+        b.step(turns)
+        p = b.perf()
+        assert p["halo_bytes"] > 0 and p["skew_launches"] >= 3
+        assert np.array_equal(b.snapshot_bytes(), want)
+        assert b.alive_count() == (int((want == 255).sum()), turns)
+
+
+@pytest.mark.parametrize("nstrips", [2, 3, 5])
+@pytest.mark.parametrize("depth,wpl", [(20, 2), (9, 4)])
+def test_skew_group_strips(coracle, nstrips, depth, wpl):
+    """In-process row strips (halos by device copies) stepped on K1w."""
+    W, H = 4096, 3001
+    board = coracle.fill_random(W, H, 0x5EED0035 + nstrips)
+    turns = 5 * depth + 1
+    want = coracle.run(board, turns)
+    bounds = [H * i // nstrips for i in range(nstrips + 1)]
+    strips = [golhip.Board(W, H, row0=bounds[i], rows=bounds[i + 1] - bounds[i]) for i in range(nstrips)]
+    try:
+        for i, s in enumerate(strips):
+            s.set_option("wpl", wpl)
+            s.set_tb_depth(depth)
+            s.load_bytes(board[bounds[i]:bounds[i + 1]])
+        golhip.group_step(strips, turns)
+        got = np.concatenate([s.snapshot_bytes() for s in strips])
+        assert sum(s.perf()["skew_launches"] for s in strips) > 0
+        assert np.array_equal(got, want)
+        assert sum(s.alive_count()[0] for s in strips) == int((want == 255).sum())
+    finally:
+        for s in strips:
+            s.close()
+
+
+def test_skew_off_uses_other_kernels(coracle):
+    board = coracle.fill_random(4096, 1000, 0x5EED0036)
+    want = coracle.run(board, 40)
+    got, p = run_skew(board, 40, 20, 2, skew=0)
+    assert p["skew_launches"] == 0 and p["kernel_variant"] in (1, 2)
+    assert np.array_equal(got, want)
+
+
+def test_skew_every_launch_counts(coracle):
+    """Steps of one launch each: the fused popcount of every K1w launch."""
+    board = coracle.fill_random(8192, 1200, 0x5EED0037)
+    with golhip.Board(8192, 1200) as b:
+        b.set_option("persistent", 0)
+        b.set_tb_depth(20)
+        b.load_bytes(board)
+        cur = board
+        for t in range(5):
+            b.step(20)
+            cur = coracle.run(cur, 20)
+            assert b.alive_count() == (int((cur == 255).sum()), 20 * (t + 1))
+        assert b.perf()["skew_launches"] == 5
+        assert np.array_equal(b.snapshot_bytes(), cur)

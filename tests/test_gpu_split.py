@@ -32,6 +32,7 @@ def run_split(board, turns, depth, wpl, rows_per_wave=0):
         b.set_option("persistent", 0)
         b.set_option("wpl", wpl)
         b.set_option("split", 1)
+        b.set_option("skew", 0)
         b.set_tb_depth(depth)
         b.set_rows_per_wave(rows_per_wave)
         b.load_bytes(board)
@@ -97,12 +98,12 @@ def test_split_falls_back_below_one_region(coracle):
 
 # ---------------------------------------------------------------- full-size BASELINE fixtures
 def test_split_config1_16384(full):
-    run_checkpoints(full, "c1", split=1, persistent=0)
+    run_checkpoints(full, "c1", split=1, persistent=0, skew=0)
 
 
 def test_split_config2_65536(full):
-    run_checkpoints(full, "c2", split=1)
+    run_checkpoints(full, "c2", split=1, skew=0)
 
 
 def test_split_config3_262144(full):
-    run_checkpoints(full, "c3", split=1)
+    run_checkpoints(full, "c3", split=1, skew=0)
