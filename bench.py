@@ -1,6 +1,6 @@
 """bench.py — cell-updates/s of the MI355X Game of Life engine (libgolhip.so).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload 65536|16384|262144]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload 65536|16384|262144|5120]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 A "step" is one run of the workload's BASELINE config over the whole board:
@@ -15,6 +15,10 @@ over RCCL (the only collective on the path):
   65536  (default, configs[2]) 65536^2,  seed 0x5EED0002, 1,000 turns a step
   16384  (configs[1])          16384^2,  seed 0x5EED0001, 10,000 turns a step
   262144 (configs[3])          262144^2, seed 0x5EED0003, 100 turns a step
+  5120   (configs[4])          5120^2, seed 0x5EED0005, the full event stream: every
+                               turn's CellFlipped list (fused turn + list kernel K5,
+                               4-byte cell indices into page-locked host memory),
+                               200 turns a step from turn 2064 on; one GPU
 
 Parity: the first untimed step starts from the freshly filled board, so after
 it the board is at exactly the config's turns; its digest (golhip_board_hash,
@@ -58,6 +62,8 @@ WORKLOADS = {
     65536: dict(key="c2", seed=0x5EED0002, turns=1000, desc="configs[2]: 65536^2 random 25%, 1000 turns a step"),
     16384: dict(key="c1", seed=0x5EED0001, turns=10000, desc="configs[1]: 16384^2 random 25%, 10000 turns a step"),
     262144: dict(key="c3", seed=0x5EED0003, turns=100, desc="configs[3]: 262144^2 random 25%, 100 turns a step"),
+    5120: dict(key="c4", seed=0x5EED0005, turns=200,
+               desc="configs[4]: 5120^2 random 25%, full CellFlipped stream, 200 turns a step from turn 2064"),
 }
 FULLSIZE = os.path.join(ROOT, "tests", "golden", "fullsize.json")
 
@@ -151,6 +157,34 @@ def cpu_baseline(W: int, seed: int, target_s: float) -> dict:
     return out
 
 
+def cpu_config0() -> dict:
+    """BASELINE configs[0]: images/512x512.pgm, 100 turns, Threads = 8, on the
+    oracle's port of the reference worker pool (distributor.go:116-173:
+    Threads + 1 workers, row queue, per-row alive lists, per-turn allocation,
+    flip diff), checked against check/images/512x512x100.pgm (the reference's
+    golden board, tests/golden/fixtures.npz)."""
+    from oracle.oracle import COracle, unpack_bits
+
+    o = COracle()
+    with np.load(os.path.join(ROOT, "tests", "golden", "fixtures.npz"), allow_pickle=False) as z:
+        board = unpack_bits(z["image_512"], 512)
+        golden = unpack_bits(z["check_512x100"], 512)
+    o.run_workerpool(board, 1, 8)  # warm
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        out = o.run_workerpool(board, 100, 8)
+        reps += 1
+        if time.perf_counter() - t0 > 1.0:
+            break
+    dt = (time.perf_counter() - t0) / reps
+    res = out[0] if isinstance(out, tuple) else out
+    return {"value": 512 * 512 * 100 / dt / 1e9, "unit": "GCUPS", "cores": 9, "kind": "port",
+            "seconds_per_run": dt, "runs": reps,
+            "parity": bool(np.array_equal(np.asarray(res), golden)),
+            "sample": "configs[0]: images/512x512.pgm, 100 turns, Threads=8 (9 workers), oracle/gol_oracle.c "
+                      "worker-pool port; parity vs check/images/512x512x100.pgm"}
+
+
 def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str) -> dict:
     """Roofline of the dominant step kernel, from HIP events around every launch
     on the engine stream (GOLHIP_FLAG_TIMING; launch-averaged).
@@ -226,8 +260,119 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str) 
     return out
 
 
+def events_main(a) -> None:
+    """configs[4]: 5120^2 with the full event stream ("GCUPS with
+    events on vs off").  Parity first: the CellFlipped lists of turns 1..50
+    from the fresh board (int32 (x, y) pairs, row-major per turn) must equal
+    tests/golden/fullsize.json c4 (per-turn counts + SHA-256 of the pairs).
+    Then the board runs untimed to turn 2064 (past the random board's first
+    turns of 3-7 M flips, ~0.4 M a turn on), and each timed step is 200 turns
+    through golhip_flip_stream with 4-byte cell indices written by the kernel
+    into page-locked host memory (golhip_host_alloc), every turn's list
+    complete on the host: `value` = W x H x turns / s with events on.
+    `events_off` times the same turns on fused launches (no lists)."""
+    import hashlib
+
+    import torch
+    torch.cuda.set_device(0)
+    wl = WORKLOADS[5120]
+    N, tps = 5120, a.turns_per_step or wl["turns"]
+    with open(FULLSIZE) as f:
+        rec = json.load(f)["c4"]
+    cap = 32 << 20
+    # parity: turns 1..T of the fixture, pairs
+    T = len(rec["flip_counts"])
+    xy = np.empty((cap, 2), dtype=np.int32)
+    sha, counts = hashlib.sha256(), []
+    with golhip.Board(N, N) as b:
+        b.fill_random(wl["seed"])
+        done = 0
+        while done < T:
+            ent, cnt, k = b.flip_stream(T - done, cap=cap, fmt=golhip.FLIPS_XY, out=xy)
+            sha.update(ent.tobytes())
+            counts += [int(c) for c in cnt]
+            done += k
+    parity = {"turns": T, "flips": sum(counts), "sha256": sha.hexdigest()[:16],
+              "ok": sha.hexdigest() == rec["flips_sha256"] and counts == rec["flip_counts"][:T],
+              "fixture": "tests/golden/fullsize.json c4 turns 1..%d" % T}
+    idx = golhip.host_array((cap,), np.uint32)
+    idx.fill(0)
+
+    def stream(b, turns):
+        done, flips = 0, 0
+        while done < turns:
+            ent, cnt, k = b.flip_stream(turns - done, cap=cap, fmt=golhip.FLIPS_INDEX, out=idx)
+            done += k
+            flips += len(ent)
+        return flips
+
+    res = {}
+    for timed in (False, True):  # turns/s without per-launch HIP events; the K5 kernel time with them
+        with golhip.Board(N, N, timing=timed) as b:
+            b.fill_random(wl["seed"])
+            b.step(2064)
+            b.sync()
+            stream(b, max(1, a.warmup) * tps)  # warmup steps (untimed)
+            b.sync()
+            b.perf_reset()
+            t0 = time.perf_counter()
+            flips = sum(stream(b, tps) for _ in range(a.steps))
+            b.sync()
+            dt = time.perf_counter() - t0
+            if not timed:
+                res.update(dt=dt, flips=flips)
+                # events off: the same turns on fused launches, from the same turn
+                b.fill_random(wl["seed"])
+                b.step(2064 + max(1, a.warmup) * tps)
+                b.sync()
+                t1 = time.perf_counter()
+                for _ in range(a.steps):
+                    b.step(tps)
+                b.sync()
+                res["dt_off"] = time.perf_counter() - t1
+            else:
+                res["perf"] = b.perf()
+                res["flips_timed"] = flips
+    p = res["perf"]
+    turns = tps * a.steps
+    kus = p["flip_kernel_ms"] * 1e3 / max(1, p["flip_launches"])
+    alg = 2 * N * N / 8 + res["flips_timed"] / max(1, turns) * 4  # board in + out + entries, per launch
+    out = {
+        "metric": METRIC, "value": round(N * N * turns / res["dt"] / 1e9, 3), "unit": "GCUPS", "n_gpus": 1,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(res["dt"] / a.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "u32 bit-sliced (1 bit/cell) + u32 cell-index lists",
+        "data": "synthetic (splitmix64 counter-hash board, 25% alive)",
+        "parity": parity["ok"], "parity_check": parity,
+        "config": {"workload": wl["desc"], "board": [N, N], "turns_per_step": tps,
+                   "events": "every turn's CellFlipped list (4-byte y*W+x) into golhip_host_alloc memory",
+                   "parallelism": "single GPU torus"},
+        "events_on": {"turns_per_s": round(turns / res["dt"], 1), "flips_per_s": round(res["flips"] / res["dt"], 1),
+                      "flips": res["flips"]},
+        "events_off": {"gcups": round(N * N * turns / res["dt_off"] / 1e9, 3),
+                       "turns_per_s": round(turns / res["dt_off"], 1)},
+        "roofline": {"bound": "hbm", "achieved": round(alg / (kus * 1e-6) / 1e9, 1) if kus > 0 else None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / (kus * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+                     if kus > 0 else None, "traffic": None, "kernel": "gol_flip_turn_kernel (K5)",
+                     "avg_launch_ms": round(kus / 1e3, 5), "launches": p["flip_launches"],
+                     "alg_bytes_per_launch": alg,
+                     "note": "one turn + its list per launch; the 5120^2 board is cache-resident and the launch is "
+                             "bound by its grid-wide predecessor sum, not by bandwidth (DESIGN 7.3)"},
+    }
+    if not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(N, wl["seed"], a.cpu_seconds)
+        out["cpu_baseline"]["config0"] = cpu_config0()
+    print(json.dumps(out), flush=True)
+    if parity["ok"] is False:
+        sys.exit(1)
+
+
 def main():
     a = parse()
+    if a.workload == 5120:
+        if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+            raise SystemExit("--workload 5120 (the event stream) runs on one GPU")
+        return events_main(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -353,6 +498,7 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(W, wl["seed"], a.cpu_seconds)
+        out["cpu_baseline"]["config0"] = cpu_config0()
     if rank == 0:
         print(json.dumps(out), flush=True)
     board.close()

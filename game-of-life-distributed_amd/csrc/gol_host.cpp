@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <sstream>
@@ -78,10 +79,128 @@ void check(int rc) {
     if (rc != GOLHIP_OK) throw std::runtime_error(std::string("golhip: ") + golhip_last_error());
 }
 
-struct Board {
-    golhip_t h = nullptr;
-    Board(int64_t w, int64_t hgt, int dev) { check(golhip_create((int32_t)w, (int32_t)hgt, dev, 0, &h)); }
-    ~Board() { golhip_destroy(h); }
+int env_int(const char *name, int dflt) {
+    const char *v = std::getenv(name);
+    return (v && *v) ? std::atoi(v) : dflt;
+}
+
+// The board behind Run: one whole-torus handle, or row strips (GOL_NGPU /
+// GOL_STRIPS) stepped together by golhip_group_step_ex.  Every side channel
+// of the strips is gathered in strip order, which is the board's row-major
+// order: alive lists and flip lists concatenate, counts add up.
+struct Engine {
+    std::vector<golhip_t> hs;
+    std::vector<int64_t> row0;
+    int64_t W = 0, H = 0;
+    Engine(int64_t w, int64_t hgt, const RunOptions &opt) : W(w), H(hgt) {
+        const int ngpu = opt.ngpu >= 0 ? opt.ngpu : env_int("GOL_NGPU", 1);
+        const int strips = opt.strips >= 0 ? opt.strips : env_int("GOL_STRIPS", 0);
+        int n = strips > 0 ? strips : std::max(1, ngpu);
+        n = (int)std::min<int64_t>(n, hgt);
+        if (n <= 1) {
+            hs.push_back(nullptr);
+            row0.push_back(0);
+            check(golhip_create((int32_t)w, (int32_t)hgt, opt.device, 0, &hs[0]));
+            return;
+        }
+        int32_t ndev = 0;
+        check(golhip_device_count(&ndev));
+        const int devs = std::max(1, std::min(ngpu > 0 ? ngpu : 1, (int)ndev));
+        for (int i = 0; i < n; ++i) {
+            const int64_t r0 = hgt * i / n, r1 = hgt * (i + 1) / n;
+            golhip_t h = nullptr;
+            const int dev = devs > 1 ? i % devs : opt.device;
+            const int rc = golhip_create_strip((int32_t)w, (int32_t)hgt, (int32_t)r0, (int32_t)(r1 - r0), dev, 0, &h);
+            if (rc != GOLHIP_OK) {
+                for (golhip_t x : hs) golhip_destroy(x);
+                hs.clear();
+                check(rc);
+            }
+            hs.push_back(h);
+            row0.push_back(r0);
+        }
+    }
+    ~Engine() {
+        for (golhip_t h : hs) golhip_destroy(h);
+    }
+    bool one() const { return hs.size() == 1; }
+    int64_t rows(size_t i) const { return (i + 1 < row0.size() ? row0[i + 1] : H) - row0[i]; }
+    void load(const uint8_t *raster) {
+        for (size_t i = 0; i < hs.size(); ++i) check(golhip_load_bytes(hs[i], raster + row0[i] * W));
+    }
+    void snapshot(uint8_t *out) {
+        for (size_t i = 0; i < hs.size(); ++i) check(golhip_snapshot_bytes(hs[i], out + row0[i] * W));
+    }
+    void alive_count(uint64_t *n, int64_t *at) {
+        *n = 0;
+        for (golhip_t h : hs) {
+            uint64_t c = 0;
+            check(golhip_alive_count(h, &c, at));
+            *n += c;
+        }
+    }
+    // calculateAliveCells (distributor.go:420-432) / the flips of the last turn
+    std::vector<util::Cell> cells(int (*fn)(golhip_t, int32_t *, uint64_t, uint64_t *), bool transpose) {
+        std::vector<util::Cell> out;
+        for (golhip_t h : hs) {
+            uint64_t n = 0;
+            int rc = fn(h, nullptr, 0, &n);
+            if (rc != GOLHIP_OK && rc != GOLHIP_ERANGE) check(rc);
+            std::vector<int32_t> xy(2 * std::max<uint64_t>(n, 1));
+            check(fn(h, xy.data(), n, &n));
+            for (uint64_t i = 0; i < n; ++i) {
+                util::Cell c;
+                c.X = transpose ? xy[2 * i + 1] : xy[2 * i];
+                c.Y = transpose ? xy[2 * i] : xy[2 * i + 1];
+                out.push_back(c);
+            }
+        }
+        return out;
+    }
+    void step(int64_t turns) {
+        if (one()) {
+            check(golhip_step(hs[0], turns, 0));
+            check(golhip_sync(hs[0]));
+        } else {
+            check(golhip_group_step_ex(hs.data(), (int32_t)hs.size(), turns, 0));
+        }
+    }
+    // Up to `want` turns with every turn's flip list as cell indices y * W + x
+    // (golhip_flip_stream's contract: stops before a turn that does not fit;
+    // GOLHIP_ERANGE with *n = what the first turn needs).  Strips: one turn a
+    // group step, each strip's list of that turn, in strip order.
+    int flip_stream(int64_t want, uint32_t *buf, uint64_t cap, uint64_t *counts, int64_t *done, uint64_t *n) {
+        if (one()) return golhip_flip_stream(hs[0], want, GOLHIP_FLIPS_INDEX, buf, cap, counts, done, n);
+        *done = 0;
+        *n = 0;
+        std::vector<int32_t> xy;
+        const uint64_t most = (uint64_t)W * (uint64_t)H;  // a turn flips at most every cell
+        for (int64_t t = 0; t < want; ++t) {
+            if (*n + most > cap) {  // the next turn might not fit: stop before it (nothing of it ran)
+                if (t > 0) break;
+                *n = most;
+                return GOLHIP_ERANGE;
+            }
+            check(golhip_group_step_ex(hs.data(), (int32_t)hs.size(), 1, 1));
+            uint64_t turn_n = 0;
+            for (golhip_t h : hs) {
+                uint64_t k = 0;
+                int rc = golhip_flips(h, nullptr, 0, &k);
+                if (rc != GOLHIP_OK && rc != GOLHIP_ERANGE) check(rc);
+                xy.resize(2 * std::max<uint64_t>(k, 1));
+                check(golhip_flips(h, xy.data(), k, &k));
+                for (uint64_t e = 0; e < k; ++e) {
+                    const uint64_t idx = (uint64_t)xy[2 * e + 1] * (uint64_t)W + (uint64_t)xy[2 * e];
+                    if (*n + turn_n + e < cap) buf[*n + turn_n + e] = (uint32_t)idx;
+                }
+                turn_n += k;
+            }
+            counts[t] = turn_n;
+            *n += turn_n;
+            *done = t + 1;
+        }
+        return GOLHIP_OK;
+    }
 };
 
 // Page-locked flip-list buffer the engine's flip kernel writes directly
@@ -104,20 +223,6 @@ struct FlipBuffer {
     }
 };
 
-std::vector<util::Cell> cells_of(golhip_t h, int (*fn)(golhip_t, int32_t *, uint64_t, uint64_t *), bool transpose) {
-    uint64_t n = 0;
-    int rc = fn(h, nullptr, 0, &n);
-    if (rc != GOLHIP_OK && rc != GOLHIP_ERANGE) check(rc);
-    std::vector<int32_t> xy(2 * std::max<uint64_t>(n, 1));
-    check(fn(h, xy.data(), n, &n));
-    std::vector<util::Cell> out(n);
-    for (uint64_t i = 0; i < n; ++i) {
-        out[i].X = transpose ? xy[2 * i + 1] : xy[2 * i];
-        out[i].Y = transpose ? xy[2 * i] : xy[2 * i + 1];
-    }
-    return out;
-}
-
 }  // namespace
 
 void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOptions &opt) {
@@ -131,15 +236,15 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
     std::printf("File %s input done!\n", name.c_str());
     std::fflush(stdout);
 
-    Board board(W, H, opt.device);
-    check(golhip_load_bytes(board.h, raster.data()));
+    Engine board(W, H, opt);
+    board.load(raster.data());
 
     auto send = [&](Event e) {
         if (events) events->send(std::move(e));
     };
     auto write_snapshot = [&](int64_t turn, bool transposed) -> std::string {
         std::vector<uint8_t> snap((size_t)W * H);
-        check(golhip_snapshot_bytes(board.h, snap.data()));
+        board.snapshot(snap.data());
         if (transposed) {  // the reference streams (*world)[x][y] for s/q (distributor.go:234-238)
             std::vector<uint8_t> t((size_t)W * H);
             for (int64_t y = 0; y < H; ++y)
@@ -156,7 +261,7 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
 
     // distributor.go:72-80: CellFlipped for every cell alive at load, turn 0.
     if (opt.cell_events && events)
-        for (const util::Cell &c : cells_of(board.h, golhip_alive_cells, quirks)) {
+        for (const util::Cell &c : board.cells(golhip_alive_cells, quirks)) {
             Event e;
             e.kind = EventKind::CellFlipped;
             e.CompletedTurns = 0;
@@ -203,7 +308,7 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
             int64_t at = 0;
             {
                 auto g = lock_mu();  // blocked while paused, like the reference
-                check(golhip_alive_count(board.h, &n, &at));
+                board.alive_count(&n, &at);
             }
             Event e;
             e.kind = EventKind::AliveCellsCount;
@@ -303,17 +408,14 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
             {
                 std::lock_guard<std::mutex> g(mu);
                 if (opt.cell_events) {
-                    int rc = golhip_flip_stream(board.h, want, GOLHIP_FLIPS_INDEX, fb.p, fb.cap, counts.data(), &done,
-                                                &n);
+                    int rc = board.flip_stream(want, fb.p, fb.cap, counts.data(), &done, &n);
                     if (rc == GOLHIP_ERANGE) {  // one turn needs more than the buffer: grow, nothing advanced
                         fb.grow(n);
-                        rc = golhip_flip_stream(board.h, want, GOLHIP_FLIPS_INDEX, fb.p, fb.cap, counts.data(), &done,
-                                                &n);
+                        rc = board.flip_stream(want, fb.p, fb.cap, counts.data(), &done, &n);
                     }
                     check(rc);
                 } else {
-                    check(golhip_step(board.h, want, 0));
-                    check(golhip_sync(board.h));
+                    board.step(want);
                 }
                 t += done;
                 turn = t;
@@ -357,7 +459,7 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
             return;
         }
         // distributor.go:180-206
-        std::vector<util::Cell> alive = cells_of(board.h, golhip_alive_cells, false);
+        std::vector<util::Cell> alive = board.cells(golhip_alive_cells, false);
         const std::string fname = write_snapshot(p.Turns, false);
         Event io;
         io.kind = EventKind::ImageOutputComplete;

@@ -135,6 +135,13 @@ struct RunOptions {
     double ticker_seconds = 2.0;  // AliveCellsCount period (distributor.go:285)
     int64_t batch_turns = 0;      // turns per engine call (0: 64 with cell events, 256 without);
                                   // keys, pause and the ticker are served between calls
+    // Row-strip decomposition (README halo extension):
+    // ngpu > 1 splits the board into row strips on devices 0..ngpu-1, stepped
+    // together with peer-copied halos (golhip_group_step_ex); strips > 1 sets
+    // the strip count (round-robin over the devices; tests run 2 or 3 strips
+    // on device 0).  -1: from the environment, GOL_NGPU / GOL_STRIPS (unset: 1).
+    int ngpu = -1;
+    int strips = -1;
 };
 
 // The PGM goroutine's file formats (io.go:42-126).

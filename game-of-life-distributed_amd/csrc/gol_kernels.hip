@@ -1274,6 +1274,9 @@ __global__ __launch_bounds__(256) void gol_split_tri_kernel(SplitArgs p) {
 // generation D of [0, H) without wrapping the output; row strips: the
 // halo rows feed the top band's first D rows and the bottom band's drain.
 // ---------------------------------------------------------------------------
+#ifndef GOL_SKEW_STORE_CPOL
+#define GOL_SKEW_STORE_CPOL 0  // cache policy of K1w's output stores (A/B builds: 16 = sc1, 2 = nt)
+#endif
 template <int D>
 struct SkewPlan {
     static constexpr int P1 = D / 4, P2 = D / 2, P3 = 3 * D / 4;
@@ -1340,13 +1343,14 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
         const bool ok = keep && (unsigned)oi < (unsigned)S;
         const int off = ok ? (oi * Ww + col) * 4 : INT_MAX;  // out of range: dropped
         if constexpr (WPL == 1)
-            __builtin_amdgcn_raw_buffer_store_b32(y.w[0], brs, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(y.w[0], brs, off, 0, GOL_SKEW_STORE_CPOL);
         else if constexpr (WPL == 2)
             __builtin_amdgcn_raw_buffer_store_b64((__attribute__((ext_vector_type(2))) unsigned){y.w[0], y.w[1]}, brs,
-                                                  off, 0, 0);
+                                                  off, 0, GOL_SKEW_STORE_CPOL);
         else
             __builtin_amdgcn_raw_buffer_store_b128(
-                (__attribute__((ext_vector_type(4))) unsigned){y.w[0], y.w[1], y.w[2], y.w[3]}, brs, off, 0, 0);
+                (__attribute__((ext_vector_type(4))) unsigned){y.w[0], y.w[1], y.w[2], y.w[3]}, brs, off, 0,
+                GOL_SKEW_STORE_CPOL);
         uint32_t pc = 0;
 #pragma unroll
         for (int k = 0; k < WPL; ++k) pc += __builtin_popcount(y.w[k]);

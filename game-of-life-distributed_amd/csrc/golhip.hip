@@ -558,6 +558,13 @@ bool split_plan(golhip_t h, int depth, int wpl, golk::SplitArgs *sp) {
     int nreg = std::max(1, pairs / tiles);
     nreg = std::min(nreg, h->rows / minlen);
     if (nreg < 1) return false;
+    // a region's buffer-store range (WPL <= 2: one resource over its rows) must
+    // stay < 2 GiB: more regions (they only need minlen rows each), else K1
+    const int64_t row_bytes = (int64_t)h->Ww * 4;
+    while (wpl <= 2 && ((int64_t)h->rows + nreg - 1) / nreg * row_bytes >= (1ll << 31)) {
+        if (nreg >= h->rows / minlen) return false;
+        ++nreg;
+    }
     sp->nreg = nreg;
     sp->tiles_x = tiles;
     sp->P0 = P0;
@@ -876,8 +883,13 @@ bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int w
     return true;
 }
 
+// The resident kernel's depths: 4, 8, 16 and, at one word per lane, 32 (its
+// instantiations); the per-launch depths 20, 24, 12, 9, 6 are not among them.
 int persist_depth_for(golhip_t h, int wpl) {
-    return largest_depth(std::min(h->persist_depth > 0 ? h->persist_depth : h->tb_depth, golk::persist_max_depth(wpl)));
+    const int cap = std::min(h->persist_depth > 0 ? h->persist_depth : h->tb_depth, golk::persist_max_depth(wpl));
+    for (int d : {32, 16, 8, 4})
+        if (d <= cap) return d;
+    return 1;
 }
 
 // Torus: J super-steps of `depth` turns in one resident launch; returns the
@@ -887,7 +899,7 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     if (!persist_on(h) || h->W % 32 != 0 || !h->torus()) return 0;
     const int wpl = wpl_for(h);
     const int depth = persist_depth_for(h, wpl);
-    if (depth < 4) return 0;
+    if (depth < 4 || golk::persist_blocks_per_cu(depth, wpl, persist_nw_for(h, depth, wpl)) < 1) return 0;
     int64_t J = left / depth;
     if (J < 2) return 0;
     // a remainder of exactly depth / 2 turns (1000 = 62 x 16 + 8) becomes a
@@ -1123,8 +1135,11 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
     const int64_t nb = golk::flip_turn_blocks(nw);
     const bool contig = h->Ww % 4 == 0;
     const int bpc = std::min(golk::flip_turn_blocks_per_cu(contig), 4);
-    // every block resident at once (with a 10 % margin): block order = blockIdx
-    const bool coresident = !h->ft_ticket && bpc > 0 && nb * 10 <= (int64_t)h->cu_count * bpc * 9;
+    // every block resident at once (with a 10 % margin): block order = blockIdx.
+    // Not in a multi-rank ring: its fallback (restore, re-run in ticket order)
+    // would redo the batch's exchanges on this rank alone and hang the ring.
+    const bool coresident = !h->ft_ticket && !(h->comm && h->nranks > 1) && bpc > 0 &&
+                            nb * 10 <= (int64_t)h->cu_count * bpc * 9;
     // launch the turns the buffer probably holds (the last batch's largest
     // list); turns past an overflow would only return at once
     int64_t nlaunch = nturns;
@@ -1645,7 +1660,11 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     if (int rc = set_dev(h)) return rc;
     const int64_t turns0 = h->turns;
     const int cur0 = h->cur;
+    // counters of this step, restored if a resident launch is abandoned below
     const int64_t persist_turns0 = h->persist_turns, persist_launches0 = h->persist_launches;
+    const int64_t step_launches0 = h->step_launches, step_turns0 = h->step_turns;
+    const int64_t split_launches0 = h->split_launches, skew_launches0 = h->skew_launches;
+    const size_t ev0 = h->ev_pending.size();
     int rc = step_locked(h, nturns, want_flips);
     if (rc || !h->guarded) return rc;
     // A resident launch ran (torus): check it before returning.  Its
@@ -1662,6 +1681,17 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     h->persist_fallbacks++;
     h->persist_turns = persist_turns0;
     h->persist_launches = persist_launches0;
+    h->step_launches = step_launches0;
+    h->step_turns = step_turns0;
+    h->split_launches = split_launches0;
+    h->skew_launches = skew_launches0;
+    if (h->ev_pending.size() >= ev0) {  // the abandoned attempt's launch timings (unless drained meanwhile)
+        for (size_t i = ev0; i < h->ev_pending.size(); ++i) {
+            h->ev_pool.push_back(h->ev_pending[i].e0);
+            h->ev_pool.push_back(h->ev_pending[i].e1);
+        }
+        h->ev_pending.resize(ev0);
+    }
     HIP_OR_FAIL(hipMemcpyAsync(h->buf[cur0] + (int64_t)kHalo * h->Ww, h->backup, (size_t)h->local_words() * 4,
                                hipMemcpyDeviceToDevice, h->stream));
     h->cur = cur0;
@@ -1671,7 +1701,14 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     return step_locked(h, nturns, want_flips);
 }
 
-int golhip_group_step(golhip_t *hs, int32_t n, int64_t nturns) {
+}  // extern "C"
+
+namespace {
+// golhip_group_step[_ex]: n strips (ring order = array order) driven from one
+// process, halos moved by peer copies; want_flips keeps every strip's flip
+// list of the last turn (golhip_flips, global coordinates, strip order =
+// row-major order of the board).
+int group_step_impl(golhip_t *hs, int32_t n, int64_t nturns, int32_t want_flips) {
     if (!hs || n < 1 || nturns < 0) return fail(GOLHIP_EINVAL, "bad group");
     for (int i = 0; i < n; ++i) {
         if (int rc = check(hs[i])) return rc;
@@ -1693,7 +1730,44 @@ int golhip_group_step(golhip_t *hs, int32_t n, int64_t nturns) {
         if (!rc) rc = set_layout(hs[i], want_il(hs[i]));
         hs[i]->flips_valid = false;
     }
-    int64_t left = nturns;
+    // halo rows of every strip from its ring neighbours' current boards: x rows each way
+    auto exchange = [&](int x) {
+        for (int i = 0; i < n && !rc; ++i) {
+            HIP_RC(hipSetDevice(hs[i]->device));
+            HIP_RC(hipEventRecord(ready[i], hs[i]->stream));
+        }
+        for (int i = 0; i < n && !rc; ++i) {
+            golhip *me = hs[i], *prev = hs[(i - 1 + n) % n], *next = hs[(i + 1) % n];
+            golhip_halo_plan_t p;
+            plan(me->rows, n, i, x, me->Ww, &p);
+            HIP_RC(hipSetDevice(me->device));
+            HIP_RC(hipStreamWaitEvent(me->stream, ready[(i - 1 + n) % n], 0));
+            HIP_RC(hipStreamWaitEvent(me->stream, ready[(i + 1) % n], 0));
+            const size_t bytes = (size_t)p.bytes;
+            // top halo <- prev's last x rows; bottom halo <- next's first x rows
+            uint32_t *mb = me->buf[me->cur];
+            const uint32_t *pb = prev->buf[prev->cur] + (int64_t)(kHalo + prev->rows - x) * prev->Ww;
+            const uint32_t *nb = next->buf[next->cur] + (int64_t)kHalo * next->Ww;
+            HIP_RC(hipMemcpyPeerAsync(mb + (int64_t)p.recv_top_row * me->Ww, me->device, pb, prev->device, bytes,
+                                      me->stream));
+            HIP_RC(hipMemcpyPeerAsync(mb + (int64_t)p.recv_bottom_row * me->Ww, me->device, nb, next->device,
+                                      bytes, me->stream));
+            me->halo_bytes += 2 * (int64_t)bytes;
+        }
+        // a strip's second launch rewrites the buffer its neighbours copied
+        // from: every stream waits for its neighbours' copies first
+        for (int i = 0; i < n && !rc; ++i) {
+            HIP_RC(hipSetDevice(hs[i]->device));
+            HIP_RC(hipEventRecord(ready[i], hs[i]->stream));
+        }
+        for (int i = 0; i < n && !rc; ++i) {
+            HIP_RC(hipSetDevice(hs[i]->device));
+            HIP_RC(hipStreamWaitEvent(hs[i]->stream, ready[(i - 1 + n) % n], 0));
+            HIP_RC(hipStreamWaitEvent(hs[i]->stream, ready[(i + 1) % n], 0));
+        }
+    };
+    const int64_t tail = (want_flips && nturns > 0) ? 1 : 0;
+    int64_t left = nturns - tail;
     while (left > 0 && rc == GOLHIP_OK) {
         int cap = GOLHIP_MAX_TB_DEPTH;
         for (int i = 0; i < n; ++i) cap = std::min(cap, depth_cap(hs[i], n > 1));
@@ -1703,40 +1777,7 @@ int golhip_group_step(golhip_t *hs, int32_t n, int64_t nturns) {
         if (n > 1) {
             k = kHalo / d;
             for (int i = 0; i < n; ++i) k = std::min(k, halo_launches(hs[i]->rows, d, run.n));
-            const int x = k * d;  // rows exchanged
-            for (int i = 0; i < n && !rc; ++i) {
-                HIP_RC(hipSetDevice(hs[i]->device));
-                HIP_RC(hipEventRecord(ready[i], hs[i]->stream));
-            }
-            for (int i = 0; i < n && !rc; ++i) {
-                golhip *me = hs[i], *prev = hs[(i - 1 + n) % n], *next = hs[(i + 1) % n];
-                golhip_halo_plan_t p;
-                plan(me->rows, n, i, x, me->Ww, &p);
-                HIP_RC(hipSetDevice(me->device));
-                HIP_RC(hipStreamWaitEvent(me->stream, ready[(i - 1 + n) % n], 0));
-                HIP_RC(hipStreamWaitEvent(me->stream, ready[(i + 1) % n], 0));
-                const size_t bytes = (size_t)p.bytes;
-                // top halo <- prev's last x rows; bottom halo <- next's first x rows
-                uint32_t *mb = me->buf[me->cur];
-                const uint32_t *pb = prev->buf[prev->cur] + (int64_t)(kHalo + prev->rows - x) * prev->Ww;
-                const uint32_t *nb = next->buf[next->cur] + (int64_t)kHalo * next->Ww;
-                HIP_RC(hipMemcpyPeerAsync(mb + (int64_t)p.recv_top_row * me->Ww, me->device, pb, prev->device, bytes,
-                                          me->stream));
-                HIP_RC(hipMemcpyPeerAsync(mb + (int64_t)p.recv_bottom_row * me->Ww, me->device, nb, next->device,
-                                          bytes, me->stream));
-                me->halo_bytes += 2 * (int64_t)bytes;
-            }
-            // a strip's second launch rewrites the buffer its neighbours copied
-            // from: every stream waits for its neighbours' copies first
-            for (int i = 0; i < n && !rc; ++i) {
-                HIP_RC(hipSetDevice(hs[i]->device));
-                HIP_RC(hipEventRecord(ready[i], hs[i]->stream));
-            }
-            for (int i = 0; i < n && !rc; ++i) {
-                HIP_RC(hipSetDevice(hs[i]->device));
-                HIP_RC(hipStreamWaitEvent(hs[i]->stream, ready[(i - 1 + n) % n], 0));
-                HIP_RC(hipStreamWaitEvent(hs[i]->stream, ready[(i + 1) % n], 0));
-            }
+            exchange(k * d);
         }
         for (int j = 0; j < k && rc == GOLHIP_OK; ++j) {
             for (int i = 0; i < n && !rc; ++i) {
@@ -1748,6 +1789,14 @@ int golhip_group_step(golhip_t *hs, int32_t n, int64_t nturns) {
             left -= d;
         }
     }
+    if (tail && rc == GOLHIP_OK) {  // the last turn alone, then its flip list on every strip
+        if (n > 1) exchange(1);
+        for (int i = 0; i < n && !rc; ++i) {
+            HIP_RC(hipSetDevice(hs[i]->device));
+            if (!rc) rc = n > 1 ? launch_ext(hs[i], 1, true, 0) : launch_depth(hs[i], 1, true, false);
+            if (!rc) rc = start_flips(hs[i]);
+        }
+    }
     for (int i = 0; i < n; ++i) {
         HIP_RC(hipSetDevice(hs[i]->device));
         if (ready[i]) {
@@ -1756,6 +1805,15 @@ int golhip_group_step(golhip_t *hs, int32_t n, int64_t nturns) {
         }
     }
     return rc;
+}
+}  // namespace
+
+extern "C" {
+
+int golhip_group_step(golhip_t *hs, int32_t n, int64_t nturns) { return group_step_impl(hs, n, nturns, 0); }
+
+int golhip_group_step_ex(golhip_t *hs, int32_t n, int64_t nturns, int32_t want_flips) {
+    return group_step_impl(hs, n, nturns, want_flips);
 }
 
 int golhip_sync(golhip_t h) {
@@ -1816,9 +1874,24 @@ int golhip_step_flips(golhip_t h, int64_t nturns, int32_t *xy, uint64_t cap, uin
     if (nturns > 0 && !counts) return fail(GOLHIP_EINVAL, "counts is null");
     if (cap > 0 && !xy) return fail(GOLHIP_EINVAL, "xy is null");
     std::lock_guard<std::mutex> g(h->mu);
-    int64_t done = 0;
+    // The flip kernel's look-back prefixes carry 40-bit offsets: run the batch
+    // in chunks whose lists cannot reach 2^40 entries (every cell flipping
+    // every turn), each appending after the last.
+    const uint64_t cells = std::max<uint64_t>(1, (uint64_t)h->W * (uint64_t)h->rows);
+    const int64_t chunk = std::max<int64_t>(1, (int64_t)((1ull << 40) / cells) - 1);
     uint64_t total = 0;
-    if (int rc = flip_stream_locked(h, nturns, GOLHIP_FLIPS_XY, xy, cap, counts, &done, &total, false)) return rc;
+    for (int64_t t = 0; t < nturns || (t == 0 && nturns == 0);) {
+        const int64_t m = std::min<int64_t>(chunk, nturns - t);
+        const uint64_t got = std::min<uint64_t>(total, cap);
+        int64_t done = 0;
+        uint64_t part = 0;
+        if (int rc = flip_stream_locked(h, m, GOLHIP_FLIPS_XY, xy ? xy + 2 * got : nullptr, cap - got, counts + t, &done,
+                                        &part, false))
+            return rc;
+        total += part;
+        t += m;
+        if (m == 0) break;
+    }
     if (n) *n = total;
     if (total > cap)
         return fail(GOLHIP_ERANGE, "buffer holds %llu cells, %llu needed", (unsigned long long)cap,

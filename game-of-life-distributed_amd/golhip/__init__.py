@@ -109,6 +109,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "golhip_comm_unique_id": ([ctypes.c_char_p], ctypes.c_int),
         "golhip_comm_init": ([H, ctypes.c_char_p, i32, i32], ctypes.c_int),
         "golhip_group_step": ([P(H), i32, i64], ctypes.c_int),
+        "golhip_group_step_ex": ([P(H), i32, i64, i32], ctypes.c_int),
         "golhip_halo_plan": ([i32, i32, i32, i32, i32, P(HaloPlan)], ctypes.c_int),
         "golhip_halo_schedule": ([i32, i32, i32, i64, P(i32), P(i32)], ctypes.c_int),
         "golhip_load_bytes": ([H, ctypes.c_void_p], ctypes.c_int),
@@ -382,9 +383,12 @@ class Board:
         _check(load().golhip_perf_reset(self._h))
 
 
-def group_step(boards: list[Board], nturns: int) -> None:
+def group_step(boards: list[Board], nturns: int, want_flips: bool = False) -> None:
     arr = (ctypes.c_void_p * len(boards))(*[b.handle for b in boards])
-    _check(load().golhip_group_step(arr, len(boards), nturns))
+    if want_flips:
+        _check(load().golhip_group_step_ex(arr, len(boards), nturns, 1))
+    else:
+        _check(load().golhip_group_step(arr, len(boards), nturns))
 
 
 def board_hash_np(words: np.ndarray, row0: int = 0) -> int:

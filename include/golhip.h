@@ -159,6 +159,11 @@ int golhip_comm_init(golhip_t h, const uint8_t id[GOLHIP_UNIQUE_ID_BYTES], int32
 /* Steps n strips (ring order = array order) driven from one process; halos
  * move with peer/device copies.  Same semantics as golhip_step on each. */
 int golhip_group_step(golhip_t *hs, int32_t n, int64_t nturns);
+/* golhip_group_step with golhip_step's want_flips: every strip keeps the flip
+ * list of the last turn for golhip_flips (global coordinates; concatenated in
+ * strip order they are the board's row-major list).  Used by gol.Run with
+ * GOL_NGPU / GOL_STRIPS (the row-strip decomposition behind the drop-in). */
+int golhip_group_step_ex(golhip_t *hs, int32_t n, int64_t nturns, int32_t want_flips);
 
 /* Halo plan used by both transports (exposed for tests): rows this strip
  * sends up/down and receives for an exchange of `depth` rows

@@ -18,20 +18,30 @@ package gol
 import "C"
 
 import (
+	"os"
+	"strconv"
 	"unsafe"
 
 	"uk.ac.bris.cs/gameoflife/util"
 )
 
-// engine is one libgolhip handle: the board of one Run on one GPU.
+// engine is the board of one Run: one libgolhip handle (a whole torus on
+// GPU 0) or, with GOL_NGPU=n / GOL_STRIPS=k in the environment (SURVEY 5's
+// config row; the README's halo-exchange extension), k row strips on devices
+// 0..n-1 (k = n by default) stepped together by golhip_group_step_ex, their
+// halo rows moved between the strips' devices by peer copies.  Side channels
+// of the strips are gathered in strip order, which is the board's row-major
+// order: alive lists and flip lists concatenate, counts add up.
 type engine struct {
-	h      C.golhip_t
+	hs     []C.golhip_t // one handle per strip, top to bottom
+	row0   []int        // first board row of each strip
 	width  int
 	height int
 
 	flipsP unsafe.Pointer // golhip_host_alloc buffer of cell indices y*width + x
 	flips  []uint32       // a Go view of it
 	counts []uint64       // per-turn list lengths of the last flipStream
+	xy     []int32        // strips: one strip's flip pairs of a turn
 }
 
 // check turns a libgolhip status into the reference's fail-fast behaviour
@@ -42,13 +52,55 @@ func check(rc C.int) {
 	}
 }
 
+func envInt(name string, dflt int) int {
+	if v, err := strconv.Atoi(os.Getenv(name)); err == nil {
+		return v
+	}
+	return dflt
+}
+
 // newEngine replaces the world allocation and fill of distributor.go:66-80:
 // cells is the raster the io goroutine sent, row-major, alive <=> 255.
 func newEngine(p Params, cells []byte) *engine {
-	var h C.golhip_t
-	check(C.golhip_create(C.int32_t(p.ImageWidth), C.int32_t(p.ImageHeight), 0, 0, &h))
-	e := &engine{h: h, width: p.ImageWidth, height: p.ImageHeight}
-	check(C.golhip_load_bytes(h, (*C.uint8_t)(unsafe.Pointer(&cells[0]))))
+	e := &engine{width: p.ImageWidth, height: p.ImageHeight}
+	ngpu := envInt("GOL_NGPU", 1)
+	n := envInt("GOL_STRIPS", 0)
+	if n <= 0 {
+		n = ngpu
+	}
+	if n > p.ImageHeight {
+		n = p.ImageHeight
+	}
+	if n <= 1 {
+		var h C.golhip_t
+		check(C.golhip_create(C.int32_t(p.ImageWidth), C.int32_t(p.ImageHeight), 0, 0, &h))
+		e.hs, e.row0 = []C.golhip_t{h}, []int{0}
+	} else {
+		var ndev C.int32_t
+		check(C.golhip_device_count(&ndev))
+		devs := ngpu
+		if devs > int(ndev) {
+			devs = int(ndev)
+		}
+		if devs < 1 {
+			devs = 1
+		}
+		for i := 0; i < n; i++ {
+			r0, r1 := p.ImageHeight*i/n, p.ImageHeight*(i+1)/n
+			var h C.golhip_t
+			rc := C.golhip_create_strip(C.int32_t(p.ImageWidth), C.int32_t(p.ImageHeight), C.int32_t(r0),
+				C.int32_t(r1-r0), C.int32_t(i%devs), 0, &h)
+			if rc != C.GOLHIP_OK {
+				e.close()
+				check(rc)
+			}
+			e.hs = append(e.hs, h)
+			e.row0 = append(e.row0, r0)
+		}
+	}
+	for i, h := range e.hs {
+		check(C.golhip_load_bytes(h, (*C.uint8_t)(unsafe.Pointer(&cells[e.row0[i]*e.width]))))
+	}
 	return e
 }
 
@@ -58,16 +110,29 @@ func (e *engine) close() {
 		e.flipsP = nil
 		e.flips = nil
 	}
-	if e.h != nil {
-		C.golhip_destroy(e.h)
-		e.h = nil
+	for i, h := range e.hs {
+		if h != nil {
+			C.golhip_destroy(h)
+			e.hs[i] = nil
+		}
 	}
+}
+
+// group is the strips' handle array for golhip_group_step_ex (Go memory
+// holding C pointers only, valid for the call).
+func (e *engine) group(turns int, wantFlips int) {
+	check(C.golhip_group_step_ex((*C.golhip_t)(unsafe.Pointer(&e.hs[0])), C.int32_t(len(e.hs)), C.int64_t(turns),
+		C.int32_t(wantFlips)))
 }
 
 // step runs n turns in fused launches (no per-turn side channels).
 func (e *engine) step(n int) {
-	check(C.golhip_step(e.h, C.int64_t(n), 0))
-	check(C.golhip_sync(e.h))
+	if len(e.hs) == 1 {
+		check(C.golhip_step(e.hs[0], C.int64_t(n), 0))
+		check(C.golhip_sync(e.hs[0]))
+		return
+	}
+	e.group(n, 0)
 }
 
 func (e *engine) growFlips(n int) {
@@ -91,20 +156,27 @@ func (e *engine) growFlips(n int) {
 // indices y*width + x, row-major within a turn.  The batch stops early rather
 // than drop an entry; the views are valid until the next call.
 func (e *engine) flipStream(n int) (int, []uint64, []uint32) {
+	most := e.width * e.height // one turn flips at most every cell
 	if e.flipsP == nil {
-		most := e.width * e.height // one turn flips at most every cell
-		if most > 16<<20 {
-			most = 16 << 20
+		first := most
+		if first > 16<<20 {
+			first = 16 << 20
 		}
-		e.growFlips(most)
+		if len(e.hs) > 1 {
+			first = most // strips: a whole turn's worst case, see below
+		}
+		e.growFlips(first)
 	}
 	if len(e.counts) < n {
 		e.counts = make([]uint64, n)
 	}
+	if len(e.hs) > 1 {
+		return e.stripFlipStream(n, most)
+	}
 	var done C.int64_t
 	var total C.uint64_t
 	call := func() C.int {
-		return C.golhip_flip_stream(e.h, C.int64_t(n), C.GOLHIP_FLIPS_INDEX, e.flipsP, C.uint64_t(len(e.flips)),
+		return C.golhip_flip_stream(e.hs[0], C.int64_t(n), C.GOLHIP_FLIPS_INDEX, e.flipsP, C.uint64_t(len(e.flips)),
 			(*C.uint64_t)(unsafe.Pointer(&e.counts[0])), &done, &total)
 	}
 	rc := call()
@@ -116,36 +188,75 @@ func (e *engine) flipStream(n int) (int, []uint64, []uint32) {
 	return int(done), e.counts[:int(done)], e.flips[:int(total)]
 }
 
+// stripFlipStream: one group turn at a time (golhip_group_step_ex keeps each
+// strip's list of that turn), the strips' lists appended in strip order;
+// stops before a turn whose worst case would not fit the buffer.
+func (e *engine) stripFlipStream(n int, most int) (int, []uint64, []uint32) {
+	total, done := 0, 0
+	for ; done < n && total+most <= len(e.flips); done++ {
+		e.group(1, 1)
+		turnN := 0
+		for _, h := range e.hs {
+			var k C.uint64_t
+			if rc := C.golhip_flips(h, nil, 0, &k); rc != C.GOLHIP_OK && rc != C.GOLHIP_ERANGE {
+				check(rc)
+			}
+			if k == 0 {
+				continue
+			}
+			if len(e.xy) < 2*int(k) {
+				e.xy = make([]int32, 2*int(k))
+			}
+			check(C.golhip_flips(h, (*C.int32_t)(unsafe.Pointer(&e.xy[0])), k, &k))
+			for i := 0; i < int(k); i++ {
+				e.flips[total+turnN+i] = uint32(int(e.xy[2*i+1])*e.width + int(e.xy[2*i]))
+			}
+			turnN += int(k)
+		}
+		e.counts[done] = uint64(turnN)
+		total += turnN
+	}
+	return done, e.counts[:done], e.flips[:total]
+}
+
 // aliveCells is calculateAliveCells (distributor.go:420-432): Cell{X: col, Y: row}, row-major.
 func (e *engine) aliveCells() []util.Cell {
-	var n C.uint64_t
-	if rc := C.golhip_alive_cells(e.h, nil, 0, &n); rc != C.GOLHIP_OK && rc != C.GOLHIP_ERANGE {
-		check(rc)
-	}
-	if n == 0 {
-		return []util.Cell{}
-	}
-	xy := make([]int32, 2*int(n))
-	check(C.golhip_alive_cells(e.h, (*C.int32_t)(unsafe.Pointer(&xy[0])), n, &n))
-	cells := make([]util.Cell, int(n))
-	for i := range cells {
-		cells[i] = util.Cell{X: int(xy[2*i]), Y: int(xy[2*i+1])}
+	cells := []util.Cell{}
+	for _, h := range e.hs {
+		var n C.uint64_t
+		if rc := C.golhip_alive_cells(h, nil, 0, &n); rc != C.GOLHIP_OK && rc != C.GOLHIP_ERANGE {
+			check(rc)
+		}
+		if n == 0 {
+			continue
+		}
+		xy := make([]int32, 2*int(n))
+		check(C.golhip_alive_cells(h, (*C.int32_t)(unsafe.Pointer(&xy[0])), n, &n))
+		for i := 0; i < int(n); i++ {
+			cells = append(cells, util.Cell{X: int(xy[2*i]), Y: int(xy[2*i+1])})
+		}
 	}
 	return cells
 }
 
 // aliveCount is the ticker's len(calculateAliveCells(world)) (:292) with the
-// turn it belongs to, read together (the reference reads *turn unlocked, :294).
+// turn it belongs to, read together (the reference reads *turn unlocked, :294);
+// strips add their counts (all at the same turn: the caller holds mu).
 func (e *engine) aliveCount() (turn int, count int) {
-	var n C.uint64_t
-	var t C.int64_t
-	check(C.golhip_alive_count(e.h, &n, &t))
-	return int(t), int(n)
+	for _, h := range e.hs {
+		var n C.uint64_t
+		var t C.int64_t
+		check(C.golhip_alive_count(h, &n, &t))
+		turn, count = int(t), count+int(n)
+	}
+	return turn, count
 }
 
 // snapshot is the board as the 0/255 raster the io goroutine writes (:186-191).
 func (e *engine) snapshot() []byte {
 	out := make([]byte, e.width*e.height)
-	check(C.golhip_snapshot_bytes(e.h, (*C.uint8_t)(unsafe.Pointer(&out[0]))))
+	for i, h := range e.hs {
+		check(C.golhip_snapshot_bytes(h, (*C.uint8_t)(unsafe.Pointer(&out[e.row0[i]*e.width]))))
+	}
 	return out
 }

@@ -23,6 +23,7 @@ ap.add_argument("--sets", default="skew=1;skew=0")
 ap.add_argument("--turns", type=int, default=1000)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--depth", type=int, default=20)
+ap.add_argument("--no-timing", action="store_true", help="no per-launch HIP timing events (wall clock only)")
 a = ap.parse_args()
 sets = [dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in s.split(",") if kv) for s in a.sets.split(";")]
 best = {}
@@ -31,7 +32,7 @@ for rep in range(a.reps):
         ring = case.endswith("r")
         W, R = (int(x) for x in case.rstrip("r").split("x"))
         for opts in sets:
-            with golhip.Board(W, R, timing=True) as b:
+            with golhip.Board(W, R, timing=not a.no_timing) as b:
                 if ring:
                     b.comm_init(golhip.unique_id(), 1, 0)
                     b.set_option("force_halo", 1)
@@ -53,7 +54,7 @@ for rep in range(a.reps):
                 g = W * R * a.turns / dt / 1e9
                 key = (case, json.dumps(opts))
                 best[key] = max(best.get(key, 0), g)
-                print(json.dumps({"case": case, "opts": opts, "rep": rep, "gcups": round(g, 1),
+                print(json.dumps({"case": case, "opts": opts, "lib": os.path.basename(golhip.LIB_PATH), "rep": rep, "gcups": round(g, 1),
                                   "launch_ms": round(p["step_kernel_ms"] / max(1, p["step_launches"]), 5),
                                   "skew": p["skew_launches"], "split": p["split_launches"],
                                   "launches": p["step_launches"], "persist": p["persist_launches"]}), flush=True)

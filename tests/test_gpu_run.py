@@ -233,3 +233,42 @@ def test_config4_5120_event_stream_through_run(tmp_path):
     out = read_pgm(str(tmp_path / "out" / f"{N}x{N}x{T}.pgm"), N, N)
     assert int((out == 255).sum()) == final_alive
     print(f"gol.Run 5120^2 with every CellFlipped: {T} turns, {counts['CellFlipped']} events in {dt:.1f} s")
+
+
+# ---------------------------------------------------------------- row strips behind gol.Run (GOL_STRIPS / GOL_NGPU)
+@pytest.fixture(params=[2, 3])
+def strips(request, monkeypatch):
+    """gol.Run on 2 or 3 row strips of device 0 (GOL_STRIPS; GOL_NGPU=n puts
+    them on devices 0..n-1): halos by peer copies, side channels gathered in
+    strip order (golhip_group_step_ex)."""
+    monkeypatch.setenv("GOL_STRIPS", str(request.param))
+    monkeypatch.setenv("GOL_NGPU", "1")
+    return request.param
+
+
+@pytest.mark.parametrize("n", [16, 64, 512])
+@pytest.mark.parametrize("turns", [0, 1, 100])
+def test_gol_strips(root, fixtures, strips, n, turns):
+    test_gol(root, fixtures, n, turns, 8)
+
+
+@pytest.mark.parametrize("n", [16, 64, 512])
+@pytest.mark.parametrize("turns", [0, 1, 100])
+def test_pgm_strips(root, manifest, strips, n, turns):
+    test_pgm(root, manifest, n, turns)
+
+
+def test_sdl_strips(root, fixtures, strips):
+    test_sdl(root, fixtures)
+
+
+def test_alive_strips(root, fixtures, strips):
+    test_alive(root, fixtures)
+
+
+def test_event_order_strips(root, fixtures, strips):
+    test_event_order(root, fixtures)
+
+
+def test_snapshot_key_s_strips(root, fixtures, strips):
+    test_snapshot_key_s(root, fixtures)
