@@ -185,9 +185,13 @@ def cpu_config0() -> dict:
                       "worker-pool port; parity vs check/images/512x512x100.pgm"}
 
 
-def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str) -> dict:
-    """Roofline of the dominant step kernel, from HIP events around every launch
-    on the engine stream (GOLHIP_FLAG_TIMING; launch-averaged).
+def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str, region_ms: float) -> dict:
+    """Roofline of the dominant step kernel, from two HIP events on the
+    engine's stream around the whole timed region (region_ms): the average
+    launch = region / launches, kernel boundaries included (per-launch events
+    cost ~5 us a launch themselves: 16384^2 ran 66 vs 74 TCUPS with and
+    without them, profiles/r3d), so rocprofv3's per-kernel average is that
+    minus the ~2 us gap between dependent launches.
 
     The kernels are VALU-issue-bound: a launch fuses 8-16
     turns per board pass, so HBM moves ~1/D of the single-pass bytes.  `frac`
@@ -199,8 +203,8 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str) 
     command (scripts/pmc_bench.sh -> profiles/pmc_bench.json): measured bytes
     (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) per launch of the same
     kernel / the live launch time / 8 TB/s."""
-    if perf["persist_kernel_ms"] >= perf["step_kernel_ms"]:
-        kname, launches, kms, kturns = "gol_persist_kernel", perf["persist_launches"], perf["persist_kernel_ms"], \
+    if perf["persist_turns"] >= perf["step_turns"]:
+        kname, launches, kms, kturns = "gol_persist_kernel", perf["persist_launches"], region_ms, \
             perf["persist_turns"]
         depth = perf["persist_depth"]
     else:
@@ -209,7 +213,7 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str) 
         # 11 split launches of 8 turns + 2 paired-band launches of 6)
         kname = ("gol_skew_kernel" if 2 * perf.get("skew_launches", 0) > perf["step_launches"] else
                  "gol_split" if 2 * perf.get("split_launches", 0) > perf["step_launches"] else "gol_tb_pair_kernel")
-        launches, kms, kturns = perf["step_launches"], perf["step_kernel_ms"], perf["step_turns"]
+        launches, kms, kturns = perf["step_launches"], region_ms, perf["step_turns"]
         depth = perf["tb_depth"]
     launches = max(1, launches)
     avg_s = kms / launches * 1e-3
@@ -229,6 +233,7 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str) 
         "traffic": None,
         "kernel": (f"gol_split_pair_kernel<{depth}, {wpl}> + gol_split_tri_kernel<{depth}, {wpl}>"
                    if kname == "gol_split" else f"{kname}<{depth}, {wpl}>"),
+        "launch_time": "HIP events on the engine stream around the timed region / launches (boundaries included)",
         "avg_launch_ms": round(avg_s * 1e3, 5),
         "launches": launches,
         "split_launches": perf.get("split_launches", 0),
@@ -394,8 +399,8 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    board = golhip.Board(W, H, device=local, row0=row0, rows=rows, timing=True) if world > 1 \
-        else golhip.Board(W, H, device=local, timing=True)
+    board = golhip.Board(W, H, device=local, row0=row0, rows=rows) if world > 1 \
+        else golhip.Board(W, H, device=local)
     board.set_tb_depth(a.tb_depth)
     board.set_rows_per_wave(a.rows_per_wave)
     for kv in a.option:
@@ -451,12 +456,17 @@ def main():
         board.step(tps)
     barrier()
     board.perf_reset()
+    engine_stream = torch.cuda.ExternalStream(board.stream())
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record(engine_stream)
     for _ in range(a.steps):
         board.step(tps)
+    ev1.record(engine_stream)
     board.sync()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    region_ms = ev0.elapsed_time(ev1)
     if dist is not None:
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -492,7 +502,7 @@ def main():
             "words_per_lane": perf["words_per_lane"],
             "parallelism": f"row strips x{world} (RCCL halo ring)" if world > 1 else "single GPU torus",
         },
-        "roofline": roofline_block(perf, W, rows, N, a.pmc),
+        "roofline": roofline_block(perf, W, rows, N, a.pmc, region_ms),
         "final_alive": alive_end,
         "final_turn": at_turn,
     }

@@ -119,7 +119,7 @@ struct golhip {
     int64_t split_meet_cap = 0;
     int last_variant = 1;           // kernel family of the last step launch (golhip_perf kernel_variant)
     int skew = 1;                   // option "skew": skewed band stacks (K1w) for per-launch steps
-    int skew_young = 100;           // option "skew_young": band height of waves 4..7, % of waves 0..3's
+    int skew_young = 0;             // option "skew_young": band height of waves 4..7, % of waves 0..3's (0: by kernel)
     int skew_hcap = -1;             // option "skew_hcap": rows a stack's bottom band gives up (-1: 3 D / 4)
     int skew_prio = 0;              // option "skew_prio": s_setprio 1 for waves 4..7
     int skew_tx = 0;                // option "skew_tx": tiles per K1w workgroup (0: plan, 1 or 2)
@@ -633,6 +633,12 @@ bool skew_plan(golhip_t h, int depth, int wpl, const golk::StepArgs &a, golk::Sk
         }
     }
     if (!best_tx) return false;
+    // "skew" 1 (default): only when the stacks fill at least 3/4 of the CUs'
+    // workgroup slots (a 5120^2 board makes 32 stacks of 2 tiles: the
+    // per-launch kernels with short bands are faster there); 2: whenever a
+    // plan exists (tests)
+    if (h->skew == 1 && (int64_t)best_nst * ((tiles + best_tx - 1) / best_tx) * 4 < (int64_t)h->cu_count * bpc * 3)
+        return false;
     // a wave's buffer-store range (its band) must stay < 2 GiB
     if (((double)L / best_nst + hcap) * h->Ww * 4 >= 2147483648.0) return false;
     if (!h->skew_err) {
@@ -650,7 +656,11 @@ bool skew_plan(golhip_t h, int depth, int wpl, const golk::StepArgs &a, golk::Sk
     sk->tx = best_tx;
     sk->nst = best_nst;
     const int sy = 8 / best_tx;
-    for (int q = 0; q < 8; ++q) sk->wgt[q] = (q < sy && q * best_tx >= 4) ? h->skew_young : 100;
+    // The SIMD arbiter serves the older wave of a SIMD (waves 0..3) first: the
+    // younger waves' bands are shorter so both finish together.  Measured
+    // (profiles/r3b, r3d): two words per lane 66-70 %, quads at depth 9 76-82 %.
+    const int young = h->skew_young > 0 ? h->skew_young : wpl == 4 ? 78 : 68;
+    for (int q = 0; q < 8; ++q) sk->wgt[q] = (q < sy && q * best_tx >= 4) ? young : 100;
     sk->hcap = hcap;
     sk->prio_young = h->skew_prio;
     sk->error = h->skew_err_dev;
@@ -932,6 +942,11 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
 bool try_persist_halo(golhip_t h, int d, int k, bool count, int *rc) {
     *rc = GOLHIP_OK;
     if (!persist_on(h) || h->W % 32 != 0 || k < 2 || d < 4) return false;
+    // never in a multi-rank ring: a resident launch that times out (a co-tenant
+    // kernel held CUs) cannot be re-run on one rank alone without
+    // desynchronising the ring, so ring strips stay on per-launch kernels
+    // (K1w, as fast: profiles/r3g); the one-rank ring (force_halo) keeps it
+    if (h->comm && h->nranks > 1) return false;
     const int wpl = wpl_for(h);
     if (d != persist_depth_for(h, wpl)) return false;
     const int e = (k - 1) * d;
@@ -1467,12 +1482,18 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         return GOLHIP_OK;
     }
     if (!strcmp(key, "skew")) {
-        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "skew %lld", (long long)value);
+        if (value < 0 || value > 2) return fail(GOLHIP_EINVAL, "skew %lld", (long long)value);
         h->skew = (int)value;
         return GOLHIP_OK;
     }
+    if (!strcmp(key, "timing")) {  // GOLHIP_FLAG_TIMING after creation (HIP events cost ~5 us a launch)
+        if (value) h->flags |= GOLHIP_FLAG_TIMING;
+        else h->flags &= ~GOLHIP_FLAG_TIMING;
+        return GOLHIP_OK;
+    }
     if (!strcmp(key, "skew_young")) {
-        if (value < 10 || value > 400) return fail(GOLHIP_EINVAL, "skew_young %lld not in 10..400", (long long)value);
+        if (value != 0 && (value < 10 || value > 400))
+            return fail(GOLHIP_EINVAL, "skew_young %lld not in 10..400", (long long)value);
         h->skew_young = (int)value;
         return GOLHIP_OK;
     }

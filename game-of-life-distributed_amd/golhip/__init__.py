@@ -277,6 +277,10 @@ class Board:
     def step(self, nturns: int, want_flips: bool = False) -> None:
         _check(load().golhip_step(self._h, nturns, 1 if want_flips else 0))
 
+    def stream(self) -> int:
+        """The handle's hipStream_t (golhip_stream), e.g. for torch.cuda.ExternalStream."""
+        return int(load().golhip_stream(self._h) or 0)
+
     def sync(self) -> None:
         _check(load().golhip_sync(self._h))
 

@@ -33,7 +33,7 @@ def run_skew(board, turns, depth, wpl, **opts):
     H, W = board.shape
     with golhip.Board(W, H) as b:
         b.set_option("persistent", 0)
-        b.set_option("skew", 1)
+        b.set_option("skew", 2)  # whenever a plan exists (the default also wants the CUs filled)
         b.set_option("wpl", wpl)
         for k, v in opts.items():
             b.set_option(k, v)
@@ -104,6 +104,7 @@ def test_skew_rccl_ring_one_rank(coracle, depth, wpl, W, H):
         b.comm_init(golhip.unique_id(), 1, 0)
         b.set_option("force_halo", 1)
         b.set_option("persistent", 0)
+        b.set_option("skew", 2)
         b.set_option("wpl", wpl)
         b.set_tb_depth(depth)
         b.load_bytes(board)
@@ -127,6 +128,7 @@ def test_skew_group_strips(coracle, nstrips, depth, wpl):
     try:
         for i, s in enumerate(strips):
             s.set_option("wpl", wpl)
+            s.set_option("skew", 2)
             s.set_tb_depth(depth)
             s.load_bytes(board[bounds[i]:bounds[i + 1]])
         golhip.group_step(strips, turns)
@@ -152,6 +154,7 @@ def test_skew_every_launch_counts(coracle):
     board = coracle.fill_random(8192, 1200, 0x5EED0037)
     with golhip.Board(8192, 1200) as b:
         b.set_option("persistent", 0)
+        b.set_option("skew", 2)
         b.set_tb_depth(20)
         b.load_bytes(board)
         cur = board
