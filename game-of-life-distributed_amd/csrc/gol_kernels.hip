@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <climits>
 #include <type_traits>
+#include <utility>
 
 namespace golk {
 #ifndef GOL_LOOP_PAD
@@ -1277,16 +1278,39 @@ __global__ __launch_bounds__(256) void gol_split_tri_kernel(SplitArgs p) {
 #ifndef GOL_SKEW_STORE_CPOL
 #define GOL_SKEW_STORE_CPOL 16  // K1w output stores sc1 (16384^2 +3.6 %, 8192-row strips +1.9 %, profiles/r3g; 0 plain, 2 nt)
 #endif
+// Pipeline phases of a band: fill phase i runs stages [0, STEP (i + 1))
+// (then [0, D)), drain phase j stages [P(j), D) with P(j) = STEP (j + 1).
+// Bands other than a stack's bottom one are multiples of 3 rows, so drain
+// groups start at d = 0 (mod 3) and, STEP being a multiple of 3, never
+// straddle a drain phase: phase j imports exactly the 2 (P(j+1) - P(j))
+// rows of generation P(j) its pushes d in [2 P(j), 2 P(j+1)) take in.
+// Coarser phases compute more stage-rows nobody needs (both at the fill and
+// at the drain, about D^2 / 4 each for phases of D / 4 stages); finer ones
+// more code (each phase is a loop of its own).
 template <int D>
 struct SkewPlan {
-    static constexpr int P1 = D / 4, P2 = D / 2, P3 = 3 * D / 4;
-    // import rows per drain phase: a group starting in phase 1 or 2 may end
-    // two rows into the next one; phase 3 clamps (rows past the drain)
-    static constexpr int N1 = 2 * (P2 - P1) + 2, N2 = 2 * (P3 - P2) + 2, N3 = 2 * (D - P3);
-    static constexpr int B1 = 0, B2 = N1, B3 = N1 + N2;
-    static constexpr int NEXP = N1 + N2 + N3;  // row NEXP of a wave's LDS slot = dummy (fill rows not exported)
-    static_assert(P1 >= 1, "skew depth >= 4");
+    static constexpr int STEP = D > 20 ? 6 : 3;
+    static constexpr int NPH = (D - 1) / STEP;  // drain phases (also the fill phases before the full one)
+    static constexpr int P(int j) { return (j + 1) * STEP; }
+    static constexpr int NROWS(int j) { return 2 * ((j + 1 < NPH ? P(j + 1) : D) - P(j)); }
+    static constexpr int BASE(int j) {
+        int b = 0;
+        for (int i = 0; i < j; ++i) b += NROWS(i);
+        return b;
+    }
+    static constexpr int NEXP = BASE(NPH);  // row NEXP of a wave's LDS slot = dummy (fill rows not exported)
+    static_assert(NPH >= 1 && STEP % 3 == 0, "skew depth >= 4");
 };
+
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>()), ...);
+}
+// f(integral_constant<int, i>) for i = 0 .. N-1, unrolled at compile time
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>());
+}
 
 // push_group for the last stages only: the group's rows enter stage LO.
 template <int D, int LO, int WPL>
@@ -1359,15 +1383,10 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
     // fill exports: the input of stage P (generation P of row ab + P + m) at
     // fill push 2 P + m, for the band above's drain phase P
     auto hook = [&](int s, int k, const Lanes<WPL> &x) {
-        int row;
-        if (s == SP::P1)
-            row = (unsigned)(k - 2 * SP::P1) < (unsigned)SP::N1 ? SP::B1 + k - 2 * SP::P1 : SP::NEXP;
-        else if (s == SP::P2)
-            row = (unsigned)(k - 2 * SP::P2) < (unsigned)SP::N2 ? SP::B2 + k - 2 * SP::P2 : SP::NEXP;
-        else if (s == SP::P3)
-            row = (unsigned)(k - 2 * SP::P3) < (unsigned)SP::N3 ? SP::B3 + k - 2 * SP::P3 : SP::NEXP;
-        else
-            return;
+        if (s % SP::STEP != 0 || s == 0 || s / SP::STEP > SP::NPH) return;  // s = P(j), folded per stage
+        const int j = s / SP::STEP - 1;
+        const int m = k - 2 * SP::P(j);
+        const int row = (unsigned)m < (unsigned)SP::NROWS(j) ? SP::BASE(j) + m : SP::NEXP;
         put_lanes<WPL>(exp_mine + row * ROW, x.w);
     };
 
@@ -1399,9 +1418,7 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
             x2 = vmov(n2);
         }
     };
-    fill(std::integral_constant<int, SP::P1>());
-    fill(std::integral_constant<int, SP::P2>());
-    fill(std::integral_constant<int, SP::P3>());
+    static_for<SP::NPH>([&](auto j) { fill(std::integral_constant<int, SP::P(decltype(j)::value)>()); });
     fill(std::integral_constant<int, D>());
     // exports done: this wave's LDS writes complete before the flag (LDS
     // operations of a wave complete in order; no wait on its global loads)
@@ -1413,7 +1430,7 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
     for (int i = 0; i < WPL; ++i) q0.w[i] = q1.w[i] = q2.w[i] = 0u;
     int qoi = -8;  // the first body stores nothing real
     // main: every stage on board rows (the bottom band of a stack to the end)
-    const int kmain = S + (self ? 2 * D : 2 * SP::P1);
+    const int kmain = S + (self ? 2 * D : 2 * SP::P(0));
     for (int i = 0; i < GOL_LOOP_PAD; ++i) asm volatile("s_nop 0");
     for (; k < kmain; k += 3) {
         const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
@@ -1449,9 +1466,12 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
         // (d = kg - S + row), P the phase of the group's first row
         auto imports = [&](int kg, Lanes<WPL> &y0, Lanes<WPL> &y1, Lanes<WPL> &y2) {
             const int d = kg - S;
-            const int base = d < 2 * SP::P2 ? SP::B1 - 2 * SP::P1 : d < 2 * SP::P3 ? SP::B2 - 2 * SP::P2
-                                                                                   : SP::B3 - 2 * SP::P3;
-            const int top = SP::NEXP - 1;  // phase 3 clamps (rows past the drain)
+            int base = SP::BASE(0) - 2 * SP::P(0);
+            static_for<SP::NPH>([&](auto j) {
+                constexpr int J = decltype(j)::value;
+                if (J > 0 && d >= 2 * SP::P(J)) base = SP::BASE(J) - 2 * SP::P(J);
+            });
+            const int top = SP::NEXP - 1;  // the last phase clamps (rows past the drain)
             y0 = get_lanes<WPL>(exp_next + min(base + d, top) * ROW);
             y1 = get_lanes<WPL>(exp_next + min(base + d + 1, top) * ROW);
             y2 = get_lanes<WPL>(exp_next + min(base + d + 2, top) * ROW);
@@ -1468,12 +1488,16 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
             for (; k < kend; k += 3) {
                 Lanes<WPL> n0, n1, n2;
                 imports(k + 3, n0, n1, n2);
+                __builtin_amdgcn_sched_barrier(0);
+                Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
+                // the previous group's stores after this group: their offset
+                // and count arithmetic right before the group put a hazard
+                // s_nop between parity_fix and the first DPP (slow parity)
+                push_group_hi<D, LO, WPL>(y0, y1, y2, h0, h1, cc);
+                __builtin_amdgcn_sched_barrier(0);
                 emit(q0, qoi);
                 emit(q1, qoi + 1);
                 emit(q2, qoi + 2);
-                __builtin_amdgcn_sched_barrier(0);
-                Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
-                push_group_hi<D, LO, WPL>(y0, y1, y2, h0, h1, cc);
                 q0 = y0;
                 q1 = y1;
                 q2 = y2;
@@ -1484,9 +1508,10 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
                 x2 = vmov(n2);
             }
         };
-        drain(std::integral_constant<int, SP::P1>(), S + 2 * SP::P2);
-        drain(std::integral_constant<int, SP::P2>(), S + 2 * SP::P3);
-        drain(std::integral_constant<int, SP::P3>(), S + 2 * D);
+        static_for<SP::NPH>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            drain(std::integral_constant<int, SP::P(J)>(), S + 2 * (J + 1 < SP::NPH ? SP::P(J + 1) : D));
+        });
     }
     emit(q0, qoi);
     emit(q1, qoi + 1);
@@ -1523,8 +1548,10 @@ __global__ __launch_bounds__(512) void gol_skew_kernel(SkewArgs p) {
         cum += q < pos ? p.wgt[q] : 0;
     }
     const bool bottom = pos == sy - 1;
-    const int ab = A0 + (int)(Ls * cum / tot);
-    const int eb = bottom ? E0 : A0 + (int)(Ls * (cum + p.wgt[pos]) / tot);
+    // band boundaries at multiples of 3 rows from the stack start (drain
+    // groups aligned with the drain phases, SkewPlan); the bottom band takes the rest
+    const int ab = A0 + (int)(Ls * cum / tot) / 3 * 3;
+    const int eb = bottom ? E0 : A0 + (int)(Ls * (cum + p.wgt[pos]) / tot) / 3 * 3;
     const long long t_start = p.trace ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
     const uint32_t cnt = stream_skew<D, WPL>(p.base, ab, eb, tile, bottom, s_exp[w], bottom ? nullptr : s_exp[w + p.tx],
                                              &s_flag[w], bottom ? nullptr : &s_flag[w + p.tx], p.error);

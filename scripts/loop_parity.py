@@ -85,6 +85,24 @@ def main_loop_parity(lines, kernel):
     raise KeyError(kernel)
 
 
+def inner_loops(lines, kernel, min_b8=300):
+    """(start, good fraction, 8-byte count) of every innermost loop of the
+    kernel with at least min_b8 8-byte instructions, in address order."""
+    for name, body in kernels(lines):
+        if kernel not in name:
+            continue
+        ins, lps = loops(body)
+        inner = [l for l in lps if not any(o is not l and l[0] <= o[0] and o[1] <= l[1] and (o[1] - o[0]) >= 400
+                                           for o in lps)]
+        out = []
+        for l in sorted(inner, key=lambda l: l[0]):
+            n = l[2]["b8@4"] + l[2]["b8@0"]
+            if n >= min_b8:
+                out.append((l[0], l[2]["b8@4"] / max(1, n), n))
+        return out
+    raise KeyError(kernel)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("lib")

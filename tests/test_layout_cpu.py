@@ -23,7 +23,7 @@ def disasm():
 
 
 @pytest.mark.parametrize("kernel", [
-    "gol_split_pair_kernelILi20ELi2E",       # configs[2] default: K1s A, 65536^2
+    "gol_split_pair_kernelILi20ELi2E",       # K1s A at 65536^2 (option skew 0)
     "gol_split_pair_kernelILi8ELi4E",        # configs[3]: 262144^2
     "gol_persist_kernelILi16ELi2ELi8E",      # configs[1]: 16384^2 resident
     "gol_tb_pair_kernelILi20ELi2ELb0E",      # the paired-band kernel (split off, strips)
@@ -33,3 +33,18 @@ def test_main_loop_on_fast_parity(disasm, kernel):
     good, n = loop_parity.main_loop_parity(disasm, kernel)
     assert n > 500, (kernel, n)
     assert good >= 0.9, f"{kernel}: {good:.2f} of {n} 8-byte instructions at 4 (mod 8)"
+
+
+@pytest.mark.parametrize("kernel,nph", [
+    ("gol_skew_kernelILi20ELi2E", 6),   # configs[1], configs[2] and their strips (default K1w)
+    ("gol_skew_kernelILi16ELi2E", 5),
+    ("gol_skew_kernelILi9ELi4E", 2),    # configs[3]
+])
+def test_skew_main_and_drain_loops_on_fast_parity(disasm, kernel, nph):
+    """K1w: the main loop and the nph drain-phase loops after it (the
+    kernel's last loops; SkewPlan::NPH of the depth)."""
+    import loop_parity
+    lps = loop_parity.inner_loops(disasm, kernel, min_b8=100)
+    assert len(lps) >= nph + 2, (kernel, len(lps))
+    for start, good, n in lps[-(nph + 1):]:
+        assert good >= 0.9, f"{kernel} loop at {start:#x}: {good:.2f} of {n} 8-byte instructions at 4 (mod 8)"
