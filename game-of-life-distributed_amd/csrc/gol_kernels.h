@@ -92,15 +92,8 @@ struct SkewArgs {
     int prio_young;   // 1: s_setprio 1 for waves 4..7 (the SIMD arbiter's age losers)
     unsigned *error;  // nullable, host-mapped: set if a band's imports never arrived (spin bound)
     unsigned long long *trace;  // nullable diagnostics: per wave (start, end) s_memrealtime at 8 + 2 (block * 64 + wave)
-    // cross-stack hand-off (nullable gexp: every stack's bottom band computes its own drain):
-    // per (stack, tile) skew_exp_rows(depth) x 64 x wpl words and one flag word
-    uint32_t *gexp;
-    unsigned *gflag;
-    unsigned epoch;   // this launch's flag value (never 0)
-    int wrap;         // torus: the last stack's next stack is stack 0
 };
 bool skew_supported(int depth, int wpl);
-int skew_exp_rows(int depth);
 int skew_blocks_per_cu(int depth, int wpl);
 hipError_t launch_skew(const SkewArgs &p, int depth, int wpl, hipStream_t s);
 

@@ -1327,37 +1327,15 @@ __device__ __forceinline__ void push_group_hi(Lanes<WPL> &x0, Lanes<WPL> &x1, La
     }
 }
 
-// One band of a stack (gol_skew_kernel): input rows [ab, eb) (StepArgs
-// frame) of tile `tile`.  A middle band exports its fill rows to its LDS slot
-// for the band above and imports the band below's from LDS.  The top band
-// exports to global memory instead (gexp, sc1 stores, then the flag gflag =
-// epoch), for the bottom band of the stack above.  The bottom band, when its
-// main loop reaches the drain, reads that flag of the next stack once: if
-// the next stack's top band is done, it copies those rows into LDS (the top
-// band's LDS slot, unused) and drains from them; otherwise (not resident yet,
-// or no next stack: self_only) it computes its drain from board rows, all
-// stages.  Nothing ever waits on another workgroup.
-struct SkewBand {
-    int ab, eb, tile;
-    bool top, bottom, self_only;
-    uint32_t *exp_mine;         // LDS slot of this wave
-    uint32_t *exp_next;         // LDS slot of the band below (middle), landing slot for a bottom band's import
-    int *flag_mine, *flag_next; // LDS flags
-    uint32_t *gexp_mine;        // top band: its global export rows (nullable: no cross-stack import)
-    unsigned *gflag_mine;
-    const uint32_t *gexp_next;  // bottom band: the next stack's top band's rows and flag
-    const unsigned *gflag_next;
-    unsigned epoch;
-    unsigned *error;
-};
-
+// One band [ab, eb) of input rows (StepArgs frame) of tile `tile`.  self: no
+// band below in the workgroup (compute the drain from board rows).  Exports
+// go to exp_mine (LDS slot of this wave), imports come from exp_next.
 template <int D, int WPL>
-__device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, const SkewBand &b) {
+__device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int eb, int tile, bool self,
+                                                uint32_t *exp_mine, const uint32_t *exp_next, int *flag_mine,
+                                                int *flag_next, unsigned *error) {
     using SP = SkewPlan<D>;
     constexpr int ROW = 64 * WPL;  // words of one LDS row
-    const int ab = b.ab, eb = b.eb, tile = b.tile;
-    uint32_t *const exp_mine = b.exp_mine;
-    const uint32_t *exp_next = b.exp_next;
     const int lane = threadIdx.x & 63;
     const int Ww = a.Ww;
     const int S = eb - ab;
@@ -1404,25 +1382,12 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, const SkewBan
     };
     // fill exports: the input of stage P (generation P of row ab + P + m) at
     // fill push 2 P + m, for the band above's drain phase P
-    const __amdgpu_buffer_rsrc_t gexp_rs = __builtin_amdgcn_make_buffer_rsrc(
-        b.gexp_mine, (short)0, (b.top && b.gexp_mine) ? SP::NEXP * ROW * 4 : 0, 0x00020000);
     auto hook = [&](int s, int k, const Lanes<WPL> &x) {
         if (s % SP::STEP != 0 || s == 0 || s / SP::STEP > SP::NPH) return;  // s = P(j), folded per stage
         const int j = s / SP::STEP - 1;
         const int m = k - 2 * SP::P(j);
         const int row = (unsigned)m < (unsigned)SP::NROWS(j) ? SP::BASE(j) + m : SP::NEXP;
-        put_lanes<WPL>(exp_mine + (b.top && b.gexp_mine ? SP::NEXP : row) * ROW, x.w);
-        // the top band's rows go to global memory (write-through sc1 stores;
-        // every other band's land out of range and are dropped)
-        const int goff = row < SP::NEXP ? (row * ROW + lane * WPL) * 4 : INT_MAX;
-        if constexpr (WPL == 1)
-            __builtin_amdgcn_raw_buffer_store_b32(x.w[0], gexp_rs, goff, 0, 16);
-        else if constexpr (WPL == 2)
-            __builtin_amdgcn_raw_buffer_store_b64((__attribute__((ext_vector_type(2))) unsigned){x.w[0], x.w[1]},
-                                                  gexp_rs, goff, 0, 16);
-        else
-            __builtin_amdgcn_raw_buffer_store_b128(
-                (__attribute__((ext_vector_type(4))) unsigned){x.w[0], x.w[1], x.w[2], x.w[3]}, gexp_rs, goff, 0, 16);
+        put_lanes<WPL>(exp_mine + row * ROW, x.w);
     };
 
     uint32_t h0[3][D][WPL], h1[3][D][WPL], cc[3][D][WPL];
@@ -1458,81 +1423,39 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, const SkewBan
     // exports done: this wave's LDS writes complete before the flag (LDS
     // operations of a wave complete in order; no wait on its global loads)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store(b.flag_mine, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (b.top && b.gflag_mine) {  // hand-off: sc1 stores drained, then the sc1 flag (MI355X_MICROARCH.md)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_store(b.gflag_mine, b.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (lane == 0) __hip_atomic_store(flag_mine, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 
     Lanes<WPL> q0, q1, q2;
 #pragma unroll
     for (int i = 0; i < WPL; ++i) q0.w[i] = q1.w[i] = q2.w[i] = 0u;
     int qoi = -8;  // the first body stores nothing real
-    // main: every stage on board rows (a bottom band that computes its own
-    // drain: to the end)
-    const int kmain = S + (b.self_only ? 2 * D : 2 * SP::P(0));
-    bool self = b.self_only;
-    // the previous group's stores after this group (still after the prefetch
-    // loads: the vmcnt wait for those leaves the stores pending); before it,
-    // their offset and count arithmetic put a hazard s_nop between parity_fix
-    // and the first DPP (slow code parity)
-    auto main_loop = [&](int kend) {
-        for (; k < kend; k += 3) {
-            const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
-            __builtin_amdgcn_sched_barrier(0);
-            Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
-            push_group<D, D, WPL>(y0, y1, y2, h0, h1, cc);
-            __builtin_amdgcn_sched_barrier(0);
-            emit(q0, qoi);
-            emit(q1, qoi + 1);
-            emit(q2, qoi + 2);
-            q0 = y0;
-            q1 = y1;
-            q2 = y2;
-            qoi = k - 2 * D;
-            __builtin_amdgcn_sched_barrier(0);
-            x0 = vmov(n0);
-            x1 = vmov(n1);
-            x2 = vmov(n2);
-        }
-    };
+    // main: every stage on board rows (the bottom band of a stack to the end)
+    const int kmain = S + (self ? 2 * D : 2 * SP::P(0));
     for (int i = 0; i < GOL_LOOP_PAD; ++i) asm volatile("s_nop 0");
-    main_loop(kmain);
-    if (b.bottom && !self) {
-        // bottom band at its drain: the next stack's top rows, if they are ready
-        const unsigned f = __hip_atomic_load(b.gflag_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__builtin_amdgcn_readfirstlane(f) == b.epoch) {
-            // global -> LDS (the top band's unused slot), 1 KiB per instruction
-            // (rolled loops: one address register, the ring state is all live here)
-            constexpr int BYTES = SP::NEXP * ROW * 4;
-            const char *g = reinterpret_cast<const char *>(b.gexp_next);
-            char *l = reinterpret_cast<char *>(b.exp_next);
-#pragma unroll 1
-            for (int i = 0; i < BYTES / 1024; ++i)
-                __builtin_amdgcn_global_load_lds(g + i * 1024 + lane * 16,
-                                                 (__attribute__((address_space(3))) void *)(l + i * 1024), 16, 0, 16);
-#pragma unroll 1
-            for (int i = (BYTES / 1024) * 4; i < BYTES / 256; ++i)
-                __builtin_amdgcn_global_load_lds(g + i * 256 + lane * 4,
-                                                 (__attribute__((address_space(3))) void *)(l + i * 256), 4, 0, 16);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else {
-            // not ready: compute the drain from board rows (a second copy of
-            // the loop: one loop with a re-entry edge costs the first copy a
-            // register copy inside the group at 256 VGPRs)
-            self = true;
-            for (int i = 0; i < GOL_LOOP_PAD; ++i) asm volatile("s_nop 0");
-            main_loop(S + 2 * D);
-        }
+    for (; k < kmain; k += 3) {
+        const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
+        emit(q0, qoi);
+        emit(q1, qoi + 1);
+        emit(q2, qoi + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
+        push_group<D, D, WPL>(y0, y1, y2, h0, h1, cc);
+        q0 = y0;
+        q1 = y1;
+        q2 = y2;
+        qoi = k - 2 * D;
+        __builtin_amdgcn_sched_barrier(0);
+        x0 = vmov(n0);
+        x1 = vmov(n1);
+        x2 = vmov(n2);
     }
     if (!self) {
         // the band below has exported its top rows (almost always long ago)
-        if (!b.bottom && __hip_atomic_load(b.flag_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+        if (__hip_atomic_load(flag_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
             const long long t_start = (long long)__builtin_amdgcn_s_memrealtime();
-            while (__hip_atomic_load(b.flag_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+            while (__hip_atomic_load(flag_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
                 if ((long long)__builtin_amdgcn_s_memrealtime() - t_start > 200000000ll) {  // 2 s: never
-                    if (b.error && lane == 0)
-                        __hip_atomic_store(b.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (error && lane == 0) __hip_atomic_store(error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
@@ -1617,43 +1540,21 @@ __global__ __launch_bounds__(512) void gol_skew_kernel(SkewArgs p) {
     if (tile >= p.tiles_x) return;  // wave-uniform, after the only barrier (its stack's waves all leave)
     if (p.prio_young && w >= 4) __builtin_amdgcn_s_setprio(1);
     const int L = p.base.rows_out;
-    // stacks start at multiples of 3 rows from -D (so do the bands inside: the
-    // drain phases need 3-row-aligned bands, SkewPlan)
-    const int A0 = (int)((int64_t)stack * L / p.nst) / 3 * 3 - D;
-    const int E0 = stack + 1 == p.nst ? L - D : (int)((int64_t)(stack + 1) * L / p.nst) / 3 * 3 - D;
-    const bool top = pos == 0, bottom = pos == sy - 1;
-    // a bottom band takes the next stack's top rows, except at the end of a
-    // strip, or when the last stack of a torus is not a multiple of 3 rows
-    const bool self_only = bottom && (!p.gexp || (stack + 1 == p.nst && (!p.wrap || (E0 - A0) % 3 != 0)));
-    const int64_t Ls = (int64_t)(E0 - A0) + (self_only ? p.hcap : 0);  // a self-computing bottom band is shorter
+    const int A0 = (int)((int64_t)stack * L / p.nst) - D, E0 = (int)((int64_t)(stack + 1) * L / p.nst) - D;
+    const int64_t Ls = (int64_t)(E0 - A0) + p.hcap;
     int cum = 0, tot = 0;
     for (int q = 0; q < sy; ++q) {
         tot += p.wgt[q];
         cum += q < pos ? p.wgt[q] : 0;
     }
-    // band boundaries at multiples of 3 rows from the stack start; the bottom band takes the rest
-    SkewBand bd{};
-    bd.ab = A0 + (int)(Ls * cum / tot) / 3 * 3;
-    bd.eb = bottom ? E0 : A0 + (int)(Ls * (cum + p.wgt[pos]) / tot) / 3 * 3;
-    bd.tile = tile;
-    bd.top = top;
-    bd.bottom = bottom;
-    bd.self_only = self_only;
-    bd.exp_mine = s_exp[w];
-    bd.exp_next = bottom ? s_exp[w % p.tx] : s_exp[w + p.tx];  // bottom: the top band's slot (its rows go to global)
-    bd.flag_mine = &s_flag[w];
-    bd.flag_next = bottom ? nullptr : &s_flag[w + p.tx];
-    if (p.gexp) {
-        const int next = stack + 1 == p.nst ? 0 : stack + 1;
-        bd.gexp_mine = p.gexp + ((size_t)stack * p.tiles_x + tile) * SP::NEXP * ROW;
-        bd.gflag_mine = p.gflag + stack * p.tiles_x + tile;
-        bd.gexp_next = p.gexp + ((size_t)next * p.tiles_x + tile) * SP::NEXP * ROW;
-        bd.gflag_next = p.gflag + next * p.tiles_x + tile;
-    }
-    bd.epoch = p.epoch;
-    bd.error = p.error;
+    const bool bottom = pos == sy - 1;
+    // band boundaries at multiples of 3 rows from the stack start (drain
+    // groups aligned with the drain phases, SkewPlan); the bottom band takes the rest
+    const int ab = A0 + (int)(Ls * cum / tot) / 3 * 3;
+    const int eb = bottom ? E0 : A0 + (int)(Ls * (cum + p.wgt[pos]) / tot) / 3 * 3;
     const long long t_start = p.trace ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
-    const uint32_t cnt = stream_skew<D, WPL>(p.base, bd);
+    const uint32_t cnt = stream_skew<D, WPL>(p.base, ab, eb, tile, bottom, s_exp[w], bottom ? nullptr : s_exp[w + p.tx],
+                                             &s_flag[w], bottom ? nullptr : &s_flag[w + p.tx], p.error);
     if (p.trace && lane == 0 && blockIdx.x < 1024) {
         p.trace[8 + 2 * (blockIdx.x * 64 + w)] = (unsigned long long)t_start;
         p.trace[8 + 2 * (blockIdx.x * 64 + w) + 1] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
@@ -1930,18 +1831,6 @@ static hipError_t dispatch_skew(int depth, int wpl, F &&f) {
     GOL_WCASE(16, 1) GOL_WCASE(32, 1)
 #undef GOL_WCASE
     return hipErrorInvalidValue;
-}
-
-int skew_exp_rows(int depth) {
-    switch (depth) {
-        case 8: return SkewPlan<8>::NEXP;
-        case 9: return SkewPlan<9>::NEXP;
-        case 12: return SkewPlan<12>::NEXP;
-        case 16: return SkewPlan<16>::NEXP;
-        case 20: return SkewPlan<20>::NEXP;
-        case 32: return SkewPlan<32>::NEXP;
-    }
-    return 0;
 }
 
 bool skew_supported(int depth, int wpl) {

@@ -124,11 +124,6 @@ struct golhip {
     int skew_prio = 0;              // option "skew_prio": s_setprio 1 for waves 4..7
     int skew_tx = 0;                // option "skew_tx": tiles per K1w workgroup (0: plan, 1 or 2)
     int skew_bpc[kNumDepths][3] = {};  // K1w workgroups per CU by (depth, wpl) (0: not queried)
-    int skew_xstack = 1;            // option "skew_xstack": stacks hand their top rows to the stack above
-    uint32_t *skew_gexp = nullptr;  // cross-stack export rows, kSkewSlots slots (grow-only)
-    unsigned *skew_gflag = nullptr;
-    int64_t skew_gexp_words = 0, skew_gflag_words = 0;  // per slot
-    unsigned skew_epoch = 0;
     unsigned *skew_err = nullptr;      // host-mapped spin-bound flag of the K1w kernels
     unsigned *skew_err_dev = nullptr;
     int64_t skew_launches = 0;
@@ -670,42 +665,6 @@ bool skew_plan(golhip_t h, int depth, int wpl, const golk::StepArgs &a, golk::Sk
     sk->prio_young = h->skew_prio;
     sk->error = h->skew_err_dev;
     sk->trace = h->d_trace;
-    sk->wrap = a.in.wrap > 0 ? 1 : 0;
-    sk->gexp = nullptr;
-    sk->gflag = nullptr;
-    if (h->skew_xstack) {
-        // Slots rotate with the launch: a slot's lines are rewritten every
-        // kSkewSlots launches, long after any XCD's L2 could still hold them
-        // (the hand-off is sc1 stores + sc1 flag / loads, MI355X_MICROARCH.md)
-        constexpr int kSkewSlots = 4;
-        const int64_t units = (int64_t)best_nst * tiles;
-        const int64_t words = units * golk::skew_exp_rows(depth) * 64 * wpl;
-        if (words > h->skew_gexp_words || units > h->skew_gflag_words) {
-            const int64_t nw = std::max(words, h->skew_gexp_words), nf = std::max(units, h->skew_gflag_words);
-            uint32_t *ge = nullptr;
-            unsigned *gf = nullptr;
-            if (hipMalloc(&ge, (size_t)nw * kSkewSlots * 4) != hipSuccess) return false;
-            if (hipMalloc(&gf, (size_t)nf * kSkewSlots * 4) != hipSuccess ||
-                hipMemsetAsync(gf, 0, (size_t)nf * kSkewSlots * 4, h->stream) != hipSuccess) {
-                (void)hipFree(ge);
-                (void)hipFree(gf);
-                return false;
-            }
-            // the old buffers may still be read by an enqueued launch
-            if (hipStreamSynchronize(h->stream) != hipSuccess) return false;
-            (void)hipFree(h->skew_gexp);
-            (void)hipFree(h->skew_gflag);
-            h->skew_gexp = ge;
-            h->skew_gflag = gf;
-            h->skew_gexp_words = nw;
-            h->skew_gflag_words = nf;
-        }
-        if (++h->skew_epoch == 0) h->skew_epoch = 1;  // 0 is the zeroed flags' value
-        const int slot = (int)(h->skew_epoch % kSkewSlots);
-        sk->gexp = h->skew_gexp + (int64_t)slot * h->skew_gexp_words;
-        sk->gflag = h->skew_gflag + (int64_t)slot * h->skew_gflag_words;
-        sk->epoch = h->skew_epoch;
-    }
     return true;
 }
 
@@ -1404,8 +1363,6 @@ int golhip_destroy(golhip_t h) {
     HIP_RC(hipFree(h->split_meet));
     if (h->h_err) HIP_RC(hipHostFree(h->h_err));
     if (h->skew_err) HIP_RC(hipHostFree(h->skew_err));
-    HIP_RC(hipFree(h->skew_gexp));
-    HIP_RC(hipFree(h->skew_gflag));
     if (h->own_stream && h->stream) HIP_RC(hipStreamDestroy(h->stream));
     delete h;
     return rc;
@@ -1548,11 +1505,6 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     if (!strcmp(key, "skew_prio")) {
         if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "skew_prio %lld", (long long)value);
         h->skew_prio = (int)value;
-        return GOLHIP_OK;
-    }
-    if (!strcmp(key, "skew_xstack")) {
-        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "skew_xstack %lld", (long long)value);
-        h->skew_xstack = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "skew_tx")) {

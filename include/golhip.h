@@ -127,10 +127,19 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * depend on them.  "fill_skip" (default 1): skip pipeline-fill stage-rows;
  * "wpl" (default 0 = auto): words per lane, 1, 2 or 4 (2 and 4 run on the
  * interleaved pair / quad layouts, converted at the I/O boundary; 4 fuses at
- * most 8 turns a launch and needs width % 128 == 0); "persistent"
- * (default -1 = auto: on for buffers of at most 64 MiB; 1 on, 0 off):
- * resident multi-super-step kernel for long runs on a whole torus and,
- * in a ring, for the launches between two deep-halo exchanges;
+ * most 8 turns a launch and needs width % 128 == 0); "skew" (default 1):
+ * skewed band stacks (gol_skew_kernel) for per-launch steps of a torus or a
+ * ring strip when they fill the CUs (2: always, 0: off); "skew_young"
+ * (0 = by kernel: 68 %, quads 78 %): band height of waves 4..7 relative to
+ * waves 0..3; "skew_hcap" (-1 = 3 D / 4): rows a stack's bottom band gives
+ * up (it computes its own drain); "skew_tx" (0 = plan, 1, 2): tiles across
+ * a stack; "skew_prio" (0): s_setprio for the
+ * younger waves; "split" (1): split tiling (gol_split_pair_kernel) for torus
+ * steps when skew is off; "timing" (the GOLHIP_FLAG_TIMING flag after
+ * creation: per-launch HIP events, ~5 us each); "persistent"
+ * (default -1 = auto: off while skew is on, else on for buffers of at most
+ * 64 MiB; 1 on, 0 off): resident multi-super-step kernel for long runs on a
+ * whole torus (never in a multi-rank ring);
  * "persist_depth" (default 0 = tb_depth): turns per super-step;
  * "persist_half" (default 1): a remainder of half a super-step runs as the
  * resident kernel's last, half-depth super-step;
