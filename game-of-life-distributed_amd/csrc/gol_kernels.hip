@@ -1276,7 +1276,7 @@ __global__ __launch_bounds__(256) void gol_split_tri_kernel(SplitArgs p) {
 // halo rows feed the top band's first D rows and the bottom band's drain.
 // ---------------------------------------------------------------------------
 #ifndef GOL_SKEW_STORE_CPOL
-#define GOL_SKEW_STORE_CPOL 16  // K1w output stores sc1 (16384^2 +3.6 %, 8192-row strips +1.9 %, profiles/r3g; 0 plain, 2 nt)
+#define GOL_SKEW_STORE_CPOL 16  // K1w output stores sc1 (16384^2 +3.6 %, 8192-row strips +1.9 % in a round-3 A/B whose scratch data was not kept; 0 plain, 2 nt)
 #endif
 // Pipeline phases of a band: fill phase i runs stages [0, STEP (i + 1))
 // (then [0, D)), drain phase j stages [P(j), D) with P(j) = STEP (j + 1).

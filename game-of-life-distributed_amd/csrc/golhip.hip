@@ -188,12 +188,15 @@ struct golhip {
     bool force_halo = false;    // option "force_halo": one-rank RCCL ring on a whole board (tests)
     int nranks = 1, rank = 0;
     int ring_rows = 0;          // smallest strip of the ring (every rank plans from it)
+    int halo_skip = 0;          // option "halo_skip" (measurement only: no exchange, wrong halos)
+    int64_t halo_exchanges = 0;
+    double halo_ms = 0;         // exchange time on the engine stream (GOLHIP_FLAG_TIMING)
 
     // measurement
     std::vector<hipEvent_t> ev_pool;
     struct Timed {
         hipEvent_t e0, e1;
-        int kind;  // 0 per-launch step, 1 resident step, 2 flip turn (K5)
+        int kind;  // 0 per-launch step, 1 resident step, 2 flip turn (K5), 3 halo exchange
     };
     std::vector<Timed> ev_pending;
     double step_ms = 0, persist_ms = 0;
@@ -494,7 +497,7 @@ int drain_events(golhip_t h) {
         HIP_OR_FAIL(hipEventSynchronize(p.e1));
         float ms = 0;
         HIP_OR_FAIL(hipEventElapsedTime(&ms, p.e0, p.e1));
-        (p.kind == 1 ? h->persist_ms : p.kind == 2 ? h->flip_ms : h->step_ms) += ms;
+        (p.kind == 1 ? h->persist_ms : p.kind == 2 ? h->flip_ms : p.kind == 3 ? h->halo_ms : h->step_ms) += ms;
         h->ev_pool.push_back(p.e0);
         h->ev_pool.push_back(p.e1);
     }
@@ -519,17 +522,30 @@ void plan(int strip_rows, int nranks, int rank, int depth, int Ww, golhip_halo_p
 // rank (one-rank ring, option "force_halo"): on every A->B channel the first
 // message is A's top rows (B's bottom halo), the second A's bottom rows.
 int exchange_rccl(golhip_t h, int depth, hipStream_t st) {
+    if (h->halo_skip) return GOLHIP_OK;  // measurement only (option "halo_skip")
     golhip_halo_plan_t p;
     plan(h->rows, h->nranks, h->rank, depth, h->Ww, &p);
     uint32_t *b = h->buf[h->cur];
     const size_t n = (size_t)depth * h->Ww;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (h->flags & GOLHIP_FLAG_TIMING) {
+        e0 = take_event(h);
+        e1 = take_event(h);
+        if (!e0 || !e1) return fail(GOLHIP_EHIP, "hipEventCreate failed");
+        HIP_OR_FAIL(hipEventRecord(e0, st));
+    }
     NCCL_OR_FAIL(ncclGroupStart());
     NCCL_OR_FAIL(ncclSend(b + (int64_t)p.send_up_row * h->Ww, n, ncclUint32, p.prev_rank, h->comm, st));
     NCCL_OR_FAIL(ncclRecv(b + (int64_t)p.recv_bottom_row * h->Ww, n, ncclUint32, p.next_rank, h->comm, st));
     NCCL_OR_FAIL(ncclSend(b + (int64_t)p.send_down_row * h->Ww, n, ncclUint32, p.next_rank, h->comm, st));
     NCCL_OR_FAIL(ncclRecv(b + (int64_t)p.recv_top_row * h->Ww, n, ncclUint32, p.prev_rank, h->comm, st));
     NCCL_OR_FAIL(ncclGroupEnd());
+    if (e1) {
+        HIP_OR_FAIL(hipEventRecord(e1, st));
+        h->ev_pending.push_back({e0, e1, 3});
+    }
     h->halo_bytes += 2 * (int64_t)n * 4;
+    h->halo_exchanges++;
     return GOLHIP_OK;
 }
 
@@ -658,7 +674,8 @@ bool skew_plan(golhip_t h, int depth, int wpl, const golk::StepArgs &a, golk::Sk
     const int sy = 8 / best_tx;
     // The SIMD arbiter serves the older wave of a SIMD (waves 0..3) first: the
     // younger waves' bands are shorter so both finish together.  Measured
-    // (profiles/r3b, r3d): two words per lane 66-70 %, quads at depth 9 76-82 %.
+    // (round-3 skew_young sweeps, scripts/sweep_opts.py): two words per lane
+    // 66-70 %, quads at depth 9 76-82 %.
     const int young = h->skew_young > 0 ? h->skew_young : wpl == 4 ? 78 : 68;
     for (int q = 0; q < 8; ++q) sk->wgt[q] = (q < sy && q * best_tx >= 4) ? young : 100;
     sk->hcap = hcap;
@@ -902,6 +919,26 @@ int persist_depth_for(golhip_t h, int wpl) {
     return 1;
 }
 
+// Keep the board recoverable before a step's first resident launch: a copy
+// of this handle's rows that golhip_step restores (and then re-runs the step
+// on the per-launch kernels) if a resident launch times out.  False (rc 0)
+// if there is no room for the copy: then no resident launch this step.
+bool take_guard(golhip_t h, int *rc) {
+    *rc = GOLHIP_OK;
+    const size_t bytes = (size_t)h->local_words() * 4;
+    if (!h->backup && hipMalloc(&h->backup, bytes) != hipSuccess) {
+        h->backup = nullptr;
+        return false;
+    }
+    hipError_t e = hipMemcpyAsync(h->backup, h->cur_rows(), bytes, hipMemcpyDeviceToDevice, h->stream);
+    if (e != hipSuccess) {
+        *rc = fail(GOLHIP_EHIP, "resident-launch guard copy: %s", hipGetErrorString(e));
+        return false;
+    }
+    h->guarded = true;
+    return true;
+}
+
 // Torus: J super-steps of `depth` turns in one resident launch; returns the
 // turns run (0 if the persistent path does not apply).
 int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
@@ -918,20 +955,11 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     if (half) ++J;
     const int64_t turns = J * depth - (half ? depth / 2 : 0);
     const bool count = count_last && turns == left;
-    // keep the board recoverable: golhip_step restores it and re-runs the step
-    // on the per-launch kernels if this launch times out
-    const size_t bytes = (size_t)h->local_words() * 4;
-    if (!h->backup && hipMalloc(&h->backup, bytes) != hipSuccess) {
-        h->backup = nullptr;
-        return 0;  // no room for the guard: per-launch kernels
-    }
-    hipError_t e = hipMemcpyAsync(h->backup, h->cur_rows(), bytes, hipMemcpyDeviceToDevice, h->stream);
-    if (e != hipSuccess) {
-        *rc = fail(GOLHIP_EHIP, "resident-launch guard copy: %s", hipGetErrorString(e));
+    if (!take_guard(h, rc)) return 0;
+    if (!persist_launch(h, step_args(h, nullptr, false), J, depth, wpl, count, rc, half)) {
+        h->guarded = false;  // nothing resident ran: no check needed
         return 0;
     }
-    if (!persist_launch(h, step_args(h, nullptr, false), J, depth, wpl, count, rc, half)) return 0;
-    h->guarded = true;
     return turns;
 }
 
@@ -939,14 +967,15 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
 // d turns as one resident launch of k super-steps over the rows
 // [-(k-1) d, rows + (k-1) d) (the outer rows go stale one super-step at a
 // time, as in the per-launch trapezoid, and are never read by a kept row).
+// Only in the one-rank ring (force_halo), under the guard step_locked took
+// at the start of the step: a timeout restores the board and re-runs the
+// step on per-launch kernels, exchanges included, which is safe with no
+// other rank.  Never in a multi-rank ring: a re-run on one rank alone would
+// desynchronise the ring, so ring strips stay on per-launch kernels (K1w).
 bool try_persist_halo(golhip_t h, int d, int k, bool count, int *rc) {
     *rc = GOLHIP_OK;
     if (!persist_on(h) || h->W % 32 != 0 || k < 2 || d < 4) return false;
-    // never in a multi-rank ring: a resident launch that times out (a co-tenant
-    // kernel held CUs) cannot be re-run on one rank alone without
-    // desynchronising the ring, so ring strips stay on per-launch kernels
-    // (K1w, as fast: profiles/r3g); the one-rank ring (force_halo) keeps it
-    if (h->comm && h->nranks > 1) return false;
+    if ((h->comm && h->nranks > 1) || !h->guarded) return false;
     const int wpl = wpl_for(h);
     if (d != persist_depth_for(h, wpl)) return false;
     const int e = (k - 1) * d;
@@ -1476,6 +1505,10 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         h->force_halo = value != 0;
         return GOLHIP_OK;
     }
+    if (!strcmp(key, "halo_skip")) {  // measurement only: the halo rows go stale (wrong results)
+        h->halo_skip = value != 0;
+        return GOLHIP_OK;
+    }
     if (!strcmp(key, "fill_skip")) {
         h->fill_skip = value != 0;
         for (int &c : h->auto_rpw) c = 0;
@@ -1638,6 +1671,10 @@ int step_locked(golhip_t h, int64_t nturns, int32_t want_flips) {
         int rc = GOLHIP_OK;
         left -= try_persist(h, left - tail, tail == 0, &rc);
         if (rc) return rc;
+    } else if (h->nranks == 1 && persist_on(h) && h->W % 32 == 0 && !h->guarded) {
+        int rc = GOLHIP_OK;  // one-rank ring that may run resident launches: guard the step
+        take_guard(h, &rc);
+        if (rc) return rc;
     }
     while (left > tail) {
         if (!halo) {
@@ -1686,9 +1723,13 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     const int64_t step_launches0 = h->step_launches, step_turns0 = h->step_turns;
     const int64_t split_launches0 = h->split_launches, skew_launches0 = h->skew_launches;
     const size_t ev0 = h->ev_pending.size();
+    const int64_t halo_exchanges0 = h->halo_exchanges, halo_bytes0 = h->halo_bytes;
     int rc = step_locked(h, nturns, want_flips);
-    if (rc || !h->guarded) return rc;
-    // A resident launch ran (torus): check it before returning.  Its
+    if (rc || !h->guarded) {
+        h->guarded = false;
+        return rc;
+    }
+    // A resident launch ran (torus, or a one-rank ring): check it before returning.  Its
     // workgroups wait on their neighbours, so a co-tenant kernel holding CUs
     // can starve one past the bounded spin; then every workgroup drains out
     // with the error word set and the board is restored from the guard copy
@@ -1696,7 +1737,7 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     h->guarded = false;
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
     h->persist_pending = false;
-    if (!*h->h_err) return GOLHIP_OK;
+    if (!h->h_err || !*h->h_err) return GOLHIP_OK;  // (a one-rank ring's guard may see no resident launch)
     *h->h_err = 0;
     h->persistent = 0;  // this device is shared: no more resident launches on this handle
     h->persist_fallbacks++;
@@ -1706,6 +1747,8 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     h->step_turns = step_turns0;
     h->split_launches = split_launches0;
     h->skew_launches = skew_launches0;
+    h->halo_exchanges = halo_exchanges0;
+    h->halo_bytes = halo_bytes0;
     if (h->ev_pending.size() >= ev0) {  // the abandoned attempt's launch timings (unless drained meanwhile)
         for (size_t i = ev0; i < h->ev_pending.size(); ++i) {
             h->ev_pool.push_back(h->ev_pending[i].e0);
@@ -2047,6 +2090,8 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     out->rows_per_wave = rows_per_wave_for(h, next_depth(h, h->tb_depth, halo));
     out->kernel_variant = h->last_variant;
     out->skew_launches = h->skew_launches;
+    out->halo_exchanges = h->halo_exchanges;
+    out->halo_ms = h->halo_ms;
     out->words_per_lane = h->W % 32 == 0 ? wpl_for(h) : 0;
     out->persist_depth = h->W % 32 == 0 ? persist_depth_for(h, wpl_for(h)) : 0;
     return GOLHIP_OK;
@@ -2086,6 +2131,8 @@ int golhip_perf_reset(golhip_t h) {
     h->persist_launches = h->persist_turns = 0;
     h->flip_launches = h->flip_entries = 0;
     h->flip_ms = 0;
+    h->halo_exchanges = 0;
+    h->halo_ms = 0;
     return GOLHIP_OK;
 }
 

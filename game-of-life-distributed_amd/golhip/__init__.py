@@ -56,6 +56,8 @@ class Perf(ctypes.Structure):
         ("reserved0", ctypes.c_int32),
         ("split_launches", ctypes.c_int64),
         ("skew_launches", ctypes.c_int64),
+        ("halo_exchanges", ctypes.c_int64),
+        ("halo_ms", ctypes.c_double),
     ]
 
     def as_dict(self) -> dict:

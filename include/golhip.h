@@ -85,6 +85,9 @@ typedef struct golhip_perf {
                                  (gol_split_pair_kernel + gol_split_tri_kernel) */
     int64_t skew_launches;    /* of step_launches, those that ran skewed band
                                  stacks (gol_skew_kernel, kernel_variant 3)     */
+    int64_t halo_exchanges;   /* halo exchanges posted (RCCL ring)               */
+    double halo_ms;           /* their summed time on the stream they ran on
+                                 (GOLHIP_FLAG_TIMING)                           */
 } golhip_perf_t;
 
 /* ---- library ---------------------------------------------------------- */
@@ -155,7 +158,9 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * restored and the step re-run on per-launch kernels, persist_fallbacks; a
  * ring strip: the step fails with GOLHIP_EHIP);
  * "force_halo" (0): after golhip_comm_init with one rank, run a whole board
- * through the multi-GPU path as a one-rank RCCL ring (tests, measurement). */
+ * through the multi-GPU path as a one-rank RCCL ring (tests, measurement);
+ * "halo_skip" (0): measurement only, post no halo exchange (the halo rows go
+ * stale: WRONG results; isolates the exchange's cost). */
 int golhip_set_option(golhip_t h, const char *key, int64_t value);
 
 /* ---- multi-GPU -------------------------------------------------------- */

@@ -35,6 +35,10 @@ for step in "$@"; do
     strips)
       timeout -k 10 400 python -u scripts/sweep_opts.py --no-timing --reps 2 --cases "65536x8192r,65536x16384r,65536x32768r,262144x32768r,16384x2048r" --sets "skew=1" > $out/strips.txt 2> $out/strips.err || { tail $out/strips.err; exit 1; }
       grep -A100 "^# best" $out/strips.txt ;;
+    stripdiag)
+      timeout -k 10 400 python -u scripts/sweep_opts.py --no-timing --reps 2 --cases "65536x8192,65536x8192r" --sets "skew=1;halo_skip=1;tb_depth=16;tb_depth=12;tb_depth=16,halo_skip=1" > $out/stripdiag.txt 2> $out/stripdiag.err || { tail $out/stripdiag.err; exit 1; }
+      timeout -k 10 200 python -u scripts/sweep_opts.py --reps 1 --cases "65536x8192r,65536x8192" --sets "skew=1" > $out/stripdiag_timed.txt 2>> $out/stripdiag.err || { tail $out/stripdiag.err; exit 1; }
+      grep -A100 "^# best" $out/stripdiag.txt; grep '^{' $out/stripdiag_timed.txt ;;
   esac
 done
 echo "gpu_r3 $tag done"

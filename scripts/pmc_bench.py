@@ -2,7 +2,7 @@
 
     python scripts/pmc_bench.py <dir with pmc_<workload>_<pass>/ outputs> <out.json>
 
-Per workload and step-kernel family (gol_tb_pair_kernel, gol_persist_kernel),
+Per workload and step-kernel family (gol_skew_kernel, gol_tb_pair_kernel, gol_persist_kernel, ...),
 averaged over every dispatch of that family in the bench run:
   HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes).  On
   gfx950 FETCH_SIZE counts half the bytes of a coalesced streaming read
@@ -22,7 +22,7 @@ import sys
 
 src, dst = sys.argv[1], sys.argv[2]
 out = json.load(open(dst)) if os.path.exists(dst) else {}
-FAMILIES = ("gol_persist_kernel", "gol_tb_pair_kernel", "gol_split_pair_kernel", "gol_split_tri_kernel")
+FAMILIES = ("gol_persist_kernel", "gol_tb_pair_kernel", "gol_split_pair_kernel", "gol_split_tri_kernel", "gol_skew_kernel")
 
 for d in sorted(glob.glob(os.path.join(src, "pmc_*_*"))):
     if not os.path.isdir(d):

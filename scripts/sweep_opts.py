@@ -57,7 +57,9 @@ for rep in range(a.reps):
                 print(json.dumps({"case": case, "opts": opts, "lib": os.path.basename(golhip.LIB_PATH), "rep": rep, "gcups": round(g, 1),
                                   "launch_ms": round(p["step_kernel_ms"] / max(1, p["step_launches"]), 5),
                                   "skew": p["skew_launches"], "split": p["split_launches"],
-                                  "launches": p["step_launches"], "persist": p["persist_launches"]}), flush=True)
+                                  "launches": p["step_launches"], "persist": p["persist_launches"],
+                                  "exchanges": p["halo_exchanges"],
+                                  "exchange_ms": round(p["halo_ms"] / max(1, p["halo_exchanges"]), 5)}), flush=True)
 print("# best GCUPS per (case, options)")
 for (case, opts), g in sorted(best.items()):
     print(f"{case:16s} {opts:50s} {g:10.1f}")

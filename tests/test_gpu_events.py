@@ -243,3 +243,35 @@ def test_persistent_timeout_restores_and_reruns(coracle, N, depth, wpl):
         assert b.alive_count() == (int((want == 255).sum()), turns)
         b.step(10)
         assert np.array_equal(b.snapshot_bytes(), coracle.run(want, 10))
+
+
+@pytest.mark.parametrize("timeout_us", [1000000, 1])
+def test_persistent_timeout_one_rank_ring(coracle, timeout_us):
+    """A strip run as a one-rank RCCL ring (force_halo) with the resident
+    kernel between exchanges: the step is guarded like a torus step, so a
+    resident launch that gives up waiting (1 us bound) restores the board and
+    re-runs the step on per-launch kernels, exchanges included (safe with no
+    other rank; multi-rank rings never run the resident kernel)."""
+    N, depth = 2048, 16
+    board = coracle.fill_random(N, N // 2, 0x5EED0024)
+    turns = 5 * depth + 7
+    want = coracle.run(board, turns)
+    with golhip.Board(N, N // 2) as b:
+        b.comm_init(golhip.unique_id(), 1, 0)
+        b.set_option("force_halo", 1)
+        b.set_option("persistent", 1)
+        b.set_option("wpl", 2)
+        b.set_tb_depth(depth)
+        b.set_option("persist_timeout_us", timeout_us)
+        b.load_bytes(board)
+        b.step(turns)
+        p = b.perf()
+        if timeout_us == 1:
+            assert p["persist_fallbacks"] == 1 and p["persist_launches"] == 0
+        else:
+            assert p["persist_fallbacks"] == 0 and p["persist_launches"] >= 1
+        assert p["halo_exchanges"] >= 1
+        assert np.array_equal(b.snapshot_bytes(), want)
+        assert b.alive_count() == (int((want == 255).sum()), turns)
+        b.step(10)
+        assert np.array_equal(b.snapshot_bytes(), coracle.run(want, 10))
