@@ -91,7 +91,8 @@ struct SkewArgs {
     int hcap;         // rows the stack's bottom band gives up (its drain is computed in full)
     int prio_young;   // 1: s_setprio 1 for waves 4..7 (the SIMD arbiter's age losers)
     unsigned *error;  // nullable, host-mapped: set if a band's imports never arrived (spin bound)
-    unsigned long long *trace;  // nullable diagnostics: per wave (start, end) s_memrealtime at 8 + 2 (block * 64 + wave)
+    unsigned long long *trace;  // nullable diagnostics: per wave (start, end) s_memrealtime at 8 + 2 (block * 64 + wave),
+                                // (fill done, main loop done) at 8 + 2 (block * 64 + 8 + wave)
 };
 bool skew_supported(int depth, int wpl);
 int skew_blocks_per_cu(int depth, int wpl);

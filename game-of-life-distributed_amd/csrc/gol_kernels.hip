@@ -1333,7 +1333,7 @@ __device__ __forceinline__ void push_group_hi(Lanes<WPL> &x0, Lanes<WPL> &x1, La
 template <int D, int WPL>
 __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int eb, int tile, bool self,
                                                 uint32_t *exp_mine, const uint32_t *exp_next, int *flag_mine,
-                                                int *flag_next, unsigned *error) {
+                                                int *flag_next, unsigned *error, unsigned long long *phase_tr) {
     using SP = SkewPlan<D>;
     constexpr int ROW = 64 * WPL;  // words of one LDS row
     const int lane = threadIdx.x & 63;
@@ -1420,6 +1420,7 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
     };
     static_for<SP::NPH>([&](auto j) { fill(std::integral_constant<int, SP::P(decltype(j)::value)>()); });
     fill(std::integral_constant<int, D>());
+    if (phase_tr && lane == 0) phase_tr[0] = (unsigned long long)__builtin_amdgcn_s_memrealtime();  // fill done
     // exports done: this wave's LDS writes complete before the flag (LDS
     // operations of a wave complete in order; no wait on its global loads)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1449,6 +1450,7 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
         x1 = vmov(n1);
         x2 = vmov(n2);
     }
+    if (phase_tr && lane == 0) phase_tr[1] = (unsigned long long)__builtin_amdgcn_s_memrealtime();  // main done
     if (!self) {
         // the band below has exported its top rows (almost always long ago)
         if (__hip_atomic_load(flag_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
@@ -1554,7 +1556,9 @@ __global__ __launch_bounds__(512) void gol_skew_kernel(SkewArgs p) {
     const int eb = bottom ? E0 : A0 + (int)(Ls * (cum + p.wgt[pos]) / tot) / 3 * 3;
     const long long t_start = p.trace ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
     const uint32_t cnt = stream_skew<D, WPL>(p.base, ab, eb, tile, bottom, s_exp[w], bottom ? nullptr : s_exp[w + p.tx],
-                                             &s_flag[w], bottom ? nullptr : &s_flag[w + p.tx], p.error);
+                                             &s_flag[w], bottom ? nullptr : &s_flag[w + p.tx], p.error,
+                                             (p.trace && blockIdx.x < 1024) ? p.trace + 8 + 2 * (blockIdx.x * 64 + 8 + w)
+                                                                            : nullptr);
     if (p.trace && lane == 0 && blockIdx.x < 1024) {
         p.trace[8 + 2 * (blockIdx.x * 64 + w)] = (unsigned long long)t_start;
         p.trace[8 + 2 * (blockIdx.x * 64 + w) + 1] = (unsigned long long)__builtin_amdgcn_s_memrealtime();

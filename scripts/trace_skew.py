@@ -38,7 +38,7 @@ with golhip.Board(W, R, timing=True) as b:
     b.step(200)
     b.sync()
     b.perf_reset()
-    b.step(a.depth)  # one launch (torus); a ring strip: the last launch of its exchange group
+    b.step(a.depth)  # one launch (torus only: a ring step would run its exchange group)
     b.sync()
     p = b.perf()
     t = b.persist_trace_waves(256).astype(np.int64)  # (blocks, 64, 2)
@@ -58,6 +58,17 @@ for w in range(8):
     if m.any():
         pos.append({"w": w, "dur_mean": round(float(dur[m, w].mean()), 2), "dur_min": round(float(dur[m, w].min()), 2),
                     "dur_max": round(float(dur[m, w].max()), 2), "end_mean": round(float(endr[m, w].mean()), 2)})
+# phase stamps (fill done, main loop done) of the same waves: slots 8..15
+fe, me = t[blocks, 8:16, 0], t[blocks, 8:16, 1]
+ok = live & (fe > 0) & (me > 0)
+if ok.any():
+    for q in pos:
+        m = ok[:, q["w"]]
+        if m.any():
+            w = q["w"]
+            q["fill_us"] = round(float(((fe[m, w] - st[m, w]) / 100.0).mean()), 2)
+            q["main_us"] = round(float(((me[m, w] - fe[m, w]) / 100.0).mean()), 2)
+            q["drain_us"] = round(float(((en[m, w] - me[m, w]) / 100.0).mean()), 2)
 res["positions"] = pos
 wg_end = np.where(live, endr, 0).max(axis=1)
 wg_mean = np.where(live, endr, 0).sum(axis=1) / np.maximum(1, live.sum(axis=1))
