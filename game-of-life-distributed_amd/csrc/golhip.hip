@@ -109,7 +109,8 @@ struct golhip {
 
     int tb_depth = 20;          // per-launch WPL-2 kernels fuse up to 20, the resident kernel 16
     int rows_per_wave = 0;      // 0 = automatic (per depth, from occupancy)
-    int cu_count = 0;
+    int cu_count = 0;           // CUs the launches are planned for (option "cu_count": fewer)
+    int dev_cu = 0;             // the device's CUs
     bool fill_skip = true;      // option "fill_skip"
     int split = 1;              // option "split": split tiling (K1s) for per-launch torus steps
                                 // (65536^2 +1.3 %, 262144^2 +4.4 %, profiles/r2t/split_ab.jsonl)
@@ -189,6 +190,15 @@ struct golhip {
     int nranks = 1, rank = 0;
     int ring_rows = 0;          // smallest strip of the ring (every rank plans from it)
     int halo_skip = 0;          // option "halo_skip" (measurement only: no exchange, wrong halos)
+    // option "overlap": the last launch of an exchange round runs its boundary
+    // rows on a side stream, then posts the next round's exchange there, while
+    // the interior rows run on the engine stream (launch_overlap)
+    int overlap = 0;
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_x = nullptr;
+    int halo_ready = 0;         // halo rows already exchanged for the board at turn halo_turn
+    int64_t halo_turn = -1;
+    int64_t overlap_launches = 0;
     int64_t halo_exchanges = 0;
     double halo_ms = 0;         // exchange time on the engine stream (GOLHIP_FLAG_TIMING)
 
@@ -403,6 +413,7 @@ int wpl_for(golhip_t h) {
 // Converts the current board in place when the wanted layout changes.
 int set_layout(golhip_t h, int il) {
     if (h->il == il) return GOLHIP_OK;
+    h->halo_ready = 0;
     if (h->loaded) HIP_OR_FAIL(golk::launch_convert_layout(h->cur_rows(), h->local_words(), h->il, il, h->stream));
     h->il = il;
     return GOLHIP_OK;
@@ -411,6 +422,7 @@ int want_il(golhip_t h) { return wpl_for(h) >= 2 ? wpl_for(h) : 0; }
 // After canonical words were written into the current buffer.
 int loaded_canonical(golhip_t h) {
     h->il = 0;
+    h->halo_ready = 0;
     h->loaded = true;
     return set_layout(h, want_il(h));
 }
@@ -688,8 +700,9 @@ bool skew_plan(golhip_t h, int depth, int wpl, const golk::StepArgs &a, golk::Sk
 // Launch the step kernel for output rows [lo, hi) of this handle (halos, if
 // used, already in place); `alive` (nullable) accumulates their popcount.
 // No bookkeeping: see finish_launch.
-int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int lo, int hi) {
-    const hipStream_t st = h->stream;
+int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int lo, int hi,
+                hipStream_t on = nullptr) {
+    const hipStream_t st = on ? on : h->stream;
     golk::StepArgs a = step_args(h, alive, halo);
     if (lo != 0 || hi != h->rows) shift_rows(a, lo, hi);
     const int wpl = wpl_for(h);
@@ -746,6 +759,7 @@ int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int
 
 void finish_launch(golhip_t h, int depth, bool count) {
     h->cur ^= 1;
+    h->halo_ready = 0;
     h->turns += depth;
     h->step_turns += depth;
     if (count) h->alive_turn = h->turns;
@@ -801,6 +815,39 @@ int launch_ext(golhip_t h, int depth, bool count, int ext) {
     }
     if (int rc = launch_rows(h, depth, alive, true, -ext, h->rows + ext)) return rc;
     finish_launch(h, depth, count);
+    return GOLHIP_OK;
+}
+
+// The last launch of an exchange round (ext 0) with the next round's
+// exchange of X rows overlapped (option "overlap"): the boundary rows
+// [0, X) and [rows - X, rows), which the exchange sends, run first on the
+// side stream and the exchange follows them there, while the interior rows
+// [X, rows - X) run on the engine stream; the engine waits for the exchange
+// before anything else.  All three launches read the current buffer and
+// write disjoint rows of the other; the exchange writes only halo rows.
+int ensure_side(golhip_t h) {
+    if (h->side) return GOLHIP_OK;
+    HIP_OR_FAIL(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+    HIP_OR_FAIL(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+    HIP_OR_FAIL(hipEventCreateWithFlags(&h->ev_x, hipEventDisableTiming));
+    return GOLHIP_OK;
+}
+
+int launch_overlap(golhip_t h, int depth, int X) {
+    if (int rc = ensure_side(h)) return rc;
+    HIP_OR_FAIL(hipEventRecord(h->ev_fork, h->stream));
+    HIP_OR_FAIL(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+    if (int rc = launch_rows(h, depth, nullptr, true, 0, X, h->side)) return rc;
+    if (int rc = launch_rows(h, depth, nullptr, true, h->rows - X, h->rows, h->side)) return rc;
+    if (int rc = launch_rows(h, depth, nullptr, true, X, h->rows - X)) return rc;
+    h->step_launches -= 2;  // one step launch in three parts
+    finish_launch(h, depth, false);
+    if (int rc = exchange_rccl(h, X, h->side)) return rc;
+    HIP_OR_FAIL(hipEventRecord(h->ev_x, h->side));
+    HIP_OR_FAIL(hipStreamWaitEvent(h->stream, h->ev_x, 0));
+    h->halo_ready = X;
+    h->halo_turn = h->turns;
+    h->overlap_launches++;
     return GOLHIP_OK;
 }
 
@@ -860,7 +907,7 @@ bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int w
     }
     p.nw = nw;
     if (!h->d_sync) {
-        if (hipMalloc(&h->d_sync, (size_t)(h->cu_count + 2) * sizeof(unsigned)) != hipSuccess ||
+        if (hipMalloc(&h->d_sync, (size_t)(h->dev_cu + 2) * sizeof(unsigned)) != hipSuccess ||
             hipHostMalloc(&h->h_err, sizeof(unsigned), hipHostMallocDefault) != hipSuccess) {
             *rc = fail(GOLHIP_ENOMEM, "persistent sync words");
             return false;
@@ -901,6 +948,7 @@ bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int w
         return false;
     }
     h->persist_pending = true;
+    h->halo_ready = 0;
     if (J & 1) h->cur ^= 1;
     const int64_t turns = J * depth - (half_last ? depth / 2 : 0);
     h->turns += turns;
@@ -1040,6 +1088,7 @@ int create_common(int32_t width, int32_t height, int32_t row0, int32_t rows, int
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) h->cu_count = prop.multiProcessorCount;
         if (h->cu_count <= 0) h->cu_count = 256;
+        h->dev_cu = h->cu_count;
     }
     const size_t bytes = (size_t)h->phys_rows * h->Ww * sizeof(uint32_t);
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
@@ -1366,6 +1415,12 @@ int golhip_destroy(golhip_t h) {
     int rc = GOLHIP_OK;
     HIP_RC(hipSetDevice(h->device));
     if (h->stream) HIP_RC(hipStreamSynchronize(h->stream));
+    if (h->side) {
+        HIP_RC(hipStreamSynchronize(h->side));
+        HIP_RC(hipStreamDestroy(h->side));
+    }
+    if (h->ev_fork) HIP_RC(hipEventDestroy(h->ev_fork));
+    if (h->ev_x) HIP_RC(hipEventDestroy(h->ev_x));
     for (auto &p : h->ev_pending) {
         HIP_RC(hipEventDestroy(p.e0));
         HIP_RC(hipEventDestroy(p.e1));
@@ -1503,6 +1558,17 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     }
     if (!strcmp(key, "force_halo")) {
         h->force_halo = value != 0;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "cu_count")) {  // measurement: plan launches for fewer CUs (0: all of the device's)
+        if (value < 0 || value > h->dev_cu) return fail(GOLHIP_EINVAL, "cu_count %lld not in 0..%d", (long long)value, h->dev_cu);
+        h->cu_count = value ? (int)value : h->dev_cu;
+        for (int &c : h->auto_rpw) c = 0;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "overlap")) {
+        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "overlap %lld", (long long)value);
+        h->overlap = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "halo_skip")) {  // measurement only: the halo rows go stale (wrong results)
@@ -1685,7 +1751,10 @@ int step_locked(golhip_t h, int64_t nturns, int32_t want_flips) {
         }
         const HaloRun hr = halo_next(depth_cap(h, true), sched_rows(h), persist_on(h), left - tail);
         const int d = hr.d, k = hr.k;
-        if (int rc = exchange_rccl(h, k * d, h->stream)) return rc;
+        // the halos may have come with the previous round's last launch (overlap)
+        if (!(h->halo_ready >= k * d && h->halo_turn == h->turns))
+            if (int rc = exchange_rccl(h, k * d, h->stream)) return rc;
+        h->halo_ready = 0;
         int prc = GOLHIP_OK;
         if (try_persist_halo(h, d, k, left - k * d == 0, &prc)) {
             left -= (int64_t)k * d;
@@ -1693,6 +1762,17 @@ int step_locked(golhip_t h, int64_t nturns, int32_t want_flips) {
         }
         if (prc) return prc;
         for (int i = 0; i < k; ++i) {
+            const int64_t after = left - d;
+            if (i == k - 1 && h->overlap && after > tail && h->W % 32 == 0) {
+                // the next round's exchange rows (every rank plans alike)
+                const HaloRun nr = halo_next(depth_cap(h, true), sched_rows(h), persist_on(h), after - tail);
+                const int X = nr.k * nr.d;
+                if (h->rows >= 4 * X) {
+                    if (int rc = launch_overlap(h, d, X)) return rc;
+                    left = after;
+                    continue;
+                }
+            }
             if (int rc = launch_ext(h, d, left - d == 0, (k - 1 - i) * d)) return rc;
             left -= d;
         }
@@ -1760,6 +1840,7 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
                                hipMemcpyDeviceToDevice, h->stream));
     h->cur = cur0;
     h->turns = turns0;
+    h->halo_ready = 0;
     h->alive_turn = -1;
     h->flips_valid = false;
     return step_locked(h, nturns, want_flips);
@@ -2092,6 +2173,7 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     out->skew_launches = h->skew_launches;
     out->halo_exchanges = h->halo_exchanges;
     out->halo_ms = h->halo_ms;
+    out->overlap_launches = h->overlap_launches;
     out->words_per_lane = h->W % 32 == 0 ? wpl_for(h) : 0;
     out->persist_depth = h->W % 32 == 0 ? persist_depth_for(h, wpl_for(h)) : 0;
     return GOLHIP_OK;
@@ -2133,6 +2215,7 @@ int golhip_perf_reset(golhip_t h) {
     h->flip_ms = 0;
     h->halo_exchanges = 0;
     h->halo_ms = 0;
+    h->overlap_launches = 0;
     return GOLHIP_OK;
 }
 

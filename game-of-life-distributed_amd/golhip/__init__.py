@@ -58,6 +58,7 @@ class Perf(ctypes.Structure):
         ("skew_launches", ctypes.c_int64),
         ("halo_exchanges", ctypes.c_int64),
         ("halo_ms", ctypes.c_double),
+        ("overlap_launches", ctypes.c_int64),
     ]
 
     def as_dict(self) -> dict:

@@ -88,6 +88,9 @@ typedef struct golhip_perf {
     int64_t halo_exchanges;   /* halo exchanges posted (RCCL ring)               */
     double halo_ms;           /* their summed time on the stream they ran on
                                  (GOLHIP_FLAG_TIMING)                           */
+    int64_t overlap_launches; /* step launches split into boundary rows + the next
+                                 exchange (side stream) and interior rows (option
+                                 "overlap")                                     */
 } golhip_perf_t;
 
 /* ---- library ---------------------------------------------------------- */
@@ -160,7 +163,10 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * "force_halo" (0): after golhip_comm_init with one rank, run a whole board
  * through the multi-GPU path as a one-rank RCCL ring (tests, measurement);
  * "halo_skip" (0): measurement only, post no halo exchange (the halo rows go
- * stale: WRONG results; isolates the exchange's cost). */
+ * stale: WRONG results; isolates the exchange's cost); "overlap" (0): in a
+ * ring, the last launch before each exchange runs the rows the exchange sends
+ * first, on a side stream followed by the exchange, while the interior rows
+ * run on the engine stream (results identical). */
 int golhip_set_option(golhip_t h, const char *key, int64_t value);
 
 /* ---- multi-GPU -------------------------------------------------------- */

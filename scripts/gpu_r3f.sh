@@ -1,28 +1,20 @@
-# skew tests, bench lines (no per-launch events), kernel traces, store policy A/B without events
+# exchange overlap (option "overlap"): parity tests, A/B on one-rank-ring strips, kernel trace of an overlapped ring
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-out=$GRAFT_REPO_ROOT/gpurun_out/${1:-r3f}
+out=gpurun_out/${1:-r3f}
 mkdir -p $out
-timeout -k 10 500 python -u -m pytest tests/test_gpu_skew.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $out/pytest_skew.log 2>&1 || { echo "pytest failed"; tail -40 $out/pytest_skew.log; exit 1; }
-tail -2 $out/pytest_skew.log
-for wl in 65536 16384 262144; do
-  timeout -k 10 300 python -u bench.py --workload $wl --steps 5 --no-cpu-baseline > $out/bench_$wl.json 2> $out/bench_$wl.err || { tail $out/bench_$wl.err; exit 1; }
-  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[2], d['value'], d['parity'], d['ms_per_step'], r['kernel'], r['avg_launch_ms'], r['launches'], r['frac'])" $out/bench_$wl.json $wl
-done
+timeout -k 10 400 python -u -m pytest tests/test_gpu_skew.py -k "overlap or rccl_ring" -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $out/pytest_overlap.log 2>&1 || { echo "pytest failed"; tail -40 $out/pytest_overlap.log; exit 1; }
+tail -2 $out/pytest_overlap.log
+timeout -k 10 300 python -u -m pytest tests/test_gpu_fullsize.py -k "rccl_ring" -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > $out/pytest_fullsize_ring.log 2>&1 || { echo "pytest failed"; tail -40 $out/pytest_fullsize_ring.log; exit 1; }
+tail -2 $out/pytest_fullsize_ring.log
+timeout -k 10 400 python -u scripts/sweep_opts.py --no-timing --reps 3 --cases "65536x8192r,65536x16384r,262144x32768r" --sets "overlap=0;overlap=1;halo_skip=1" > $out/overlap_ab.txt 2> $out/overlap_ab.err || { tail $out/overlap_ab.err; exit 1; }
+grep -A100 "^# best" $out/overlap_ab.txt
+timeout -k 10 200 python -u scripts/sweep_opts.py --reps 1 --cases "65536x8192r" --sets "overlap=0;overlap=1" > $out/overlap_timed.txt 2>> $out/overlap_ab.err || { tail $out/overlap_ab.err; exit 1; }
+grep '^{' $out/overlap_timed.txt
 cd /tmp && export TMPDIR=/tmp
-for wl in 65536 16384; do
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_$wl -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --workload $wl --steps 3 --warmup-seconds 0.5 --no-cpu-baseline > $out/trace_$wl.log 2>&1 || { tail $out/trace_$wl.log; exit 1; }
-done
-cd $GRAFT_REPO_ROOT
-for rep in 1 2; do
-  for lib in libgolhip.so libgolhip_sc1.so; do
-    GOLHIP_LIB=$GRAFT_REPO_ROOT/game-of-life-distributed_amd/golhip/$lib timeout -k 10 200 python -u scripts/sweep_opts.py --no-timing --reps 1 --cases "65536x65536,16384x16384,65536x8192,65536x8192r,262144x32768r" --sets "skew=1" >> $out/storepol.txt 2>> $out/storepol.err || { tail $out/storepol.err; exit 1; }
-  done
-done
-grep '^{' $out/storepol.txt | python3 -c "
-import json,sys,collections
-best=collections.defaultdict(float)
-for l in sys.stdin:
-    d=json.loads(l); k=(d['case'],d['lib']); best[k]=max(best[k],d['gcups'])
-for k,v in sorted(best.items()): print(k, round(v,1))
-"
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$out/trace_overlap -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/scripts/sweep_opts.py --no-timing --reps 1 --turns 400 --cases 65536x8192r --sets "overlap=1" > $GRAFT_REPO_ROOT/$out/trace_overlap.log 2>&1 || { tail $GRAFT_REPO_ROOT/$out/trace_overlap.log; exit 1; }
+
+# instruction-fetch sharing probe: the same per-wave work on all CUs vs half / a quarter of them
+timeout -k 10 300 python -u scripts/sweep_opts.py --no-timing --reps 2 --cases "65536x65536,65536x32768,65536x16384" --sets "cu_count=0;cu_count=128;cu_count=64" > $GRAFT_REPO_ROOT/$out/cu_probe.txt 2>> $GRAFT_REPO_ROOT/$out/overlap_ab.err || { tail $GRAFT_REPO_ROOT/$out/overlap_ab.err; exit 1; }
+grep -A100 "^# best" $GRAFT_REPO_ROOT/$out/cu_probe.txt
+echo done

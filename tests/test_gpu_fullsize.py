@@ -117,9 +117,10 @@ def test_config2_strips_in_process(full, nstrips):
             s.close()
 
 
-@pytest.mark.parametrize("persistent", [-1, 1, 0])
-def test_config2_rccl_ring_one_rank(full, persistent):
-    """configs[2] through the RCCL halo path (a one-rank ring, deep halos)."""
+@pytest.mark.parametrize("persistent,overlap", [(-1, 0), (1, 0), (0, 0), (-1, 1)])
+def test_config2_rccl_ring_one_rank(full, persistent, overlap):
+    """configs[2] through the RCCL halo path (a one-rank ring, deep halos;
+    overlap: boundary rows + exchange on a side stream)."""
     js, rows = full
     rec = js["c2"]
     N = rec["width"]
@@ -127,6 +128,7 @@ def test_config2_rccl_ring_one_rank(full, persistent):
         b.comm_init(golhip.unique_id(), 1, 0)
         b.set_option("force_halo", 1)
         b.set_option("persistent", persistent)
+        b.set_option("overlap", overlap)
         if persistent == 0:
             b.set_option("skew", 0)
         b.fill_random(rec["seed"])
