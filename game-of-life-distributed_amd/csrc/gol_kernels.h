@@ -14,6 +14,7 @@ namespace golk {
 constexpr int kHalo = 128;
 constexpr int kWave = 64;
 constexpr int kTileValid = 62;   // lanes per wavefront tile that are stored (lanes 1..62)
+constexpr int kHalfTileValid = 30;  // K1w half-wave tiles: lanes 1..30 of each 32-lane half
 
 // How a step kernel finds input row i (logical, may be outside 0..rows-1).
 //   torus mode : phys = base + mod(i, wrap)                 (whole board on one device)
@@ -86,6 +87,8 @@ struct SkewArgs {
     StepArgs base;
     int tiles_x;
     int tx;           // tiles per workgroup: 1 (stacks of 8 bands) or 2 (stacks of 4)
+    int half;         // 1: half-wave tiles of 30 lanes (tiles_x counts them); each wave's upper lanes
+                      //    run the same band of the stack rows_out / 2 further down (rows_out even)
     int nst;          // stacks per tile column
     int wgt[8];       // band heights by stack position (relative weights)
     int hcap;         // rows the stack's bottom band gives up (its drain is computed in full)
@@ -94,8 +97,8 @@ struct SkewArgs {
     unsigned long long *trace;  // nullable diagnostics: per wave (start, end) s_memrealtime at 8 + 2 (block * 64 + wave),
                                 // (fill done, main loop done) at 8 + 2 (block * 64 + 8 + wave)
 };
-bool skew_supported(int depth, int wpl);
-int skew_blocks_per_cu(int depth, int wpl);
+bool skew_supported(int depth, int wpl, bool half = false);
+int skew_blocks_per_cu(int depth, int wpl, bool half = false);
 hipError_t launch_skew(const SkewArgs &p, int depth, int wpl, hipStream_t s);
 
 // Persistent multi-super-step step kernel (torus, or a strip's extended rows

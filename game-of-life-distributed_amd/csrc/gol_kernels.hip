@@ -1330,21 +1330,31 @@ __device__ __forceinline__ void push_group_hi(Lanes<WPL> &x0, Lanes<WPL> &x1, La
 // One band [ab, eb) of input rows (StepArgs frame) of tile `tile`.  self: no
 // band below in the workgroup (compute the drain from board rows).  Exports
 // go to exp_mine (LDS slot of this wave), imports come from exp_next.
-template <int D, int WPL>
+// HALF (half-wave tiles): lanes 0-31 and 32-63 are two tiles of 30 stored
+// lanes each (lanes 0, 31, 32, 63 are their halos), of the same tile column
+// but rows `dr` apart (the same band of two stacks): narrow boards waste less
+// of a wave on padding (16384^2: nine 60-word tiles for 512 words instead of
+// five 124-word ones).  Everything lane-wise (loads, stores, LDS hand-offs)
+// just takes the upper half's rows `dr` further down.
+template <int D, int WPL, bool HALF = false>
 __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int eb, int tile, bool self,
                                                 uint32_t *exp_mine, const uint32_t *exp_next, int *flag_mine,
-                                                int *flag_next, unsigned *error, unsigned long long *phase_tr) {
+                                                int *flag_next, unsigned *error, unsigned long long *phase_tr,
+                                                int dr = 0) {
     using SP = SkewPlan<D>;
     constexpr int ROW = 64 * WPL;  // words of one LDS row
+    constexpr int TV = HALF ? kHalfTileValid : kTileValid;
     const int lane = threadIdx.x & 63;
+    const int hl = HALF ? (lane & 31) : lane;        // lane within its tile
+    const int rofs = (HALF && lane >= 32) ? dr : 0;  // the upper half's rows
     const int Ww = a.Ww;
     const int S = eb - ab;
-    const int t0 = tile * kTileValid * WPL;
-    int col = (t0 + WPL * (lane - 1)) % Ww;
+    const int t0 = tile * TV * WPL;
+    int col = (t0 + WPL * (hl - 1)) % Ww;
     if (col < 0) col += Ww;
-    const bool keep = lane >= 1 && lane <= kTileValid && (t0 + WPL * (lane - 1)) < Ww;
+    const bool keep = hl >= 1 && hl <= TV && (t0 + WPL * (hl - 1)) < Ww;
     // input rows ab, ab + 1, ... through the row map (torus wrap or halo clamp)
-    int r = ab + a.in.off;
+    int r = ab + rofs + a.in.off;
     const int wrap = a.in.wrap > 0 ? a.in.wrap : INT_MAX;
     if (a.in.wrap > 0) {
         r %= a.in.wrap;
@@ -1360,12 +1370,13 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
     // (buffer stores for every width: a masked store's branch and EXEC writes
     // put hazard s_nops between parity_fix and the group's first DPP)
     const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
-        a.dst + (size_t)(a.dst_base + ab + D) * Ww, (short)0, S * Ww * 4, 0x00020000);
-    const int clo = a.count_lo - (ab + D), chi = a.count_hi - (ab + D);
+        a.dst + (size_t)(a.dst_base + ab + D) * Ww, (short)0, (S + (HALF ? dr : 0)) * Ww * 4, 0x00020000);
+    const int clo = a.count_lo - (ab + D + rofs), chi = a.count_hi - (ab + D + rofs);
+    const int colw = col + rofs * Ww;  // the lane's word offset from the band's first output row
     uint32_t cnt = 0;
     auto emit = [&](const Lanes<WPL> &y, int oi) {
         const bool ok = keep && (unsigned)oi < (unsigned)S;
-        const int off = ok ? (oi * Ww + col) * 4 : INT_MAX;  // out of range: dropped
+        const int off = ok ? (oi * Ww + colw) * 4 : INT_MAX;  // out of range: dropped
         if constexpr (WPL == 1)
             __builtin_amdgcn_raw_buffer_store_b32(y.w[0], brs, off, 0, GOL_SKEW_STORE_CPOL);
         else if constexpr (WPL == 2)
@@ -1523,7 +1534,7 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
 
 // K1w: one workgroup = one stack = tx tiles x (8 / tx) bands; wave w takes
 // tile w % tx and stack position w / tx (top to bottom).
-template <int D, int WPL>
+template <int D, int WPL, bool HALF = false>
 __global__ __launch_bounds__(512) void gol_skew_kernel(SkewArgs p) {
     using SP = SkewPlan<D>;
     constexpr int ROW = 64 * WPL;
@@ -1541,7 +1552,9 @@ __global__ __launch_bounds__(512) void gol_skew_kernel(SkewArgs p) {
     __syncthreads();
     if (tile >= p.tiles_x) return;  // wave-uniform, after the only barrier (its stack's waves all leave)
     if (p.prio_young && w >= 4) __builtin_amdgcn_s_setprio(1);
-    const int L = p.base.rows_out;
+    // HALF: the stacks split the first half of the rows; each wave's upper
+    // lanes take the same band L / 2 rows further down (L even, host-checked)
+    const int L = HALF ? p.base.rows_out / 2 : p.base.rows_out;
     const int A0 = (int)((int64_t)stack * L / p.nst) - D, E0 = (int)((int64_t)(stack + 1) * L / p.nst) - D;
     const int64_t Ls = (int64_t)(E0 - A0) + p.hcap;
     int cum = 0, tot = 0;
@@ -1555,10 +1568,11 @@ __global__ __launch_bounds__(512) void gol_skew_kernel(SkewArgs p) {
     const int ab = A0 + (int)(Ls * cum / tot) / 3 * 3;
     const int eb = bottom ? E0 : A0 + (int)(Ls * (cum + p.wgt[pos]) / tot) / 3 * 3;
     const long long t_start = p.trace ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
-    const uint32_t cnt = stream_skew<D, WPL>(p.base, ab, eb, tile, bottom, s_exp[w], bottom ? nullptr : s_exp[w + p.tx],
+    const uint32_t cnt = stream_skew<D, WPL, HALF>(p.base, ab, eb, tile, bottom, s_exp[w], bottom ? nullptr : s_exp[w + p.tx],
                                              &s_flag[w], bottom ? nullptr : &s_flag[w + p.tx], p.error,
                                              (p.trace && blockIdx.x < 1024) ? p.trace + 8 + 2 * (blockIdx.x * 64 + 8 + w)
-                                                                            : nullptr);
+                                                                            : nullptr,
+                                             L);
     if (p.trace && lane == 0 && blockIdx.x < 1024) {
         p.trace[8 + 2 * (blockIdx.x * 64 + w)] = (unsigned long long)t_start;
         p.trace[8 + 2 * (blockIdx.x * 64 + w) + 1] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
@@ -1828,22 +1842,26 @@ hipError_t launch_split(const SplitArgs &p, int depth, int wpl, hipStream_t s) {
 }
 
 template <typename F>
-static hipError_t dispatch_skew(int depth, int wpl, F &&f) {
+static hipError_t dispatch_skew(int depth, int wpl, bool half, F &&f) {
 #define GOL_WCASE(D, WP) \
-    if (depth == D && wpl == WP) return f(gol_skew_kernel<D, WP>);
+    if (!half && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP>);
+#define GOL_HCASE(D, WP) \
+    if (half && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP, true>);
     GOL_WCASE(8, 2) GOL_WCASE(12, 2) GOL_WCASE(16, 2) GOL_WCASE(20, 2) GOL_WCASE(8, 4) GOL_WCASE(9, 4)
     GOL_WCASE(16, 1) GOL_WCASE(32, 1)
+    GOL_HCASE(16, 2) GOL_HCASE(20, 2)
 #undef GOL_WCASE
+#undef GOL_HCASE
     return hipErrorInvalidValue;
 }
 
-bool skew_supported(int depth, int wpl) {
-    return dispatch_skew(depth, wpl, [](auto) { return hipSuccess; }) == hipSuccess;
+bool skew_supported(int depth, int wpl, bool half) {
+    return dispatch_skew(depth, wpl, half, [](auto) { return hipSuccess; }) == hipSuccess;
 }
 
-int skew_blocks_per_cu(int depth, int wpl) {
+int skew_blocks_per_cu(int depth, int wpl, bool half) {
     int b = 0;
-    hipError_t e = dispatch_skew(depth, wpl, [&](auto kern) {
+    hipError_t e = dispatch_skew(depth, wpl, half, [&](auto kern) {
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 512, 0);
     });
     return e == hipSuccess ? b : 0;
@@ -1851,7 +1869,7 @@ int skew_blocks_per_cu(int depth, int wpl) {
 
 hipError_t launch_skew(const SkewArgs &p, int depth, int wpl, hipStream_t s) {
     const int tcols = (p.tiles_x + p.tx - 1) / p.tx;
-    return dispatch_skew(depth, wpl, [&](auto kern) {
+    return dispatch_skew(depth, wpl, p.half != 0, [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(tcols * p.nst), dim3(512), 0, s, p);
         return hipGetLastError();
     });

@@ -124,10 +124,13 @@ struct golhip {
     int skew_hcap = -1;             // option "skew_hcap": rows a stack's bottom band gives up (-1: 3 D / 4)
     int skew_prio = 0;              // option "skew_prio": s_setprio 1 for waves 4..7
     int skew_tx = 0;                // option "skew_tx": tiles per K1w workgroup (0: plan, 1 or 2)
-    int skew_bpc[kNumDepths][3] = {};  // K1w workgroups per CU by (depth, wpl) (0: not queried)
+    int skew_half = 0;
+    int skew_nst = 0;               // option "skew_nst" (measurement): stacks per tile column (0: plan)              // option "skew_half": half-wave tiles (0: when fewer wave-rows, 1: whenever possible, -1: never)
+    int skew_bpc[kNumDepths][6] = {};  // K1w workgroups per CU by (depth, wpl, half) (0: not queried)
     unsigned *skew_err = nullptr;      // host-mapped spin-bound flag of the K1w kernels
     unsigned *skew_err_dev = nullptr;
     int64_t skew_launches = 0;
+    int64_t skew_half_launches = 0;
     int persistent = -1;        // option "persistent": K1p for long torus runs (1 on, 0 off, -1 auto)
     int wpl_opt = 0;            // option "wpl": words per lane (0 = auto, 1, 2, 4)
     int persist_depth = 0;      // option "persist_depth" (0: tb_depth)
@@ -365,9 +368,14 @@ int persist_nw_for(golhip_t h, int depth, int wpl) {
 // a ring decides alike, as the choice also fixes the word layout).  A row
 // strip runs K1p between two deep-halo exchanges (golhip_step).
 constexpr int64_t kPersistAutoMaxBytes = 64ll << 20;
+int wpl_per_launch(golhip_t h);
+bool skew_fills(golhip_t h);
 bool persist_on(golhip_t h) {
     if (h->persistent >= 0) return h->persistent != 0;
-    if (h->skew) return false;  // K1w per launch (round 3)
+    // round 3: K1w per launch wherever its stacks fill the CUs (16384^2: 82
+    // vs 62 TCUPS); smaller boards keep the resident kernel (8192^2: 27.9
+    // vs 21.7 for K1w and 12.8 for the per-launch K1, profiles/r3i)
+    if (h->skew && skew_fills(h)) return false;
     return (int64_t)sched_rows(h) * h->Ww * 4 <= kPersistAutoMaxBytes;
 }
 
@@ -378,7 +386,25 @@ int wpl_for(golhip_t h) {
     if (h->W % 64 != 0) return 1;
     if (h->wpl_opt == 1 || h->wpl_opt == 2) return h->wpl_opt;
     if (h->wpl_opt == 4) return h->W % 128 == 0 ? 4 : 2;
-    if ((!h->torus() && !h->comm) || !persist_on(h)) {
+    if ((!h->torus() && !h->comm) || !persist_on(h)) return wpl_per_launch(h);
+    auto best = [&](int wpl) {
+        const int d = default_depth(h, wpl);
+        const int def = golk::persist_waves_for(d, wpl);
+        return std::max(plan_rate(h, wpl, def, d), def == 16 ? plan_rate(h, wpl, 8, d) : 0.0);
+    };
+    // The model charges WPL 2's halved bands too much fill: at 16384^2 it
+    // prefers WPL 1 by 4 %, but WPL 2 (8 waves) measured 61.7 vs 59.0 TCUPS
+    // on the same box (profiles/r2p/persist_wpl_16384.txt), so WPL 2 wins
+    // unless the model puts it more than 5 % behind.
+    return best(2) >= 0.95 * best(1) ? 2 : 1;
+}
+
+// Words per lane of the per-launch kernels (the option, else the rate model).
+int wpl_per_launch(golhip_t h) {
+    if (h->W % 64 != 0) return 1;
+    if (h->wpl_opt == 1 || h->wpl_opt == 2) return h->wpl_opt;
+    if (h->wpl_opt == 4) return h->W % 128 == 0 ? 4 : 2;
+    {
         // per-launch kernels (group strips, large boards): the hardware refills freed wave
         // slots, so band height matters less; stored fraction / slots per word
         // (16384-wide strips: 55.6 vs 51.2 TCUPS for wpl 2 vs 1, profiles/r1e)
@@ -396,16 +422,6 @@ int wpl_for(golhip_t h) {
         const int two = rate(2) >= rate(1) ? 2 : 1;
         return (h->W % 128 == 0 && rate(4) > 1.03 * rate(two)) ? 4 : two;
     }
-    auto best = [&](int wpl) {
-        const int d = default_depth(h, wpl);
-        const int def = golk::persist_waves_for(d, wpl);
-        return std::max(plan_rate(h, wpl, def, d), def == 16 ? plan_rate(h, wpl, 8, d) : 0.0);
-    };
-    // The model charges WPL 2's halved bands too much fill: at 16384^2 it
-    // prefers WPL 1 by 4 %, but WPL 2 (8 waves) measured 61.7 vs 59.0 TCUPS
-    // on the same box (profiles/r2p/persist_wpl_16384.txt), so WPL 2 wins
-    // unless the model puts it more than 5 % behind.
-    return best(2) >= 0.95 * best(1) ? 2 : 1;
 }
 
 // The wpl = 2 step kernels run on the interleaved pair layout; every other
@@ -629,46 +645,83 @@ int split_buffers(golhip_t h, golk::SplitArgs &sp, int depth, int wpl) {
 // band below's exports) and the stack's bottom band `hcap` rows shorter (it
 // computes its drain in full).  tx = 2 (stacks of 4
 // bands, two tiles a workgroup) when the tile count fits the CUs better.
-int skew_bpc(golhip_t h, int depth, int wpl) {
-    int &c = h->skew_bpc[depth_index(depth)][wpl == 4 ? 2 : wpl - 1];
+int skew_bpc(golhip_t h, int depth, int wpl, bool half) {
+    int &c = h->skew_bpc[depth_index(depth)][(wpl == 4 ? 2 : wpl - 1) + (half ? 3 : 0)];
     if (c == 0) {
-        const int b = golk::skew_blocks_per_cu(depth, wpl);
+        const int b = golk::skew_blocks_per_cu(depth, wpl, half);
         c = b > 0 ? b : -1;
     }
     return c;
 }
 
-bool skew_plan(golhip_t h, int depth, int wpl, const golk::StepArgs &a, golk::SkewArgs *sk) {
+// The stack plan of a K1w launch over L rows: tiles, workgroup shape, stacks
+// and tile kind (no side effects); false if K1w does not apply.
+bool skew_dims(golhip_t h, int depth, int wpl, int L, golk::SkewArgs *sk) {
     if (!h->skew || h->W % 32 != 0 || !golk::skew_supported(depth, wpl)) return false;
-    const int bpc = skew_bpc(h, depth, wpl);
-    if (bpc < 1) return false;
-    const int tiles = golk::tb_tiles(h->Ww, wpl);
-    const int L = a.rows_out;
     const int hcap = h->skew_hcap >= 0 ? h->skew_hcap : 3 * depth / 4;
     const int smin = depth + 3;
-    int best_tx = 0, best_nst = 0;
+    // half-wave tiles (30 stored lanes a tile, two tiles a wave, the upper one
+    // L / 2 rows down): when they need fewer wave-rows than 62-lane tiles
+    // (16384^2: 4.5 vs 5 waves a row), or when forced; L must be even
+    const bool half_ok = h->skew_half >= 0 && L % 2 == 0 && golk::skew_supported(depth, wpl, true);
+    int best_tx = 0, best_nst = 0, best_half = 0, best_tiles = 0;
     double best = 1e300;
-    for (int tx = 1; tx <= 2; ++tx) {
-        if (h->skew_tx && tx != h->skew_tx) continue;
-        const int sy = 8 / tx, tcols = (tiles + tx - 1) / tx;
-        const int nst = std::min(h->cu_count * bpc / tcols, (L + hcap) / (sy * (smin + hcap)));
-        if (nst < 1) continue;
-        const double per_wave = ((double)L / nst + hcap) / sy;  // input rows a wave streams
-        if (per_wave < best * 0.999) {
-            best = per_wave;
-            best_tx = tx;
-            best_nst = nst;
+    for (int half = 0; half <= (half_ok ? 1 : 0); ++half) {
+        if (!half && half_ok && h->skew_half > 0) continue;  // forced
+        const int bpc = skew_bpc(h, depth, wpl, half);
+        if (bpc < 1) continue;
+        const int tiles = half ? (h->Ww + golk::kHalfTileValid * wpl - 1) / (golk::kHalfTileValid * wpl)
+                               : golk::tb_tiles(h->Ww, wpl);
+        const int Lh = half ? L / 2 : L;
+        for (int tx = 1; tx <= 2; ++tx) {
+            if (h->skew_tx && tx != h->skew_tx) continue;
+            const int sy = 8 / tx, tcols = (tiles + tx - 1) / tx;
+            // stacks of Lh / nst + hcap rows whose bands average at least smin + hcap
+            // rows (the bottom band gives up hcap of them)
+            const int nst = std::min(h->cu_count * bpc / tcols,
+                                     h->skew_nst > 0 ? h->skew_nst : Lh / (sy * (smin + hcap) - hcap));
+            if (nst < 1) continue;
+            // "skew" 1 (default): only when the stacks fill at least 3/4 of the CUs'
+            // workgroup slots (smaller tori run the resident kernel, persist_on);
+            // 2: whenever a plan exists (tests)
+            if (h->skew == 1 && (int64_t)nst * tcols * 4 < (int64_t)h->cu_count * bpc * 3) continue;
+            // a wave's buffer-store range (its band, plus L / 2 rows for half tiles) must stay < 2 GiB
+            if (((double)Lh / nst + hcap + (half ? Lh : 0)) * h->Ww * 4 >= 2147483648.0) continue;
+            // input rows a wave streams; half tiles pay ~2 % for per-lane row addressing
+            const double per_wave = ((double)Lh / nst + hcap) / sy * (half ? 1.02 : 1.0);
+            if (per_wave < best * 0.999) {
+                best = per_wave;
+                best_tx = tx;
+                best_nst = nst;
+                best_half = half;
+                best_tiles = tiles;
+            }
         }
     }
     if (!best_tx) return false;
-    // "skew" 1 (default): only when the stacks fill at least 3/4 of the CUs'
-    // workgroup slots (a 5120^2 board makes 32 stacks of 2 tiles: the
-    // per-launch kernels with short bands are faster there); 2: whenever a
-    // plan exists (tests)
-    if (h->skew == 1 && (int64_t)best_nst * ((tiles + best_tx - 1) / best_tx) * 4 < (int64_t)h->cu_count * bpc * 3)
-        return false;
-    // a wave's buffer-store range (its band) must stay < 2 GiB
-    if (((double)L / best_nst + hcap) * h->Ww * 4 >= 2147483648.0) return false;
+    sk->tiles_x = best_tiles;
+    sk->tx = best_tx;
+    sk->nst = best_nst;
+    sk->half = best_half;
+    sk->hcap = hcap;
+    return true;
+}
+
+// Whether K1w would run this handle's whole-launch steps (its stacks fill
+// the CUs at the per-launch words per lane and depth); persist_on keeps the
+// resident kernel for the tori where it would not.
+bool skew_fills(golhip_t h) {
+    if (!h->skew || h->W % 32 != 0) return false;
+    const int wpl = wpl_per_launch(h);
+    int cap = std::min(h->tb_depth, golk::max_depth_for(wpl));
+    if (cap == 9 && wpl != 4) cap = 8;
+    const int depth = cap == 9 ? 9 : largest_depth(cap);
+    golk::SkewArgs sk{};
+    return skew_dims(h, depth, wpl, sched_rows(h), &sk);
+}
+
+bool skew_plan(golhip_t h, int depth, int wpl, const golk::StepArgs &a, golk::SkewArgs *sk) {
+    if (!skew_dims(h, depth, wpl, a.rows_out, sk)) return false;
     if (!h->skew_err) {
         void *p = nullptr, *d = nullptr;
         if (hipHostMalloc(&p, sizeof(unsigned), hipHostMallocMapped) != hipSuccess) return false;
@@ -680,17 +733,13 @@ bool skew_plan(golhip_t h, int depth, int wpl, const golk::StepArgs &a, golk::Sk
         h->skew_err_dev = static_cast<unsigned *>(d);
         *h->skew_err = 0;
     }
-    sk->tiles_x = tiles;
-    sk->tx = best_tx;
-    sk->nst = best_nst;
-    const int sy = 8 / best_tx;
+    const int sy = 8 / sk->tx;
     // The SIMD arbiter serves the older wave of a SIMD (waves 0..3) first: the
     // younger waves' bands are shorter so both finish together.  Measured
     // (round-3 skew_young sweeps, scripts/sweep_opts.py): two words per lane
     // 66-70 %, quads at depth 9 76-82 %.
     const int young = h->skew_young > 0 ? h->skew_young : wpl == 4 ? 78 : 68;
-    for (int q = 0; q < 8; ++q) sk->wgt[q] = (q < sy && q * best_tx >= 4) ? young : 100;
-    sk->hcap = hcap;
+    for (int q = 0; q < 8; ++q) sk->wgt[q] = (q < sy && q * sk->tx >= 4) ? young : 100;
     sk->prio_young = h->skew_prio;
     sk->error = h->skew_err_dev;
     sk->trace = h->d_trace;
@@ -754,6 +803,7 @@ int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int
     h->step_launches++;
     h->split_launches += split;
     h->skew_launches += skew;
+    h->skew_half_launches += skew && sk.half;
     return GOLHIP_OK;
 }
 
@@ -1606,6 +1656,16 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         h->skew_prio = (int)value;
         return GOLHIP_OK;
     }
+    if (!strcmp(key, "skew_nst")) {
+        if (value < 0 || value > 100000) return fail(GOLHIP_EINVAL, "skew_nst %lld", (long long)value);
+        h->skew_nst = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "skew_half")) {
+        if (value < -1 || value > 1) return fail(GOLHIP_EINVAL, "skew_half %lld", (long long)value);
+        h->skew_half = (int)value;
+        return GOLHIP_OK;
+    }
     if (!strcmp(key, "skew_tx")) {
         if (value < 0 || value > 2) return fail(GOLHIP_EINVAL, "skew_tx %lld", (long long)value);
         h->skew_tx = (int)value;
@@ -1802,6 +1862,7 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     const int64_t persist_turns0 = h->persist_turns, persist_launches0 = h->persist_launches;
     const int64_t step_launches0 = h->step_launches, step_turns0 = h->step_turns;
     const int64_t split_launches0 = h->split_launches, skew_launches0 = h->skew_launches;
+    const int64_t skew_half_launches0 = h->skew_half_launches;
     const size_t ev0 = h->ev_pending.size();
     const int64_t halo_exchanges0 = h->halo_exchanges, halo_bytes0 = h->halo_bytes;
     int rc = step_locked(h, nturns, want_flips);
@@ -1827,6 +1888,7 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     h->step_turns = step_turns0;
     h->split_launches = split_launches0;
     h->skew_launches = skew_launches0;
+    h->skew_half_launches = skew_half_launches0;
     h->halo_exchanges = halo_exchanges0;
     h->halo_bytes = halo_bytes0;
     if (h->ev_pending.size() >= ev0) {  // the abandoned attempt's launch timings (unless drained meanwhile)
@@ -2174,6 +2236,7 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     out->halo_exchanges = h->halo_exchanges;
     out->halo_ms = h->halo_ms;
     out->overlap_launches = h->overlap_launches;
+    out->skew_half_launches = h->skew_half_launches;
     out->words_per_lane = h->W % 32 == 0 ? wpl_for(h) : 0;
     out->persist_depth = h->W % 32 == 0 ? persist_depth_for(h, wpl_for(h)) : 0;
     return GOLHIP_OK;
@@ -2216,6 +2279,7 @@ int golhip_perf_reset(golhip_t h) {
     h->halo_exchanges = 0;
     h->halo_ms = 0;
     h->overlap_launches = 0;
+    h->skew_half_launches = 0;
     return GOLHIP_OK;
 }
 

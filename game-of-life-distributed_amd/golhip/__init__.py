@@ -59,6 +59,7 @@ class Perf(ctypes.Structure):
         ("halo_exchanges", ctypes.c_int64),
         ("halo_ms", ctypes.c_double),
         ("overlap_launches", ctypes.c_int64),
+        ("skew_half_launches", ctypes.c_int64),
     ]
 
     def as_dict(self) -> dict:

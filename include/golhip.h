@@ -91,6 +91,7 @@ typedef struct golhip_perf {
     int64_t overlap_launches; /* step launches split into boundary rows + the next
                                  exchange (side stream) and interior rows (option
                                  "overlap")                                     */
+    int64_t skew_half_launches; /* of skew_launches, those on half-wave tiles    */
 } golhip_perf_t;
 
 /* ---- library ---------------------------------------------------------- */
@@ -139,12 +140,14 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * (0 = by kernel: 68 %, quads 78 %): band height of waves 4..7 relative to
  * waves 0..3; "skew_hcap" (-1 = 3 D / 4): rows a stack's bottom band gives
  * up (it computes its own drain); "skew_tx" (0 = plan, 1, 2): tiles across
- * a stack; "skew_prio" (0): s_setprio for the
+ * a stack; "skew_half" (0 = when they need fewer wave-rows, 1 = whenever
+ * possible, -1 = never): half-wave tiles (30 stored lanes each, two per
+ * wave); "skew_prio" (0): s_setprio for the
  * younger waves; "split" (1): split tiling (gol_split_pair_kernel) for torus
  * steps when skew is off; "timing" (the GOLHIP_FLAG_TIMING flag after
  * creation: per-launch HIP events, ~5 us each); "persistent"
- * (default -1 = auto: off while skew is on, else on for buffers of at most
- * 64 MiB; 1 on, 0 off): resident multi-super-step kernel for long runs on a
+ * (default -1 = auto: off where the skewed band stacks fill the CUs, else on
+ * for buffers of at most 64 MiB; 1 on, 0 off): resident multi-super-step kernel for long runs on a
  * whole torus (never in a multi-rank ring);
  * "persist_depth" (default 0 = tb_depth): turns per super-step;
  * "persist_half" (default 1): a remainder of half a super-step runs as the

@@ -189,3 +189,82 @@ def test_skew_every_launch_counts(coracle):
             assert b.alive_count() == (int((cur == 255).sum()), 20 * (t + 1))
         assert b.perf()["skew_launches"] == 5
         assert np.array_equal(b.snapshot_bytes(), cur)
+
+
+# ------------------------------------------------- half-wave tiles (option "skew_half")
+@pytest.mark.parametrize("depth", [20, 16])
+@pytest.mark.parametrize("W,H", [(16384, 1000), (5120, 2222), (3072, 1502), (4160, 3000), (2048, 818)])
+@pytest.mark.parametrize("tx", [0, 2])
+def test_skew_half_tiles_match_oracle(coracle, depth, W, H, tx):
+    """Half-wave tiles: lanes 0-31 and 32-63 of a wave are two 30-lane tiles
+    of one tile column, the upper one H / 2 rows further down (the same band
+    of a second stack); torus seam, narrow and ragged tile columns."""
+    board = coracle.fill_random(W, H, 0x5EED0041 + W + H + depth)
+    turns = 2 * depth + 5
+    want = coracle.run(board, turns)
+    got, p = run_skew(board, turns, depth, 2, skew_half=1, skew_tx=tx)
+    assert p["skew_half_launches"] >= 2
+    assert np.array_equal(got, want)
+
+
+def test_skew_half_tiles_need_even_rows(coracle):
+    """An odd number of rows cannot split into two equal halves: full tiles."""
+    board = coracle.fill_random(16384, 1001, 0x5EED0042)
+    want = coracle.run(board, 43)
+    got, p = run_skew(board, 43, 20, 2, skew_half=1)
+    assert p["skew_launches"] >= 2 and p["skew_half_launches"] == 0
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("W,H", [(16384, 3000), (5120, 2048)])
+def test_skew_half_tiles_rccl_ring_and_strips(coracle, W, H):
+    """Half-wave tiles on a strip's extended rows: a one-rank RCCL ring and
+    three in-process strips."""
+    board = coracle.fill_random(W, H, 0x5EED0043 + W)
+    turns = 130
+    want = coracle.run(board, turns)
+    with golhip.Board(W, H) as b:
+        b.comm_init(golhip.unique_id(), 1, 0)
+        b.set_option("force_halo", 1)
+        b.set_option("skew", 2)
+        b.set_option("skew_half", 1)
+        b.set_option("wpl", 2)  # (5120 wide would plan one word per lane)
+        b.load_bytes(board)
+        b.step(turns)
+        assert b.perf()["skew_half_launches"] >= 1
+        assert np.array_equal(b.snapshot_bytes(), want)
+    bounds = [0, H // 3 * 1 // 2 * 2, 2 * H // 3 // 2 * 2, H]
+    strips = [golhip.Board(W, H, row0=bounds[i], rows=bounds[i + 1] - bounds[i]) for i in range(3)]
+    try:
+        for i, s in enumerate(strips):
+            s.set_option("skew", 2)
+            s.set_option("skew_half", 1)
+            s.set_option("wpl", 2)
+            s.load_bytes(board[bounds[i]:bounds[i + 1]])
+        golhip.group_step(strips, turns)
+        assert sum(s.perf()["skew_half_launches"] for s in strips) >= 1
+        got = np.concatenate([s.snapshot_bytes() for s in strips])
+        assert np.array_equal(got, want)
+    finally:
+        for s in strips:
+            s.close()
+
+
+def test_default_plans_by_board_size():
+    """The default plan: half-wave tiles at 16384^2 (configs[1]: 4.5 instead
+    of 5 waves a row), full tiles at 65536^2, and the resident kernel for tori
+    whose K1w stacks would not fill the CUs (8192^2)."""
+    with golhip.Board(16384, 16384) as b:
+        b.fill_random(0x5EED0001)
+        b.step(40)
+        p = b.perf()
+        assert p["skew_launches"] == 2 and p["skew_half_launches"] == 2
+    with golhip.Board(65536, 4096) as b:
+        b.fill_random(0x5EED0002)
+        b.step(20)
+        assert b.perf()["skew_half_launches"] == 0
+    with golhip.Board(8192, 8192) as b:
+        b.fill_random(0x5EED0003)
+        b.step(64)
+        p = b.perf()
+        assert p["persist_launches"] >= 1 and p["skew_launches"] == 0
