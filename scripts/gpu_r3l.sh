@@ -1,17 +1,8 @@
+# GPU tests from test_gpu_parity.py on (the files before it passed in r3k)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-out=$GRAFT_REPO_ROOT/gpurun_out/${1:-r3l}
+out=gpurun_out/${1:-r3l}
 mkdir -p $out
-L=game-of-life-distributed_amd/golhip
-for rep in 1 2; do
-for lib in libgolhip.so libgolhip_8416.so libgolhip_020c.so; do
-  GOLHIP_LIB=$L/$lib timeout -k 10 200 python -u scripts/sweep_opts.py --no-timing --reps 1 --turns 2000 --cases "262144x32768r,65536x65536,65536x8192r,16384x16384" --sets "skew=1" >> $out/ab.txt 2> $out/ab.err || { tail $out/ab.err; exit 1; }
-done
-done
-grep '"gcups"' $out/ab.txt | python3 -c "
-import sys,json,collections
-b=collections.defaultdict(list)
-for l in sys.stdin:
-    d=json.loads(l); b[(d['case'],d['lib'])].append(d['gcups'])
-for k in sorted(b): print(k, b[k])
-"
+PYT="python -u -m pytest -v --timeout 200 --timeout-method thread -p no:cacheprovider"
+timeout -k 10 1000 $PYT tests/test_gpu_skew.py tests/test_gpu_split.py -m gpu -x > $out/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -40 $out/pytest_gpu.log; exit 1; }
+tail -3 $out/pytest_gpu.log

@@ -252,9 +252,11 @@ def test_persistent_timeout_one_rank_ring(coracle, timeout_us):
     resident launch that gives up waiting (1 us bound) restores the board and
     re-runs the step on per-launch kernels, exchanges included (safe with no
     other rank; multi-rank rings never run the resident kernel)."""
-    N, depth = 2048, 16
+    # depth 8: one resident launch of 16 super-steps per exchange, i.e. 15
+    # neighbour waits per workgroup, each of which the 1 us bound can cut
+    N, depth = 4096, 8
     board = coracle.fill_random(N, N // 2, 0x5EED0024)
-    turns = 5 * depth + 7
+    turns = 16 * depth + 7
     want = coracle.run(board, turns)
     with golhip.Board(N, N // 2) as b:
         b.comm_init(golhip.unique_id(), 1, 0)

@@ -126,6 +126,7 @@ def test_overlap_rccl_ring_one_rank(coracle, depth, wpl, W, H, turns):
     with golhip.Board(W, H) as b:
         b.comm_init(golhip.unique_id(), 1, 0)
         b.set_option("force_halo", 1)
+        b.set_option("persistent", 0)  # (overlap splits per-launch rounds; small rings may run K1p)
         b.set_option("overlap", 1)
         b.set_option("wpl", wpl)
         b.set_tb_depth(depth)
