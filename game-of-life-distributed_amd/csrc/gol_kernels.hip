@@ -1847,8 +1847,8 @@ static hipError_t dispatch_skew(int depth, int wpl, bool half, F &&f) {
     if (!half && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP>);
 #define GOL_HCASE(D, WP) \
     if (half && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP, true>);
-    GOL_WCASE(8, 2) GOL_WCASE(12, 2) GOL_WCASE(16, 2) GOL_WCASE(20, 2) GOL_WCASE(8, 4) GOL_WCASE(9, 4)
-    GOL_WCASE(16, 1) GOL_WCASE(32, 1)
+    GOL_WCASE(8, 2) GOL_WCASE(12, 2) GOL_WCASE(16, 2) GOL_WCASE(20, 2) GOL_WCASE(6, 4) GOL_WCASE(8, 4)
+    GOL_WCASE(9, 4) GOL_WCASE(16, 1) GOL_WCASE(32, 1)
     GOL_HCASE(16, 2) GOL_HCASE(20, 2)
 #undef GOL_WCASE
 #undef GOL_HCASE

@@ -13,6 +13,9 @@ for step in "$@"; do
     fullsize)
       timeout -k 10 600 $PYT tests/test_gpu_fullsize.py -m gpu -x > $out/pytest_fullsize.log 2>&1 || { echo "fullsize tests failed"; tail -40 $out/pytest_fullsize.log; exit 1; }
       tail -3 $out/pytest_fullsize.log ;;
+    skew64)
+      timeout -k 10 300 $PYT tests/test_gpu_skew.py -m gpu -x -k "6-4" > $out/pytest_skew64.log 2>&1 || { echo "skew (6,4) tests failed"; tail -40 $out/pytest_skew64.log; exit 1; }
+      tail -2 $out/pytest_skew64.log ;;
     full)
       timeout -k 10 900 $PYT tests -m gpu -x > $out/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; tail -40 $out/pytest_gpu.log; exit 1; }
       tail -3 $out/pytest_gpu.log ;;

@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 
 golhip = pytest.importorskip("golhip")
 
-SKEW = [(8, 2), (12, 2), (16, 2), (20, 2), (8, 4), (9, 4), (16, 1), (32, 1)]
+SKEW = [(8, 2), (12, 2), (16, 2), (20, 2), (6, 4), (8, 4), (9, 4), (16, 1), (32, 1)]
 
 
 @pytest.fixture(scope="module")
