@@ -290,7 +290,9 @@ int largest_depth(int64_t want) {
 // order: 100 turns at cap 16 run as 4 x 16 + 3 x 12, not 6 x 16 + 4 (a
 // 4-turn launch costs about as much as a 16-turn one on a large board:
 // 65536^2 x 100 turns ran at 108 vs 122 TCUPS kernel-only).  Far from the
-// end the run is `cap` turns; the last 3-4 caps are planned exactly.
+// end the run is `cap` turns; the last 12-13 caps are planned exactly
+// (262144^2 x 100 turns at cap 9: 4 x 9 + 8 x 8, not 8 x 9 + 2 x 8 + 2 x 6,
+// which a plan of only the last 3-4 caps found).
 struct DepthRun {
     int d;
     int64_t n;
@@ -298,8 +300,8 @@ struct DepthRun {
 DepthRun depth_plan(int cap, int64_t left) {
     const int M = cap == 9 ? 9 : largest_depth(std::max(1, cap));  // 9: quads (depth_cap)
     if (left <= 0) return {M, 0};
-    const int64_t head = std::max<int64_t>(0, left / M - 3);  // launches of M before the planned tail
-    const int t = (int)(left - head * M);                     // < 4 M <= 128
+    const int64_t head = std::max<int64_t>(0, left / M - 12);  // launches of M before the planned tail
+    const int t = (int)(left - head * M);                      // < 13 M <= 416
     // best[v] = (launches, -smallest launch) for v turns; pick[v] = first depth
     std::vector<int> nl(t + 1, INT_MAX), mn(t + 1, 0), pick(t + 1, 0);
     nl[0] = 0;

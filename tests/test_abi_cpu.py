@@ -84,7 +84,7 @@ def test_halo_schedule(rows, tb, left, want):
     (16384, 16, 20, [(12, 1), (8, 1)]),
     (16384, 16, 7, [(6, 1), (1, 1)]),
     (65536, 8, 100, [(8, 11), (6, 2)]),              # quads: no 4-turn tail
-    (65536, 9, 100, [(9, 8), (8, 2), (6, 2)]),       # quads' own depth 9: 12 launches, not 13
+    (65536, 9, 100, [(9, 4), (8, 8)]),               # quads' own depth 9: 12 launches, the smallest 8
     (16384, 16, 36, [(12, 3)]),
 ])
 def test_halo_schedule_sequence(rows, tb, left, want):
