@@ -129,7 +129,14 @@ def test_fastcpu_comparator_matches_golden_boards(fixtures, coracle, n, t):
 @pytest.mark.parametrize("W,H,turns,threads", [(64, 3, 7, 1), (128, 37, 13, 4), (1024, 99, 20, 8), (192, 200, 33, 5)])
 def test_fastcpu_comparator_matches_oracle(coracle, W, H, turns, threads):
     b = coracle.fill_random(W, H, 0x5EED0042 + W)
-    assert np.array_equal(coracle.run_fast(b, turns, threads), coracle.run(b, turns))
+    assert np.array_equal(coracle.run_fast(b, turns, threads), coracle.run_exact(b, turns))
+
+
+def test_oracle_run_switches_to_the_comparator_on_large_cases(coracle):
+    """run() answers large cases with the comparator: same board as the per-cell oracle."""
+    b = coracle.fill_random(2048, 1000, 0x5EED0044)
+    assert 2048 * 1000 * 10 >= coracle.FAST_CELL_UPDATES
+    assert np.array_equal(coracle.run(b, 10), coracle.run_exact(b, 10))
 
 
 # ------------------------------------------- full-size fixture generator (make_fullsize.py)
