@@ -115,8 +115,9 @@ def test_skew_rccl_ring_one_rank(coracle, depth, wpl, W, H):
         assert b.alive_count() == (int((want == 255).sum()), turns)
 
 
-@pytest.mark.parametrize("depth,wpl", [(20, 2), (9, 4), (16, 1), (8, 2)])
-@pytest.mark.parametrize("W,H,turns", [(4096, 1500, 300), (2048, 4096, 257), (8192, 1000, 123)])
+@pytest.mark.parametrize("depth,wpl,W,H,turns", [(20, 2, 4096, 1500, 300), (9, 4, 4096, 1500, 300),
+                                                  (16, 1, 2048, 4096, 257), (8, 2, 2048, 4096, 257),
+                                                  (20, 2, 8192, 1000, 123), (9, 4, 8192, 1000, 123)])
 def test_overlap_rccl_ring_one_rank(coracle, depth, wpl, W, H, turns):
     """Option "overlap": the last launch of each exchange round in three
     parts (boundary rows on a side stream, then the next exchange there;
