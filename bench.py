@@ -501,6 +501,10 @@ def main():
             "rows_per_wave": perf["rows_per_wave"],
             "words_per_lane": perf["words_per_lane"],
             "parallelism": f"row strips x{world} (RCCL halo ring)" if world > 1 else "single GPU torus",
+            # halo traffic of this rank over the timed steps (deep halos: one
+            # exchange of k x depth rows feeds k launches)
+            "halo_exchanges": perf.get("halo_exchanges", 0),
+            "halo_bytes_per_step": perf["halo_bytes"] // max(1, a.steps),
         },
         "roofline": roofline_block(perf, W, rows, N, a.pmc, region_ms),
         "final_alive": alive_end,
