@@ -364,6 +364,16 @@ def events_main(a) -> None:
                      "note": "one turn + its list per launch; the 5120^2 board is cache-resident and the launch is "
                              "bound by its grid-wide predecessor sum, not by bandwidth (DESIGN 7.3)"},
     }
+    try:  # HBM bytes of K5 from the PMC passes of this command (scripts/pmc_bench.sh ... 5120)
+        with open(a.pmc) as f:
+            rec = json.load(f).get(f"{N}:gol_flip_turn_kernel")
+    except (OSError, ValueError):
+        rec = None
+    if rec and rec.get("hbm_bytes_per_launch") and kus > 0:
+        out["roofline"]["traffic"] = rec["hbm_bytes_per_launch"]
+        out["roofline"]["hbm"] = {"achieved_GBps": round(rec["hbm_bytes_per_launch"] / (kus * 1e-6) / 1e9, 1),
+                                  "peak_GBps": HBM_PEAK_GBS, "source": os.path.relpath(a.pmc, ROOT),
+                                  "note": "FETCH_SIZE x2 + WRITE_SIZE; the entries go to page-locked host memory"}
     if not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(N, wl["seed"], a.cpu_seconds)
         out["cpu_baseline"]["config0"] = cpu_config0()

@@ -22,7 +22,8 @@ import sys
 
 src, dst = sys.argv[1], sys.argv[2]
 out = json.load(open(dst)) if os.path.exists(dst) else {}
-FAMILIES = ("gol_persist_kernel", "gol_tb_pair_kernel", "gol_split_pair_kernel", "gol_split_tri_kernel", "gol_skew_kernel")
+FAMILIES = ("gol_persist_kernel", "gol_tb_pair_kernel", "gol_split_pair_kernel", "gol_split_tri_kernel", "gol_skew_kernel",
+            "gol_flip_turn_kernel")
 
 for d in sorted(glob.glob(os.path.join(src, "pmc_*_*"))):
     if not os.path.isdir(d):
@@ -39,14 +40,14 @@ for d in sorted(glob.glob(os.path.join(src, "pmc_*_*"))):
                 bench = json.loads(line)
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(path)):
-            fam = next((f for f in FAMILIES if f + "<" in row["Kernel_Name"]), None)
+            fam = next((f for f in FAMILIES if f + "<" in row["Kernel_Name"] or f + "(" in row["Kernel_Name"]), None)
             if fam is None:
                 continue
             rec = out.setdefault(f"{wl}:{fam}", {"_vals": {}, "_durs": []})
             rec.setdefault("_vals", {}).setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
             rec.setdefault("_durs", []).append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
             if bench and fam in bench["roofline"]["kernel"]:
-                rec["turns_per_launch"] = bench["roofline"]["turns_per_launch"]
+                rec["turns_per_launch"] = bench["roofline"].get("turns_per_launch", 1)
                 rec["bench_kernel"] = bench["roofline"]["kernel"]
 
 for key, rec in list(out.items()):
