@@ -190,8 +190,9 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str, 
     engine's stream around the whole timed region (region_ms): the average
     launch = region / launches, kernel boundaries included (per-launch events
     cost ~5 us a launch themselves: 16384^2 ran 66 vs 74 TCUPS with and
-    without them, profiles/r3d), so rocprofv3's per-kernel average is that
-    minus the ~2 us gap between dependent launches.
+    without them in an earlier round-3 A/B), so rocprofv3's per-kernel
+    average is that minus the small gap between dependent launches
+    (profiles/r3final: 65536^2 671.9 us rocprof vs 670.9 us here).
 
     The kernels are VALU-issue-bound: a launch fuses 8-16
     turns per board pass, so HBM moves ~1/D of the single-pass bytes.  `frac`
