@@ -86,6 +86,11 @@ def parse():
     ap.add_argument("--option", action="append", default=[], help="engine option key=value (A/B runs)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--launch-timeout", type=float, default=1500.0,
+                    help="--gpus N > 1 without a launcher: end the ranks after this long (s)")
+    ap.add_argument("--stage-timeout", type=float, default=300.0,
+                    help="multi-rank runs: the longest one stage (comm init, parity step, warmup, timed "
+                         "steps) may take before the watchdog ends the rank with a JSON error line")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_bench.json"),
                     help="rocprofv3 --pmc summary of this bench command (scripts/pmc_bench.py)")
     return ap.parse_args()
@@ -383,17 +388,152 @@ def events_main(a) -> None:
         sys.exit(1)
 
 
+def error_line(a, msg: str, **extra) -> None:
+    """The one JSON line of a run that could not measure: value null, the
+    reason in `error`, exit status non-zero (the caller exits)."""
+    out = {"metric": METRIC, "value": None, "unit": "GCUPS", "n_gpus": a.gpus, "steps": a.steps,
+           "warmup": a.warmup, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+           "error": msg, "config": {"workload": WORKLOADS[a.workload]["desc"]}}
+    out.update(extra)
+    print(json.dumps(out), flush=True)
+
+
+class Watchdog:
+    """Bounds every multi-rank stage (RCCL comm init, parity step, warmup,
+    timed steps): a stage that does not finish in time prints a JSON error
+    line naming the rank and the stage and ends the process with status 3,
+    instead of hanging until an outside timeout (a lost peer blocks
+    ncclCommInitRank and every exchange forever)."""
+
+    def __init__(self, a, rank: int):
+        import threading
+        self.a, self.rank = a, rank
+        self.stage, self.deadline = None, None
+        self._lock = threading.Lock()
+        t = threading.Thread(target=self._run, daemon=True)
+        t.start()
+
+    def arm(self, stage: str, seconds: float) -> None:
+        with self._lock:
+            self.stage, self.deadline = stage, time.monotonic() + seconds
+
+    def disarm(self) -> None:
+        with self._lock:
+            self.stage, self.deadline = None, None
+
+    def _run(self) -> None:
+        while True:
+            time.sleep(0.5)
+            with self._lock:
+                late = self.deadline is not None and time.monotonic() > self.deadline
+                stage = self.stage
+            if late:
+                msg = f"rank {self.rank}: stage '{stage}' did not finish in time (watchdog)"
+                print(msg, file=sys.stderr, flush=True)
+                if self.rank == 0:
+                    error_line(self.a, msg, rank=self.rank, stage=stage)
+                os._exit(3)
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a, cmd: list | None = None, n_devices: int | None = None) -> int:
+    """`--gpus N > 1` without a launcher (no WORLD_SIZE): start the N rank
+    processes here, torchrun-style (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR=127.0.0.1 / MASTER_PORT in each child's environment), before
+    this process touches the GPU (torch.cuda.device_count() does not
+    initialise it on this image).  Rank 0's stdout is relayed line by line;
+    the first rank to fail ends the others and the launcher prints a JSON
+    error line if rank 0 printed none.  Returns the exit status.  (`cmd` /
+    `n_devices` replace the child command and the device count in the CPU
+    tests of the launcher.)"""
+    import subprocess
+    import threading
+
+    if n_devices is None:
+        import torch
+        n_devices = torch.cuda.device_count()
+    n = n_devices
+    if n < a.gpus:
+        error_line(a, f"{n} devices < {a.gpus} ranks: --gpus {a.gpus} needs {a.gpus} visible GPUs", devices=n)
+        return 2
+    port = free_port()
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, GOL_BENCH_SELF_LAUNCH="1", RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                   LOCAL_WORLD_SIZE=str(a.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd or [sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True,
+                                      start_new_session=True))
+    printed = []
+
+    def relay():
+        for line in procs[0].stdout:
+            print(line, end="", flush=True)
+            if line.lstrip().startswith("{") and '"metric"' in line:
+                printed.append(line)
+
+    th = threading.Thread(target=relay, daemon=True)
+    th.start()
+    deadline = time.monotonic() + a.launch_timeout
+    failed = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            failed = f"rank {bad[0][0]} exited with status {bad[0][1]}"
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.monotonic() > deadline:
+            failed = f"ranks still running after --launch-timeout {a.launch_timeout:.0f} s"
+            break
+        time.sleep(0.2)
+    if failed:
+        import signal
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except OSError:
+                    pass
+        t_kill = time.monotonic() + 10
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_kill - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except OSError:
+                    pass
+                p.wait()
+    th.join(timeout=5)
+    if failed:
+        if not printed:
+            error_line(a, failed, rank_status=[p.returncode for p in procs])
+        return max(1, max(abs(p.returncode or 0) for p in procs))
+    return 0
+
+
 def main():
     a = parse()
     if a.workload == 5120:
-        if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+        if int(os.environ.get("WORLD_SIZE", "1")) != 1 or a.gpus != 1:
             raise SystemExit("--workload 5120 (the event stream) runs on one GPU")
         return events_main(a)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+        error_line(a, f"--gpus {a.gpus} but WORLD_SIZE={world}")
+        sys.exit(2)
     wl = WORKLOADS[a.workload]
     N = a.workload
     if N % world:
@@ -403,11 +543,19 @@ def main():
     row0 = rank * rows
     tps = a.turns_per_step or wl["turns"]
 
+    wd = Watchdog(a, rank) if world > 1 else None
+
+    def stage(name: str) -> None:  # bound the next multi-rank stage
+        if wd is not None:
+            wd.arm(name, a.stage_timeout)
+            print(f"[rank {rank}/{world}] {name}", file=sys.stderr, flush=True)
+
     import torch
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
+        stage("process group init (RCCL)")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     board = golhip.Board(W, H, device=local, row0=row0, rows=rows) if world > 1 \
@@ -417,10 +565,15 @@ def main():
     for kv in a.option:
         k, v = kv.split("=")
         board.set_option(k, int(v))
+    comm = None
     if world > 1:
+        stage("golhip_comm_init (ncclCommInitRank + strip-row allreduce)")
         uid = [golhip.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         board.comm_init(uid[0], world, rank)
+        comm = board.comm_info()
+        if comm["nranks"] != world or comm["rank"] != rank:
+            raise SystemExit(f"RCCL ring reports rank {comm['rank']} of {comm['nranks']}, expected {rank} of {world}")
     board.fill_random(wl["seed"])
 
     def barrier():
@@ -437,6 +590,7 @@ def main():
         return int(t.item()) % (1 << 64)
 
     # warmup step 1 from the fresh board = the parity run
+    stage("parity step (first warmup step, halo exchanges)")
     t_w = time.perf_counter()
     board.step(tps)
     board.sync()
@@ -463,9 +617,11 @@ def main():
             x = torch.tensor([extra], dtype=torch.int64, device="cuda")
             dist.broadcast(x, src=0)
             extra = int(x.item())
+    stage("warmup steps")
     for _ in range(extra):
         board.step(tps)
     barrier()
+    stage("timed steps")
     board.perf_reset()
     engine_stream = torch.cuda.ExternalStream(board.stream())
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -477,6 +633,7 @@ def main():
     board.sync()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    dt_rank = dt
     region_ms = ev0.elapsed_time(ev1)
     if dist is not None:
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
@@ -485,6 +642,15 @@ def main():
         dist.barrier()
     perf = board.perf()
     alive_end, at_turn = board.alive_count(global_sum=world > 1)
+    ranks = None
+    if dist is not None:  # every rank's status, as the library sees it
+        me = {"rank": rank, "row0": row0, "rows": rows, "comm": comm, "seconds": round(dt_rank, 6),
+              "region_ms": round(region_ms, 3), "launches": perf["step_launches"] + perf["persist_launches"],
+              "halo_exchanges": perf.get("halo_exchanges", 0), "halo_bytes": perf["halo_bytes"]}
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
+    if wd is not None:
+        wd.arm("shutdown", 120.0)
 
     gcups = W * H * tps * a.steps / dt / 1e9
     out = {
@@ -516,6 +682,10 @@ def main():
             # exchange of k x depth rows feeds k launches)
             "halo_exchanges": perf.get("halo_exchanges", 0),
             "halo_bytes_per_step": perf["halo_bytes"] // max(1, a.steps),
+            "launcher": ("self (bench.py --gpus N)" if os.environ.get("GOL_BENCH_SELF_LAUNCH") else
+                         "torch.distributed.run" if world > 1 else None),
+            "comm": comm,
+            "ranks": ranks,
         },
         "roofline": roofline_block(perf, W, rows, N, a.pmc, region_ms),
         "final_alive": alive_end,

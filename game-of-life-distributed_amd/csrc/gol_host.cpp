@@ -88,6 +88,28 @@ int env_int(const char *name, int dflt) {
 // GOL_STRIPS) stepped together by golhip_group_step_ex.  Every side channel
 // of the strips is gathered in strip order, which is the board's row-major
 // order: alive lists and flip lists concatenate, counts add up.
+// Page-locked flip-list buffer the engine's flip kernel writes directly
+// (golhip_host_alloc): 4-byte cell indices y * W + x.
+struct FlipBuffer {
+    uint32_t *p = nullptr;
+    uint64_t cap = 0;  // entries
+    void grow(uint64_t n) { grow_keep(n, 0); }
+    // at least n entries (doubling), the first `keep` entries preserved
+    void grow_keep(uint64_t n, uint64_t keep) {
+        if (n <= cap) return;
+        if (keep) n = std::max<uint64_t>(n, 2 * cap);
+        void *q = nullptr;
+        check(golhip_host_alloc(n * sizeof(uint32_t), &q));
+        if (keep) memcpy(q, p, keep * sizeof(uint32_t));
+        if (p) golhip_host_free(p);
+        p = static_cast<uint32_t *>(q);
+        cap = n;
+    }
+    ~FlipBuffer() {
+        if (p) golhip_host_free(p);
+    }
+};
+
 struct Engine {
     std::vector<golhip_t> hs;
     std::vector<int64_t> row0;
@@ -168,31 +190,27 @@ struct Engine {
     // Up to `want` turns with every turn's flip list as cell indices y * W + x
     // (golhip_flip_stream's contract: stops before a turn that does not fit;
     // GOLHIP_ERANGE with *n = what the first turn needs).  Strips: one turn a
-    // group step, each strip's list of that turn, in strip order.
-    int flip_stream(int64_t want, uint32_t *buf, uint64_t cap, uint64_t *counts, int64_t *done, uint64_t *n) {
-        if (one()) return golhip_flip_stream(hs[0], want, GOLHIP_FLIPS_INDEX, buf, cap, counts, done, n);
+    // group step; each strip's list of that turn is sized after the step
+    // (golhip_flips with cap 0) and the buffer grown to fit before the copy,
+    // so every turn runs and the buffer holds only what the lists need.
+    int flip_stream(int64_t want, FlipBuffer &fb, uint64_t *counts, int64_t *done, uint64_t *n) {
+        if (one()) return golhip_flip_stream(hs[0], want, GOLHIP_FLIPS_INDEX, fb.p, fb.cap, counts, done, n);
         *done = 0;
         *n = 0;
         std::vector<int32_t> xy;
-        const uint64_t most = (uint64_t)W * (uint64_t)H;  // a turn flips at most every cell
         for (int64_t t = 0; t < want; ++t) {
-            if (*n + most > cap) {  // the next turn might not fit: stop before it (nothing of it ran)
-                if (t > 0) break;
-                *n = most;
-                return GOLHIP_ERANGE;
-            }
             check(golhip_group_step_ex(hs.data(), (int32_t)hs.size(), 1, 1));
             uint64_t turn_n = 0;
             for (golhip_t h : hs) {
                 uint64_t k = 0;
                 int rc = golhip_flips(h, nullptr, 0, &k);
                 if (rc != GOLHIP_OK && rc != GOLHIP_ERANGE) check(rc);
-                xy.resize(2 * std::max<uint64_t>(k, 1));
+                if (k == 0) continue;
+                xy.resize(2 * k);
                 check(golhip_flips(h, xy.data(), k, &k));
-                for (uint64_t e = 0; e < k; ++e) {
-                    const uint64_t idx = (uint64_t)xy[2 * e + 1] * (uint64_t)W + (uint64_t)xy[2 * e];
-                    if (*n + turn_n + e < cap) buf[*n + turn_n + e] = (uint32_t)idx;
-                }
+                fb.grow_keep(*n + turn_n + k, *n + turn_n);
+                for (uint64_t e = 0; e < k; ++e)
+                    fb.p[*n + turn_n + e] = (uint32_t)((uint64_t)xy[2 * e + 1] * (uint64_t)W + (uint64_t)xy[2 * e]);
                 turn_n += k;
             }
             counts[t] = turn_n;
@@ -200,26 +218,6 @@ struct Engine {
             *done = t + 1;
         }
         return GOLHIP_OK;
-    }
-};
-
-// Page-locked flip-list buffer the engine's flip kernel writes directly
-// (golhip_host_alloc): 4-byte cell indices y * W + x.
-struct FlipBuffer {
-    uint32_t *p = nullptr;
-    uint64_t cap = 0;  // entries
-    void grow(uint64_t n) {
-        if (n <= cap) return;
-        if (p) golhip_host_free(p);
-        p = nullptr;
-        cap = 0;
-        void *q = nullptr;
-        check(golhip_host_alloc(n * sizeof(uint32_t), &q));
-        p = static_cast<uint32_t *>(q);
-        cap = n;
-    }
-    ~FlipBuffer() {
-        if (p) golhip_host_free(p);
     }
 };
 
@@ -408,10 +406,10 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
             {
                 std::lock_guard<std::mutex> g(mu);
                 if (opt.cell_events) {
-                    int rc = board.flip_stream(want, fb.p, fb.cap, counts.data(), &done, &n);
+                    int rc = board.flip_stream(want, fb, counts.data(), &done, &n);
                     if (rc == GOLHIP_ERANGE) {  // one turn needs more than the buffer: grow, nothing advanced
                         fb.grow(n);
-                        rc = board.flip_stream(want, fb.p, fb.cap, counts.data(), &done, &n);
+                        rc = board.flip_stream(want, fb, counts.data(), &done, &n);
                     }
                     check(rc);
                 } else {

@@ -190,4 +190,7 @@ int64_t flip_turn_blocks(int64_t nwords);
 hipError_t launch_flip_turn(const FlipTurnArgs &a, hipStream_t s);
 int flip_turn_blocks_per_cu(bool contig);
 
+// "NAME=value ..." of the build's tuning macros (golhip_build_info).
+const char *build_info();
+
 }  // namespace golk

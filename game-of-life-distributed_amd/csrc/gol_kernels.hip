@@ -23,6 +23,9 @@ namespace golk {
 #ifndef GOL_LOOP_PAD
 #define GOL_LOOP_PAD 0  // code-layout experiments: 4-byte s_nop pads ahead of the main loops (profiles/r2la)
 #endif
+#ifndef GOL_FILL_PHASES
+#define GOL_FILL_PHASES 4  // K1 fill phases: quarters (8: eighths, round-1 A/B, profiles/r1*)
+#endif
 
 // ---------------------------------------------------------------------------
 // bit-sliced helpers
@@ -413,8 +416,8 @@ template <int WPL>
 constexpr int pair_store() {
     return GOL_PAIR_STORE >= 0 ? GOL_PAIR_STORE : (WPL == 4 ? kStoreDeferred : kStoreBufAfterLoads);
 }
-#ifndef GOL_SPLIT_NOHOOK
-#define GOL_SPLIT_NOHOOK 0
+#ifdef GOL_SPLIT_NOHOOK
+#error "GOL_SPLIT_NOHOOK (round-2 timing experiment, wrong results) was removed"
 #endif
 #ifndef GOL_PAIR_G2
 #define GOL_PAIR_G2 0
@@ -989,11 +992,7 @@ __device__ __forceinline__ uint32_t stream_split(const SplitArgs &p, int region,
             const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
             __builtin_amdgcn_sched_barrier(0);
             Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
-#if GOL_SPLIT_NOHOOK  // timing experiments only: no start exports (wrong results)
-            push_group<D, A, WPL>(y0, y1, y2, h0, h1, cc);
-#else
             push_group_exp<D, A, WPL>(y0, y1, y2, h0, h1, cc, ii, hook);
-#endif
             if constexpr (A == D) {
                 emit(y0, ii - 2 * D);
                 emit(y1, ii + 1 - 2 * D);
@@ -2662,6 +2661,18 @@ hipError_t launch_compact_scatter(const uint32_t *a, const uint32_t *b, int64_t 
     hipLaunchKernelGGL(compact_scatter_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, b, nwords, Ww, row0, blk_off,
                        xy, cap, il);
     return hipGetLastError();
+}
+
+// The build's tuning macros (A/B builds override them; the product build
+// uses the defaults, tests/test_abi_cpu.py::test_product_build_macros).
+#define GOL_STR2(x) #x
+#define GOL_STR(x) GOL_STR2(x)
+const char *build_info() {
+    return "GOL_LOOP_PAD=" GOL_STR(GOL_LOOP_PAD) " GOL_PARITY_FIX=" GOL_STR(GOL_PARITY_FIX)
+           " GOL_PERSIST_STORE=" GOL_STR(GOL_PERSIST_STORE) " GOL_PAIR_STORE=" GOL_STR(GOL_PAIR_STORE)
+           " GOL_PAIR_G2=" GOL_STR(GOL_PAIR_G2) " GOL_FILL_PHASES=" GOL_STR(GOL_FILL_PHASES)
+           " GOL_SKEW_STORE_CPOL=" GOL_STR(GOL_SKEW_STORE_CPOL) " GOL_PERSIST_WG_COUNT=" GOL_STR(GOL_PERSIST_WG_COUNT)
+           " GOL_COMPACT_WPT=" GOL_STR(GOL_COMPACT_WPT);
 }
 
 }  // namespace golk

@@ -373,6 +373,9 @@ constexpr int64_t kPersistAutoMaxBytes = 64ll << 20;
 int wpl_per_launch(golhip_t h);
 bool skew_fills(golhip_t h);
 bool persist_on(golhip_t h) {
+    // a multi-rank ring never runs the resident kernel (try_persist_halo):
+    // plan words per lane and halos for the per-launch kernels that do run
+    if (h->comm && h->nranks > 1) return false;
     if (h->persistent >= 0) return h->persistent != 0;
     // round 3: K1w per launch wherever its stacks fill the CUs (16384^2: 82
     // vs 62 TCUPS); smaller boards keep the resident kernel (8192^2: 27.9
@@ -917,13 +920,27 @@ int check_persist(golhip_t h) {
     return GOLHIP_OK;
 }
 
-int sync_stream(golhip_t h) {
-    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+// Options whose results are wrong by design (they isolate a cost) need the
+// environment's explicit consent: GOLHIP_MEASUREMENT=1.
+bool measurement_env() {
+    const char *v = getenv("GOLHIP_MEASUREMENT");
+    return v && !strcmp(v, "1");
+}
+
+// After the stream has synchronised: the K1w spin-bound flag of the launches
+// it ran (reported by the call that ran them, then cleared).
+int take_skew_err(golhip_t h) {
     if (h->skew_err && *h->skew_err) {
         *h->skew_err = 0;
         return fail(GOLHIP_EHIP, "skewed-band step kernel: a band waited past its spin bound for the band below "
                                  "(board state is undefined)");
     }
+    return GOLHIP_OK;
+}
+
+int sync_stream(golhip_t h) {
+    HIP_OR_FAIL(hipStreamSynchronize(h->stream));
+    if (int rc = take_skew_err(h)) return rc;
     return check_persist(h);
 }
 
@@ -1413,6 +1430,8 @@ extern "C" {
 
 const char *golhip_version(void) { return "golhip 0.1 (gfx950)"; }
 
+const char *golhip_build_info(void) { return golk::build_info(); }
+
 const char *golhip_last_error(void) { return g_err.c_str(); }
 
 int golhip_device_count(int32_t *n) {
@@ -1605,6 +1624,9 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         // 1 no look-back, 2 no entries (measurement only: wrong lists); 4 report a
         // co-residency failure once (tests the ticket-order fallback; lists exact)
         if (value < 0 || value > 7) return fail(GOLHIP_EINVAL, "flip_debug %lld", (long long)value);
+        if ((value & 3) && !measurement_env())
+            return fail(GOLHIP_EINVAL, "flip_debug %lld gives wrong lists: measurement runs only (GOLHIP_MEASUREMENT=1)",
+                        (long long)value);
         h->flip_debug = (int)value;
         return GOLHIP_OK;
     }
@@ -1624,6 +1646,8 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         return GOLHIP_OK;
     }
     if (!strcmp(key, "halo_skip")) {  // measurement only: the halo rows go stale (wrong results)
+        if (value && !measurement_env())
+            return fail(GOLHIP_EINVAL, "halo_skip gives wrong results: measurement runs only (GOLHIP_MEASUREMENT=1)");
         h->halo_skip = value != 0;
         return GOLHIP_OK;
     }
@@ -1714,6 +1738,25 @@ int golhip_comm_init(golhip_t h, const uint8_t id[GOLHIP_UNIQUE_ID_BYTES], int32
     if (nr != ncclSuccess) return fail(GOLHIP_ERCCL, "ncclAllReduce(strip rows): %s", ncclGetErrorString(nr));
     if (e != hipSuccess) return fail(GOLHIP_EHIP, "strip rows: %s", hipGetErrorString(e));
     h->ring_rows = rows;
+    return GOLHIP_OK;
+}
+
+int golhip_comm_info(golhip_t h, int32_t *nranks, int32_t *rank, int32_t *ring_rows) {
+    if (int rc = check(h)) return rc;
+    if (!nranks || !rank || !ring_rows) return fail(GOLHIP_EINVAL, "null output");
+    std::lock_guard<std::mutex> g(h->mu);
+    if (!h->comm) {  // no ring: this handle alone
+        *nranks = 1;
+        *rank = 0;
+        *ring_rows = h->rows;
+        return GOLHIP_OK;
+    }
+    int n = 0, r = 0;
+    NCCL_OR_FAIL(ncclCommCount(h->comm, &n));
+    NCCL_OR_FAIL(ncclCommUserRank(h->comm, &r));
+    *nranks = n;
+    *rank = r;
+    *ring_rows = h->ring_rows;
     return GOLHIP_OK;
 }
 
@@ -1880,6 +1923,7 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     h->guarded = false;
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
     h->persist_pending = false;
+    if (int rc_ = take_skew_err(h)) return rc_;
     if (!h->h_err || !*h->h_err) return GOLHIP_OK;  // (a one-rank ring's guard may see no resident launch)
     *h->h_err = 0;
     h->persistent = 0;  // this device is shared: no more resident launches on this handle
@@ -2012,6 +2056,7 @@ int group_step_impl(golhip_t *hs, int32_t n, int64_t nturns, int32_t want_flips)
             HIP_RC(hipStreamSynchronize(hs[i]->stream));
             HIP_RC(hipEventDestroy(ready[i]));
         }
+        if (!rc) rc = take_skew_err(hs[i]);
     }
     return rc;
 }

@@ -98,6 +98,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     P = ctypes.POINTER
     sig = {
         "golhip_version": ([], ctypes.c_char_p),
+        "golhip_build_info": ([], ctypes.c_char_p),
         "golhip_last_error": ([], ctypes.c_char_p),
         "golhip_device_count": ([P(i32)], ctypes.c_int),
         "golhip_host_alloc": ([u64, P(ctypes.c_void_p)], ctypes.c_int),
@@ -112,6 +113,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "golhip_set_option": ([H, ctypes.c_char_p, i64], ctypes.c_int),
         "golhip_comm_unique_id": ([ctypes.c_char_p], ctypes.c_int),
         "golhip_comm_init": ([H, ctypes.c_char_p, i32, i32], ctypes.c_int),
+        "golhip_comm_info": ([H, P(i32), P(i32), P(i32)], ctypes.c_int),
         "golhip_group_step": ([P(H), i32, i64], ctypes.c_int),
         "golhip_group_step_ex": ([P(H), i32, i64, i32], ctypes.c_int),
         "golhip_halo_plan": ([i32, i32, i32, i32, i32, P(HaloPlan)], ctypes.c_int),
@@ -260,6 +262,12 @@ class Board:
 
     def comm_init(self, uid: bytes, nranks: int, rank: int) -> None:
         _check(load().golhip_comm_init(self._h, uid, nranks, rank))
+
+    def comm_info(self) -> dict:
+        """The ring as RCCL reports it (golhip_comm_info): nranks, rank, ring_rows."""
+        n, r, rows = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        _check(load().golhip_comm_info(self._h, ctypes.byref(n), ctypes.byref(r), ctypes.byref(rows)))
+        return {"nranks": n.value, "rank": r.value, "ring_rows": rows.value}
 
     # board I/O
     def load_bytes(self, cells: np.ndarray) -> None:

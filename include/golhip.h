@@ -96,6 +96,9 @@ typedef struct golhip_perf {
 
 /* ---- library ---------------------------------------------------------- */
 const char *golhip_version(void);
+/* The build's kernel tuning macros, "NAME=value ..." (A/B builds override
+ * them; the shipped library is built with the defaults).  Measurement. */
+const char *golhip_build_info(void);
 const char *golhip_last_error(void);
 int golhip_device_count(int32_t *n);
 
@@ -160,9 +163,10 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * "dummy_rows" (0 = all halo rows): rows that absorb masked stores;
  * "trace" (0): persistent-kernel diagnostics (golhip_persist_trace);
  * "persist_timeout_us" (default 1000000): how long a resident workgroup waits
- * for a neighbour before the launch is abandoned (whole torus: the board is
- * restored and the step re-run on per-launch kernels, persist_fallbacks; a
- * ring strip: the step fails with GOLHIP_EHIP);
+ * for a neighbour before the launch is abandoned (the board is restored and
+ * the step re-run on per-launch kernels, persist_fallbacks; the resident
+ * kernel runs only on a whole torus or a one-rank ring, never in a
+ * multi-rank ring);
  * "force_halo" (0): after golhip_comm_init with one rank, run a whole board
  * through the multi-GPU path as a one-rank RCCL ring (tests, measurement);
  * "halo_skip" (0): measurement only, post no halo exchange (the halo rows go
@@ -178,6 +182,11 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value);
  * golhip_comm_unique_id, broadcast by the caller. */
 int golhip_comm_unique_id(uint8_t id[GOLHIP_UNIQUE_ID_BYTES]);
 int golhip_comm_init(golhip_t h, const uint8_t id[GOLHIP_UNIQUE_ID_BYTES], int32_t nranks, int32_t rank);
+/* The ring as the communicator itself reports it (ncclCommCount /
+ * ncclCommUserRank) and the strip rows every rank plans from (the ring's
+ * smallest strip, agreed at golhip_comm_init).  Without a comm: 1, 0, and
+ * this handle's rows.  No reference counterpart (measurement). */
+int golhip_comm_info(golhip_t h, int32_t *nranks, int32_t *rank, int32_t *ring_rows);
 
 /* Steps n strips (ring order = array order) driven from one process; halos
  * move with peer/device copies.  Same semantics as golhip_step on each. */

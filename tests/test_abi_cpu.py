@@ -115,3 +115,26 @@ def test_halo_schedule_covers_turns(tb):
             r -= d
             g += 1
         assert len(seq) <= g
+
+
+def test_product_build_macros():
+    """The shipped libgolhip.so is built with the default tuning macros: no
+    A/B or layout-experiment build (GOL_LOOP_PAD etc.) is mistaken for the
+    product.  Macros that gave wrong results (GOL_SPLIT_NOHOOK) are gone:
+    defining one is a compile error."""
+    info = golhip.load().golhip_build_info().decode()
+    want = {"GOL_LOOP_PAD": "0", "GOL_PARITY_FIX": "1", "GOL_PERSIST_STORE": "6", "GOL_PAIR_STORE": "-1",
+            "GOL_PAIR_G2": "0", "GOL_FILL_PHASES": "4", "GOL_SKEW_STORE_CPOL": "16", "GOL_PERSIST_WG_COUNT": "1",
+            "GOL_COMPACT_WPT": "4"}
+    got = dict(kv.split("=", 1) for kv in info.split())
+    assert got == want, info
+
+
+def test_wrong_result_macro_is_a_compile_error(tmp_path):
+    import os
+    import subprocess
+    src = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(golhip.__file__)), "..", "csrc",
+                                        "gol_kernels.hip"))
+    p = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-fsyntax-only",
+                        "-DGOL_SPLIT_NOHOOK=1", src], capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0 and "GOL_SPLIT_NOHOOK" in p.stderr
