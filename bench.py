@@ -64,6 +64,9 @@ WORKLOADS = {
     262144: dict(key="c3", seed=0x5EED0003, turns=100, desc="configs[3]: 262144^2 random 25%, 100 turns a step"),
     5120: dict(key="c4", seed=0x5EED0005, turns=200,
                desc="configs[4]: 5120^2 random 25%, full CellFlipped stream, 200 turns a step from turn 2064"),
+    512: dict(key=None, seed=None, turns=100,
+              desc="configs[0]: images/512x512.pgm, 100 turns, Threads=8, end to end through gol.Run (host mirror): "
+                   "PGM in, every event drained, PGM out"),
 }
 FULLSIZE = os.path.join(ROOT, "tests", "golden", "fullsize.json")
 
@@ -84,6 +87,8 @@ def parse():
     ap.add_argument("--tb-depth", type=int, default=20)
     ap.add_argument("--rows-per-wave", type=int, default=0, help="0 = automatic")
     ap.add_argument("--option", action="append", default=[], help="engine option key=value (A/B runs)")
+    ap.add_argument("--e2e-turns", type=int, default=20,
+                    help="--workload 5120: turns of the end_to_end block through gol.Run (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--launch-timeout", type=float, default=1500.0,
@@ -380,12 +385,52 @@ def events_main(a) -> None:
         out["roofline"]["hbm"] = {"achieved_GBps": round(rec["hbm_bytes_per_launch"] / (kus * 1e-6) / 1e9, 1),
                                   "peak_GBps": HBM_PEAK_GBS, "source": os.path.relpath(a.pmc, ROOT),
                                   "note": "FETCH_SIZE x2 + WRITE_SIZE; the entries go to page-locked host memory"}
+    if a.e2e_turns > 0:
+        out["end_to_end"] = events_end_to_end(rec, a.e2e_turns)
+        parity["ok"] = parity["ok"] and out["end_to_end"]["parity"]
+        out["parity"] = parity["ok"]
     if not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(N, wl["seed"], a.cpu_seconds)
         out["cpu_baseline"]["config0"] = cpu_config0()
     print(json.dumps(out), flush=True)
     if parity["ok"] is False:
         sys.exit(1)
+
+
+def events_end_to_end(rec: dict, T: int) -> dict:
+    """configs[4] through the whole gol.Run mirror (SURVEY 8d end to end):
+    images/5120x5120.pgm of the fixture board, T turns, every CellFlipped
+    event (the initial alive cells, then each turn's flips) delivered through
+    an events channel of capacity 1000 (main.go:53) into main.go's headless
+    drain loop (golrun_drain, C++), then the final PGM and FinalTurnComplete.
+    Parity: per-turn CellFlipped counts and order-dependent digests equal
+    tests/golden/fullsize.json c4 (turns 1..T)."""
+    import tempfile
+
+    from oracle.oracle import COracle
+
+    N = rec["width"]
+    T = min(T, len(rec["flip_counts"]))
+    board = COracle().fill_random(N, N, rec["seed"])
+    with tempfile.TemporaryDirectory() as root:
+        write_images(root, {f"{N}x{N}": board})
+        del board
+        t0 = time.perf_counter()
+        r = golhip.Run(T, 8, N, N, root, events_cap=1000)
+        counts, last, final_alive, flips, digests = r.drain(T, N)
+        err = r.wait()
+        r.close()
+        dt = time.perf_counter() - t0
+    ok = (not err and last == T and [int(x) for x in flips] == rec["flip_counts"][:T]
+          and [f"{int(x):016x}" for x in digests] == rec["flip_digests"][:T]
+          and counts["CellFlipped"] == rec["initial_alive"] + sum(rec["flip_counts"][:T]))
+    return {"turns": T, "seconds": round(dt, 3), "turns_per_s": round(T / dt, 2),
+            "events_per_s": round(sum(counts.values()) / dt, 1), "events": counts, "parity": ok,
+            "fixture": f"tests/golden/fullsize.json c4 turns 1..{T}: per-turn counts + ordered digests",
+            "timed": "one whole gol.Run: PGM read, handle create + load, T turns with every CellFlipped through a "
+                     "capacity-1000 channel drained by main.go's loop (C++), PGM write, close",
+            "note": "the first turns of the random board flip 2.6-7.2 M cells each: the channel hand-off of "
+                    "every event (one at a time, as the reference's consumer) bounds this rate, not the GPU"}
 
 
 def error_line(a, msg: str, **extra) -> None:
@@ -520,8 +565,91 @@ def launch_ranks(a, cmd: list | None = None, n_devices: int | None = None) -> in
     return 0
 
 
+def write_images(root: str, names: dict) -> None:
+    """images/<name>.pgm under `root` (the reference's io.go reads them from images/)."""
+    from oracle.oracle import pgm_bytes
+    os.makedirs(os.path.join(root, "images"), exist_ok=True)
+    for name, board in names.items():
+        with open(os.path.join(root, "images", f"{name}.pgm"), "wb") as f:
+            f.write(pgm_bytes(board))
+
+
+def run_main(a) -> None:
+    """configs[0] end to end (SURVEY 8d: "... and end-to-end through gol.Run";
+    gol_test.go:15-47's shape): one step = one whole gol.Run(Params{Turns: 100,
+    Threads: 8, 512, 512}) through the C++ mirror (libgolhost.so over
+    libgolhip.so) -- images/512x512.pgm read, a GPU handle created and loaded,
+    100 turns with every CellFlipped and TurnComplete event delivered through
+    the events channel and drained (main.go's headless loop, golrun_drain),
+    out/512x512x100.pgm written, FinalTurnComplete, close.  Parity: the PGM's
+    SHA-256 equals check/images/512x512x100.pgm (tests/golden/manifest.json)
+    and the alive count equals check/alive.  `value` = cells x turns / wall
+    seconds of a whole Run; the CPU port of the reference's worker pool on the
+    same config sits beside it (cpu_baseline.config0)."""
+    import hashlib
+    import tempfile
+
+    from oracle.oracle import unpack_bits
+
+    with np.load(os.path.join(ROOT, "tests", "golden", "fixtures.npz"), allow_pickle=False) as z:
+        board = unpack_bits(z["image_512"], 512)
+        alive = z["alive_512"]
+    with open(os.path.join(ROOT, "tests", "golden", "manifest.json")) as f:
+        want_sha = json.load(f)["check_512x100"]["sha256"]
+    N, T = 512, a.turns_per_step or 100
+    with tempfile.TemporaryDirectory() as root:
+        write_images(root, {"512x512": board})
+
+        def one():
+            r = golhip.Run(T, 8, N, N, root)
+            counts, last, final_alive, _, _ = r.drain(0, 0)
+            err = r.wait()
+            r.close()
+            if err:
+                raise RuntimeError(err)
+            return counts, last, final_alive
+
+        for _ in range(max(1, a.warmup)):
+            one()
+        times, res = [], None
+        for _ in range(a.steps):
+            t0 = time.perf_counter()
+            res = one()
+            times.append(time.perf_counter() - t0)
+        counts, last, final_alive = res
+        with open(os.path.join(root, "out", f"{N}x{N}x{T}.pgm"), "rb") as f:
+            sha = hashlib.sha256(f.read()).hexdigest()
+    dt = sum(times)
+    ok = (T != 100) or (sha == want_sha and final_alive == int(alive[T]) and last == T)
+    out = {
+        "metric": METRIC, "value": round(N * N * T * a.steps / dt / 1e9, 4), "unit": "GCUPS", "n_gpus": 1,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "u32 bit-sliced (1 bit/cell) on the GPU; 0/255 bytes at the PGM boundary",
+        "data": "images/512x512.pgm (the reference's own input, tests/golden/fixtures.npz)",
+        "parity": ok,
+        "parity_check": {"pgm_sha256": sha[:16], "final_alive": final_alive, "last_turn": last,
+                         "fixture": "check/images/512x512x100.pgm (manifest sha256), check/alive/512x512.csv"},
+        "config": {"workload": WORKLOADS[512]["desc"], "board": [N, N], "turns_per_step": T, "threads": 8,
+                   "events": {k: v for k, v in counts.items()}, "parallelism": "single GPU torus",
+                   "timed": "whole gol.Run calls, wall clock: PGM read, handle create + load, turns, every event, "
+                            "PGM write, close"},
+        "runs_per_s": round(a.steps / dt, 2),
+        "ms_per_run_min": round(min(times) * 1e3, 3),
+    }
+    if not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_config0()
+    print(json.dumps(out), flush=True)
+    if not ok:
+        sys.exit(1)
+
+
 def main():
     a = parse()
+    if a.workload == 512:
+        if int(os.environ.get("WORLD_SIZE", "1")) != 1 or a.gpus != 1:
+            raise SystemExit("--workload 512 (configs[0] through gol.Run) runs on one GPU")
+        return run_main(a)
     if a.workload == 5120:
         if int(os.environ.get("WORLD_SIZE", "1")) != 1 or a.gpus != 1:
             raise SystemExit("--workload 5120 (the event stream) runs on one GPU")

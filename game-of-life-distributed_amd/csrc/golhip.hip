@@ -124,8 +124,8 @@ struct golhip {
     int skew_hcap = -1;             // option "skew_hcap": rows a stack's bottom band gives up (-1: 3 D / 4)
     int skew_prio = 0;              // option "skew_prio": s_setprio 1 for waves 4..7
     int skew_tx = 0;                // option "skew_tx": tiles per K1w workgroup (0: plan, 1 or 2)
-    int skew_half = 0;
-    int skew_nst = 0;               // option "skew_nst" (measurement): stacks per tile column (0: plan)              // option "skew_half": half-wave tiles (0: when fewer wave-rows, 1: whenever possible, -1: never)
+    int skew_half = 0;              // option "skew_half": half-wave tiles (0: when fewer wave-rows, 1: whenever possible, -1: never)
+    int skew_nst = 0;               // option "skew_nst" (measurement): stacks per tile column (0: plan)
     int skew_bpc[kNumDepths][6] = {};  // K1w workgroups per CU by (depth, wpl, half) (0: not queried)
     unsigned *skew_err = nullptr;      // host-mapped spin-bound flag of the K1w kernels
     unsigned *skew_err_dev = nullptr;

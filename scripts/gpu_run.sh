@@ -1,6 +1,6 @@
 # One parameterised GPU-box runner (replaces round 3's one-off gpu_r3*.sh).
 # usage: bash scripts/gpu_run.sh <tag> <step> [step ...]
-#   tests[:<pytest -k expr>]   GPU suite (or a subset), one process, per-test timeout
+#   tests[:<pytest -k expr>]   GPU suite (or a subset; commas stand for spaces), one process
 #   smoke                      __graft_entry__.smoke()
 #   bench[:<workload>]         bench.py line (default workload 65536) -> bench_<wl>.json
 #   trace[:<workload>]         rocprofv3 --kernel-trace --stats of that bench command
@@ -23,7 +23,7 @@ for st in "$@"; do
   case $name in
     tests)
       k=()
-      [ -n "$arg" ] && k=(-k "$arg")
+      [ -n "$arg" ] && k=(-k "${arg//,/ }")
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread "${k[@]}" \
         > $out/pytest.log 2>&1 || { tail -30 $out/pytest.log; exit 1; }
       tail -3 $out/pytest.log ;;

@@ -132,6 +132,16 @@ def test_fastcpu_comparator_matches_oracle(coracle, W, H, turns, threads):
     assert np.array_equal(coracle.run_fast(b, turns, threads), coracle.run_exact(b, turns))
 
 
+@pytest.mark.parametrize("W,H,turns", [(4096, 2048, 3), (65536, 96, 2), (128, 8192, 4)])
+def test_fastcpu_comparator_matches_oracle_wide_and_tall(coracle, W, H, turns):
+    """the large GPU parity cases compare against the bit-packed
+    comparator, so pin it to the per-cell oracle on boards as wide and as tall
+    as those cases (word and row wrap on a 4096 x 2048 board, the 65536-wide
+    rows of configs[2], an 8192-row column)."""
+    b = coracle.fill_random(W, H, 0x5EED0046 + W + H)
+    assert np.array_equal(coracle.run_fast(b, turns, 8), coracle.run_exact(b, turns))
+
+
 def test_oracle_run_switches_to_the_comparator_on_large_cases(coracle):
     """run() answers large cases with the comparator: same board as the per-cell oracle."""
     b = coracle.fill_random(2048, 1000, 0x5EED0044)
