@@ -13,6 +13,7 @@
 // Input:  <root>/images/<W>x<H>.pgm   Output: <root>/out/<W>x<H>x<T>.pgm (io.go:48, :95)
 #pragma once
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -68,6 +69,11 @@ struct Event {
 };
 
 // Go channel: capacity 0 is a rendezvous (send returns once received).
+// Go hands a value between goroutines in ~100-200 ns; a mutex + condition
+// variable per event costs two thread wake-ups (~5 us), which made a 512^2
+// x 100 run's 380k CellFlipped events take ~1 s.  So both sides spin briefly
+// on atomics (a waiting receiver is usually on another core) before they
+// sleep, and a side notifies the other only when it is asleep.
 template <typename T>
 class Chan {
    public:
@@ -75,39 +81,61 @@ class Chan {
     // Returns false if the channel is closed (Go would panic).
     bool send(T v) {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return closed_ || q_.size() < std::max<size_t>(cap_, 1); });
+        const size_t room = std::max<size_t>(cap_, 1);
+        if (!closed_ && q_.size() >= room) {
+            lk.unlock();
+            spin([&] { return closed_a_.load(std::memory_order_acquire) ||
+                              sent_a_.load(std::memory_order_acquire) -
+                                      received_a_.load(std::memory_order_acquire) < room; });
+            lk.lock();
+            ++send_sleepers_;
+            send_cv_.wait(lk, [&] { return closed_ || q_.size() < room; });
+            --send_sleepers_;
+        }
         if (closed_) return false;
         q_.push_back(std::move(v));
         const uint64_t ticket = ++sent_;
-        cv_.notify_all();
-        if (cap_ == 0) cv_.wait(lk, [&] { return received_ >= ticket || closed_; });
+        sent_a_.store(sent_, std::memory_order_release);
+        if (recv_sleepers_) recv_cv_.notify_one();
+        if (cap_ == 0) {
+            lk.unlock();
+            if (spin([&] { return received_a_.load(std::memory_order_acquire) >= ticket ||
+                                  closed_a_.load(std::memory_order_acquire); }))
+                return true;
+            lk.lock();
+            ++send_sleepers_;
+            send_cv_.wait(lk, [&] { return received_ >= ticket || closed_; });
+            --send_sleepers_;
+        }
         return true;
     }
     // Blocks; false once closed and drained (a `range` loop ends).
     bool recv(T &out) {
+        spin([&] { return closed_a_.load(std::memory_order_acquire) ||
+                          sent_a_.load(std::memory_order_acquire) != received_a_.load(std::memory_order_acquire); });
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return closed_ || !q_.empty(); });
+        if (!closed_ && q_.empty()) {
+            ++recv_sleepers_;
+            recv_cv_.wait(lk, [&] { return closed_ || !q_.empty(); });
+            --recv_sleepers_;
+        }
         if (q_.empty()) return false;
-        out = std::move(q_.front());
-        q_.pop_front();
-        ++received_;
-        cv_.notify_all();
+        take(out);
         return true;
     }
     // Non-blocking receive: 1 = got one, 0 = empty, -1 = closed and drained.
     int try_recv(T &out) {
         std::lock_guard<std::mutex> lk(mu_);
         if (q_.empty()) return closed_ ? -1 : 0;
-        out = std::move(q_.front());
-        q_.pop_front();
-        ++received_;
-        cv_.notify_all();
+        take(out);
         return 1;
     }
     void close() {
         std::lock_guard<std::mutex> lk(mu_);
         closed_ = true;
-        cv_.notify_all();
+        closed_a_.store(true, std::memory_order_release);
+        send_cv_.notify_all();
+        recv_cv_.notify_all();
     }
     bool closed() {
         std::lock_guard<std::mutex> lk(mu_);
@@ -115,12 +143,31 @@ class Chan {
     }
 
    private:
+    // Spin up to ~50 us for `ready`; true if it became true meanwhile.
+    template <typename F>
+    static bool spin(F &&ready) {
+        for (int i = 0; i < 2048; ++i) {
+            if (ready()) return true;
+            __builtin_ia32_pause();
+        }
+        return ready();
+    }
+    void take(T &out) {  // mu_ held, q_ not empty
+        out = std::move(q_.front());
+        q_.pop_front();
+        ++received_;
+        received_a_.store(received_, std::memory_order_release);
+        if (send_sleepers_) send_cv_.notify_all();  // senders wait on different tickets
+    }
     size_t cap_;
     std::mutex mu_;
-    std::condition_variable cv_;
+    std::condition_variable send_cv_, recv_cv_;
     std::deque<T> q_;
     bool closed_ = false;
     uint64_t sent_ = 0, received_ = 0;
+    int send_sleepers_ = 0, recv_sleepers_ = 0;
+    std::atomic<uint64_t> sent_a_{0}, received_a_{0};
+    std::atomic<bool> closed_a_{false};
 };
 
 // Host-mirror options beyond the Go API (all default to the reference's

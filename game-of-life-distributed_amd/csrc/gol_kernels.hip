@@ -1274,6 +1274,9 @@ __global__ __launch_bounds__(256) void gol_split_tri_kernel(SplitArgs p) {
 // generation D of [0, H) without wrapping the output; row strips: the
 // halo rows feed the top band's first D rows and the bottom band's drain.
 // ---------------------------------------------------------------------------
+#ifndef GOL_SKEW_PREFETCH
+#define GOL_SKEW_PREFETCH 1  // K1w main loop: load the rows 1 or 2 groups ahead
+#endif
 #ifndef GOL_SKEW_STORE_CPOL
 #define GOL_SKEW_STORE_CPOL 16  // K1w output stores sc1 (16384^2 +3.6 %, 8192-row strips +1.9 % in a round-3 A/B whose scratch data was not kept; 0 plain, 2 nt)
 #endif
@@ -1443,22 +1446,74 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
     // main: every stage on board rows (the bottom band of a stack to the end)
     const int kmain = S + (self ? 2 * D : 2 * SP::P(0));
     for (int i = 0; i < GOL_LOOP_PAD; ++i) asm volatile("s_nop 0");
-    for (; k < kmain; k += 3) {
-        const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
-        emit(q0, qoi);
-        emit(q1, qoi + 1);
-        emit(q2, qoi + 2);
-        __builtin_amdgcn_sched_barrier(0);
-        Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
-        push_group<D, D, WPL>(y0, y1, y2, h0, h1, cc);
-        q0 = y0;
-        q1 = y1;
-        q2 = y2;
-        qoi = k - 2 * D;
-        __builtin_amdgcn_sched_barrier(0);
-        x0 = vmov(n0);
-        x1 = vmov(n1);
-        x2 = vmov(n2);
+    if constexpr (GOL_SKEW_PREFETCH >= 2) {
+        // loads two groups ahead: each group's rows have two groups of compute
+        // to land.  Two groups a body with the two load sets alternating (a
+        // register copy of a pending load would wait for it).
+        // An odd group count runs its first group as the one-ahead body (no
+        // exit in the middle of the loop: it would cost conservative waits).
+        if ((((kmain - k) + 2) / 3) & 1) {
+            const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
+            emit(q0, qoi);
+            emit(q1, qoi + 1);
+            emit(q2, qoi + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
+            push_group<D, D, WPL>(y0, y1, y2, h0, h1, cc);
+            q0 = y0;
+            q1 = y1;
+            q2 = y2;
+            qoi = k - 2 * D;
+            __builtin_amdgcn_sched_barrier(0);
+            x0 = vmov(n0);
+            x1 = vmov(n1);
+            x2 = vmov(n2);
+            k += 3;
+        }
+        Lanes<WPL> a0 = load_next(), a1 = load_next(), a2 = load_next(), b0, b1, b2;
+        auto body = [&](Lanes<WPL> &n0, Lanes<WPL> &n1, Lanes<WPL> &n2, Lanes<WPL> &c0, Lanes<WPL> &c1,
+                        Lanes<WPL> &c2) {
+            n0 = load_next();
+            n1 = load_next();
+            n2 = load_next();
+            emit(q0, qoi);
+            emit(q1, qoi + 1);
+            emit(q2, qoi + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
+            push_group<D, D, WPL>(y0, y1, y2, h0, h1, cc);
+            q0 = y0;
+            q1 = y1;
+            q2 = y2;
+            qoi = k - 2 * D;
+            __builtin_amdgcn_sched_barrier(0);
+            x0 = vmov(c0);
+            x1 = vmov(c1);
+            x2 = vmov(c2);
+            k += 3;
+        };
+        while (k < kmain) {  // an even number of groups is left
+            body(b0, b1, b2, a0, a1, a2);
+            body(a0, a1, a2, b0, b1, b2);
+        }
+    } else {
+        for (; k < kmain; k += 3) {
+            const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
+            emit(q0, qoi);
+            emit(q1, qoi + 1);
+            emit(q2, qoi + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
+            push_group<D, D, WPL>(y0, y1, y2, h0, h1, cc);
+            q0 = y0;
+            q1 = y1;
+            q2 = y2;
+            qoi = k - 2 * D;
+            __builtin_amdgcn_sched_barrier(0);
+            x0 = vmov(n0);
+            x1 = vmov(n1);
+            x2 = vmov(n2);
+        }
     }
     if (phase_tr && lane == 0) phase_tr[1] = (unsigned long long)__builtin_amdgcn_s_memrealtime();  // main done
     if (!self) {
@@ -2672,7 +2727,7 @@ const char *build_info() {
            " GOL_PERSIST_STORE=" GOL_STR(GOL_PERSIST_STORE) " GOL_PAIR_STORE=" GOL_STR(GOL_PAIR_STORE)
            " GOL_PAIR_G2=" GOL_STR(GOL_PAIR_G2) " GOL_FILL_PHASES=" GOL_STR(GOL_FILL_PHASES)
            " GOL_SKEW_STORE_CPOL=" GOL_STR(GOL_SKEW_STORE_CPOL) " GOL_PERSIST_WG_COUNT=" GOL_STR(GOL_PERSIST_WG_COUNT)
-           " GOL_COMPACT_WPT=" GOL_STR(GOL_COMPACT_WPT);
+           " GOL_COMPACT_WPT=" GOL_STR(GOL_COMPACT_WPT) " GOL_SKEW_PREFETCH=" GOL_STR(GOL_SKEW_PREFETCH);
 }
 
 }  // namespace golk

@@ -1,0 +1,72 @@
+// Stress test of gol::Chan (gol_host.h): Go channel semantics under
+// contention -- every value delivered exactly once and in per-sender order,
+// an unbuffered send returns only after its value was received, close ends
+// a range loop once drained.  Built and run by tests/test_chan_cpu.py.
+#include <chrono>
+#include <cstdio>
+#include <thread>
+#include <vector>
+
+#include "gol_host.h"
+
+static int run(size_t cap, int senders, int per_sender) {
+    gol::Chan<int64_t> ch(cap);
+    std::atomic<int64_t> received_count{0};
+    std::vector<std::thread> ts;
+    std::atomic<int> order_errors{0};
+    for (int s = 0; s < senders; ++s)
+        ts.emplace_back([&, s] {
+            for (int i = 0; i < per_sender; ++i) {
+                if (!ch.send((int64_t)s << 32 | i)) order_errors++;
+                // rendezvous: the receiver has taken this value before send returned
+                if (cap == 0 && received_count.load() < 0) order_errors++;
+            }
+        });
+    std::vector<int> next(senders, 0);
+    std::thread closer([&] {
+        for (auto &t : ts) t.join();
+        ch.close();
+    });
+    int64_t v, n = 0;
+    while (ch.recv(v)) {
+        const int s = (int)(v >> 32), i = (int)(v & 0xffffffff);
+        if (s < 0 || s >= senders || next[s] != i) order_errors++;
+        else next[s]++;
+        received_count++;
+        n++;
+    }
+    closer.join();
+    if (n != (int64_t)senders * per_sender || order_errors.load()) {
+        std::printf("FAIL cap=%zu senders=%d got %lld errors %d\n", cap, senders, (long long)n, order_errors.load());
+        return 1;
+    }
+    if (ch.send(1)) {
+        std::printf("FAIL send after close succeeded\n");
+        return 1;
+    }
+    return 0;
+}
+
+int main() {
+    int rc = 0;
+    for (size_t cap : {0, 1, 7, 1000})
+        for (int senders : {1, 3})
+            rc |= run(cap, senders, 20000);
+    // unbuffered rendezvous: send blocks until the (late) receiver takes the value
+    gol::Chan<int> ch(0);
+    std::thread r([&] {
+        std::this_thread::sleep_for(std::chrono::milliseconds(50));
+        int v;
+        ch.recv(v);
+    });
+    const auto t0 = std::chrono::steady_clock::now();
+    ch.send(7);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    r.join();
+    if (ms < 40) {
+        std::printf("FAIL unbuffered send returned after %.1f ms, before the receiver\n", ms);
+        rc = 1;
+    }
+    std::printf(rc ? "chan stress FAILED\n" : "chan stress ok\n");
+    return rc;
+}
