@@ -1277,6 +1277,9 @@ __global__ __launch_bounds__(256) void gol_split_tri_kernel(SplitArgs p) {
 #ifndef GOL_SKEW_PREFETCH
 #define GOL_SKEW_PREFETCH 1  // K1w main loop: load the rows 1 or 2 groups ahead
 #endif
+#ifndef GOL_SKEW_FILL6
+#define GOL_SKEW_FILL6 0  // K1w fill in six-row groups (push_group6_exp)
+#endif
 #ifndef GOL_SKEW_STORE_CPOL
 #define GOL_SKEW_STORE_CPOL 16  // K1w output stores sc1 (16384^2 +3.6 %, 8192-row strips +1.9 % in a round-3 A/B whose scratch data was not kept; 0 plain, 2 nt)
 #endif
@@ -1326,6 +1329,31 @@ __device__ __forceinline__ void push_group_hi(Lanes<WPL> &x0, Lanes<WPL> &x1, La
         if (s < D) stage<D, 0, WPL>(s, x0, h0, h1, cc);
         if (s - 1 >= LO && s - 1 < D) stage<D, 1, WPL>(s - 1, x1, h0, h1, cc);
         if (s - 2 >= LO) stage<D, 2, WPL>(s - 2, x2, h0, h1, cc);
+    }
+}
+
+// push_group_exp for six rows at once (K1w fill, GOL_SKEW_FILL6): row i of
+// the group runs stage s - i at step s, so up to six independent rows share a
+// step (three in push_group) -- the fill's short groups (A = 3, 6, ...
+// stages) otherwise leave the SIMD without independent work at their ends.
+// Rows i and i + 3 have the same ring slot but never the same stage in one
+// step, and row i + 3 overwrites row i's slot of stage t one step after row
+// i + 2 read it there.
+template <int D, int A, int WPL, typename Hook>
+__device__ __forceinline__ void push_group6_exp(Lanes<WPL> (&x)[6], uint32_t (&h0)[3][D][WPL],
+                                                uint32_t (&h1)[3][D][WPL], uint32_t (&cc)[3][D][WPL], int ii0,
+                                                Hook &&hook) {
+    parity_fix<1>();
+#pragma unroll
+    for (int s = 0; s < A + 5; ++s) {
+        if constexpr (WPL <= 2) parity_fix<1>();
+        static_for<6>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            if (s - i >= 0 && s - i < A) {
+                hook(s - i, ii0 + i, x[i]);
+                stage<D, i % 3, WPL>(s - i, x[i], h0, h1, cc);
+            }
+        });
     }
 }
 
@@ -1431,8 +1459,48 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
             x2 = vmov(n2);
         }
     };
-    static_for<SP::NPH>([&](auto j) { fill(std::integral_constant<int, SP::P(decltype(j)::value)>()); });
-    fill(std::integral_constant<int, D>());
+    if constexpr (GOL_SKEW_FILL6 && SP::STEP == 3) {
+        // Six-row fill: each phase A = P(j) < D spans exactly the six input
+        // rows [6 j, 6 j + 6) (the rows below input index 2 A), and the last
+        // phase (A = D) rows [6 NPH, 2 D) rounded up to whole groups of three:
+        // one more six-row group when that is six rows, else the three-row
+        // loop.  Straight-line code (each group runs once); the loads of a
+        // group fetch exactly the rows of the next one.
+        constexpr int LAST6 = 2 * D - 6 * SP::NPH > 3;  // (2D - 6 NPH) in {4, 5, 6}: one six-row group
+        Lanes<WPL> xs[6] = {x0, x1, x2};
+        xs[3] = vmov(load_next());
+        xs[4] = vmov(load_next());
+        xs[5] = vmov(load_next());
+        auto group6 = [&](auto a_tag, auto next6_tag) {
+            constexpr int A = decltype(a_tag)::value;
+            constexpr bool NEXT6 = decltype(next6_tag)::value;
+            Lanes<WPL> n[6];
+            static_for<(NEXT6 ? 6 : 3)>([&](auto ic) { n[decltype(ic)::value] = load_next(); });
+            __builtin_amdgcn_sched_barrier(0);
+            Lanes<WPL> y[6] = {xs[0], xs[1], xs[2], xs[3], xs[4], xs[5]};
+            push_group6_exp<D, A, WPL>(y, h0, h1, cc, k, hook);
+            if constexpr (A == D) static_for<6>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                emit(y[i], k + i - 2 * D);
+            });
+            __builtin_amdgcn_sched_barrier(0);
+            static_for<(NEXT6 ? 6 : 3)>([&](auto ic) { xs[decltype(ic)::value] = vmov(n[decltype(ic)::value]); });
+            k += 6;
+        };
+        static_for<SP::NPH>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            group6(std::integral_constant<int, SP::P(J)>(),
+                   std::integral_constant<bool, (J + 1 < SP::NPH) || LAST6>());
+        });
+        if constexpr (LAST6) group6(std::integral_constant<int, D>(), std::false_type());
+        x0 = xs[0];
+        x1 = xs[1];
+        x2 = xs[2];
+        if constexpr (!LAST6) fill(std::integral_constant<int, D>());
+    } else {
+        static_for<SP::NPH>([&](auto j) { fill(std::integral_constant<int, SP::P(decltype(j)::value)>()); });
+        fill(std::integral_constant<int, D>());
+    }
     if (phase_tr && lane == 0) phase_tr[0] = (unsigned long long)__builtin_amdgcn_s_memrealtime();  // fill done
     // exports done: this wave's LDS writes complete before the flag (LDS
     // operations of a wave complete in order; no wait on its global loads)
@@ -2727,7 +2795,8 @@ const char *build_info() {
            " GOL_PERSIST_STORE=" GOL_STR(GOL_PERSIST_STORE) " GOL_PAIR_STORE=" GOL_STR(GOL_PAIR_STORE)
            " GOL_PAIR_G2=" GOL_STR(GOL_PAIR_G2) " GOL_FILL_PHASES=" GOL_STR(GOL_FILL_PHASES)
            " GOL_SKEW_STORE_CPOL=" GOL_STR(GOL_SKEW_STORE_CPOL) " GOL_PERSIST_WG_COUNT=" GOL_STR(GOL_PERSIST_WG_COUNT)
-           " GOL_COMPACT_WPT=" GOL_STR(GOL_COMPACT_WPT) " GOL_SKEW_PREFETCH=" GOL_STR(GOL_SKEW_PREFETCH);
+           " GOL_COMPACT_WPT=" GOL_STR(GOL_COMPACT_WPT) " GOL_SKEW_PREFETCH=" GOL_STR(GOL_SKEW_PREFETCH)
+           " GOL_SKEW_FILL6=" GOL_STR(GOL_SKEW_FILL6);
 }
 
 }  // namespace golk
