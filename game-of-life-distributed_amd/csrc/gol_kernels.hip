@@ -1280,6 +1280,9 @@ __global__ __launch_bounds__(256) void gol_split_tri_kernel(SplitArgs p) {
 #ifndef GOL_SKEW_FILL6
 #define GOL_SKEW_FILL6 0  // K1w fill in six-row groups (push_group6_exp)
 #endif
+#ifndef GOL_SKEW_DRAIN6
+#define GOL_SKEW_DRAIN6 0  // K1w drain in six-row groups (push_group6_hi)
+#endif
 #ifndef GOL_SKEW_STORE_CPOL
 #define GOL_SKEW_STORE_CPOL 16  // K1w output stores sc1 (16384^2 +3.6 %, 8192-row strips +1.9 % in a round-3 A/B whose scratch data was not kept; 0 plain, 2 nt)
 #endif
@@ -1353,6 +1356,22 @@ __device__ __forceinline__ void push_group6_exp(Lanes<WPL> (&x)[6], uint32_t (&h
                 hook(s - i, ii0 + i, x[i]);
                 stage<D, i % 3, WPL>(s - i, x[i], h0, h1, cc);
             }
+        });
+    }
+}
+
+// push_group_hi for six rows at once (K1w drain, GOL_SKEW_DRAIN6): the rows
+// enter stage LO, row i at step LO + i (see push_group6_exp).
+template <int D, int LO, int WPL>
+__device__ __forceinline__ void push_group6_hi(Lanes<WPL> (&x)[6], uint32_t (&h0)[3][D][WPL],
+                                               uint32_t (&h1)[3][D][WPL], uint32_t (&cc)[3][D][WPL]) {
+    parity_fix<1>();
+#pragma unroll
+    for (int s = LO; s < D + 5; ++s) {
+        parity_fix<2>();
+        static_for<6>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            if (s - i >= LO && s - i < D) stage<D, i % 3, WPL>(s - i, x[i], h0, h1, cc);
         });
     }
 }
@@ -1643,10 +1662,67 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
                 x2 = vmov(n2);
             }
         };
-        static_for<SP::NPH>([&](auto j) {
-            constexpr int J = decltype(j)::value;
-            drain(std::integral_constant<int, SP::P(J)>(), S + 2 * (J + 1 < SP::NPH ? SP::P(J + 1) : D));
-        });
+        if constexpr (GOL_SKEW_DRAIN6 && SP::STEP == 3) {
+            // Six-row drain: drain phase J spans exactly the six pushes
+            // [S + 2 P(J), S + 2 P(J + 1)); the last phase [S + 2 P(NPH-1), S + 2 D)
+            // is one six-row group when it is 4-6 pushes, else the three-row loop.
+            constexpr bool LAST6 = 2 * (D - SP::STEP * SP::NPH) > 3;
+            constexpr int N6 = LAST6 ? SP::NPH : SP::NPH - 1;  // phases run as six-row groups
+            Lanes<WPL> xs[6], qs[6];
+            {
+                Lanes<WPL> n[6];
+                imports(k + 3, n[3], n[4], n[5]);
+                xs[0] = x0;
+                xs[1] = x1;
+                xs[2] = x2;
+                static_for<3>([&](auto ic) { xs[3 + decltype(ic)::value] = vmov(n[3 + decltype(ic)::value]); });
+            }
+            qs[0] = q0;
+            qs[1] = q1;
+            qs[2] = q2;
+            int npend = 3;  // stores pending from the main loop
+            auto group6 = [&](auto lo_tag, auto next6_tag) {
+                constexpr int LO = decltype(lo_tag)::value;
+                constexpr bool NEXT6 = decltype(next6_tag)::value;
+                Lanes<WPL> n[6];
+                imports(k + 6, n[0], n[1], n[2]);
+                if constexpr (NEXT6) imports(k + 9, n[3], n[4], n[5]);
+                __builtin_amdgcn_sched_barrier(0);
+                Lanes<WPL> y[6] = {xs[0], xs[1], xs[2], xs[3], xs[4], xs[5]};
+                push_group6_hi<D, LO, WPL>(y, h0, h1, cc);
+                __builtin_amdgcn_sched_barrier(0);
+                static_for<6>([&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+                    if (i < npend) emit(qs[i], qoi + i);
+                    qs[i] = y[i];
+                });
+                npend = 6;
+                qoi = k - 2 * D;
+                __builtin_amdgcn_sched_barrier(0);
+                static_for<(NEXT6 ? 6 : 3)>([&](auto ic) { xs[decltype(ic)::value] = vmov(n[decltype(ic)::value]); });
+                k += 6;
+            };
+            static_for<N6>([&](auto j) {
+                constexpr int J = decltype(j)::value;
+                group6(std::integral_constant<int, SP::P(J)>(), std::integral_constant<bool, (J + 1 < N6)>());
+            });
+            if constexpr (!LAST6) {  // the last phase on three-row groups
+                static_for<6>([&](auto ic) { emit(qs[decltype(ic)::value], qoi + decltype(ic)::value); });
+                x0 = xs[0];
+                x1 = xs[1];
+                x2 = xs[2];
+                qoi = -8;  // nothing pending
+                drain(std::integral_constant<int, SP::P(SP::NPH - 1)>(), S + 2 * D);
+            } else {
+                static_for<6>([&](auto ic) { emit(qs[decltype(ic)::value], qoi + decltype(ic)::value); });
+                return cnt;
+            }
+        } else {
+            static_for<SP::NPH>([&](auto j) {
+                constexpr int J = decltype(j)::value;
+                drain(std::integral_constant<int, SP::P(J)>(), S + 2 * (J + 1 < SP::NPH ? SP::P(J + 1) : D));
+            });
+        }
     }
     emit(q0, qoi);
     emit(q1, qoi + 1);
@@ -2796,7 +2872,7 @@ const char *build_info() {
            " GOL_PAIR_G2=" GOL_STR(GOL_PAIR_G2) " GOL_FILL_PHASES=" GOL_STR(GOL_FILL_PHASES)
            " GOL_SKEW_STORE_CPOL=" GOL_STR(GOL_SKEW_STORE_CPOL) " GOL_PERSIST_WG_COUNT=" GOL_STR(GOL_PERSIST_WG_COUNT)
            " GOL_COMPACT_WPT=" GOL_STR(GOL_COMPACT_WPT) " GOL_SKEW_PREFETCH=" GOL_STR(GOL_SKEW_PREFETCH)
-           " GOL_SKEW_FILL6=" GOL_STR(GOL_SKEW_FILL6);
+           " GOL_SKEW_FILL6=" GOL_STR(GOL_SKEW_FILL6) " GOL_SKEW_DRAIN6=" GOL_STR(GOL_SKEW_DRAIN6);
 }
 
 }  // namespace golk
