@@ -1283,6 +1283,9 @@ __global__ __launch_bounds__(256) void gol_split_tri_kernel(SplitArgs p) {
 #ifndef GOL_SKEW_DRAIN6
 #define GOL_SKEW_DRAIN6 0  // K1w drain in six-row groups (push_group6_hi)
 #endif
+#ifndef GOL_SKEW_WAIT_TRACE
+#define GOL_SKEW_WAIT_TRACE 0  // diagnostic builds: per-wave load-wait ticks of K1w (option "trace")
+#endif
 #ifndef GOL_SKEW_STORE_CPOL
 #define GOL_SKEW_STORE_CPOL 16  // K1w output stores sc1 (16384^2 +3.6 %, 8192-row strips +1.9 % in a round-3 A/B whose scratch data was not kept; 0 plain, 2 nt)
 #endif
@@ -1460,6 +1463,9 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
 
     Lanes<WPL> x0 = vmov(load_next()), x1 = vmov(load_next()), x2 = vmov(load_next());
     int k = 0;  // push index of x0, from ab
+    // GOL_SKEW_WAIT_TRACE (diagnostic build, option "trace"): s_memrealtime
+    // ticks each wave spends waiting for its next group's rows
+    [[maybe_unused]] unsigned long long wt0 = 0, wmain = 0, nmain = 0, wfill = 0, nfill = 0;
     auto fill = [&](auto a_tag) {
         constexpr int A = decltype(a_tag)::value;
         for (; A == D ? k <= 2 * D - 1 : (k + 2) / 2 <= A - 1; k += 3) {
@@ -1473,9 +1479,15 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
                 emit(y2, k + 2 - 2 * D);
             }
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (GOL_SKEW_WAIT_TRACE) wt0 = __builtin_amdgcn_s_memrealtime();
             x0 = vmov(n0);
             x1 = vmov(n1);
             x2 = vmov(n2);
+            if constexpr (GOL_SKEW_WAIT_TRACE) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                wfill += __builtin_amdgcn_s_memrealtime() - wt0;
+                ++nfill;
+            }
         }
     };
     if constexpr (GOL_SKEW_FILL6 && SP::STEP == 3) {
@@ -1597,9 +1609,23 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
             q2 = y2;
             qoi = k - 2 * D;
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (GOL_SKEW_WAIT_TRACE) wt0 = __builtin_amdgcn_s_memrealtime();
             x0 = vmov(n0);
             x1 = vmov(n1);
             x2 = vmov(n2);
+            if constexpr (GOL_SKEW_WAIT_TRACE) {
+                asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // the rows have landed
+                wmain += __builtin_amdgcn_s_memrealtime() - wt0;
+                ++nmain;
+            }
+        }
+    }
+    if constexpr (GOL_SKEW_WAIT_TRACE) {
+        if (phase_tr && lane == 0) {
+            phase_tr[16] = wmain;  // (block, 16 + wave): main-loop wait ticks, groups
+            phase_tr[17] = nmain;
+            phase_tr[32] = wfill;  // (block, 24 + wave): fill wait ticks, groups
+            phase_tr[33] = nfill;
         }
     }
     if (phase_tr && lane == 0) phase_tr[1] = (unsigned long long)__builtin_amdgcn_s_memrealtime();  // main done
@@ -2872,7 +2898,8 @@ const char *build_info() {
            " GOL_PAIR_G2=" GOL_STR(GOL_PAIR_G2) " GOL_FILL_PHASES=" GOL_STR(GOL_FILL_PHASES)
            " GOL_SKEW_STORE_CPOL=" GOL_STR(GOL_SKEW_STORE_CPOL) " GOL_PERSIST_WG_COUNT=" GOL_STR(GOL_PERSIST_WG_COUNT)
            " GOL_COMPACT_WPT=" GOL_STR(GOL_COMPACT_WPT) " GOL_SKEW_PREFETCH=" GOL_STR(GOL_SKEW_PREFETCH)
-           " GOL_SKEW_FILL6=" GOL_STR(GOL_SKEW_FILL6) " GOL_SKEW_DRAIN6=" GOL_STR(GOL_SKEW_DRAIN6);
+           " GOL_SKEW_FILL6=" GOL_STR(GOL_SKEW_FILL6) " GOL_SKEW_DRAIN6=" GOL_STR(GOL_SKEW_DRAIN6)
+           " GOL_SKEW_WAIT_TRACE=" GOL_STR(GOL_SKEW_WAIT_TRACE);
 }
 
 }  // namespace golk

@@ -69,6 +69,19 @@ if ok.any():
             q["fill_us"] = round(float(((fe[m, w] - st[m, w]) / 100.0).mean()), 2)
             q["main_us"] = round(float(((me[m, w] - fe[m, w]) / 100.0).mean()), 2)
             q["drain_us"] = round(float(((en[m, w] - me[m, w]) / 100.0).mean()), 2)
+# diagnostic builds (GOL_SKEW_WAIT_TRACE): load-wait ticks and groups, main loop (slots 16..23) and fill (24..31)
+wm, nm, wf, nf = t[blocks, 16:24, 0], t[blocks, 16:24, 1], t[blocks, 24:32, 0], t[blocks, 24:32, 1]
+if (nm > 0).any():
+    for q in pos:
+        w = q["w"]
+        m = live[:, w] & (nm[:, w] > 0)
+        if m.any():
+            q["main_wait_us"] = round(float((wm[m, w] / 100.0).mean()), 2)
+            q["main_groups"] = round(float(nm[m, w].mean()), 1)
+        m = live[:, w] & (nf[:, w] > 0)
+        if m.any():
+            q["fill_wait_us"] = round(float((wf[m, w] / 100.0).mean()), 2)
+            q["fill_groups"] = round(float(nf[m, w].mean()), 1)
 res["positions"] = pos
 wg_end = np.where(live, endr, 0).max(axis=1)
 wg_mean = np.where(live, endr, 0).sum(axis=1) / np.maximum(1, live.sum(axis=1))
