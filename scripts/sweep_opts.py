@@ -26,6 +26,8 @@ ap.add_argument("--depth", type=int, default=20)
 ap.add_argument("--no-timing", action="store_true", help="no per-launch HIP timing events (wall clock only)")
 a = ap.parse_args()
 sets = [dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in s.split(",") if kv) for s in a.sets.split(";")]
+if any("halo_skip" in o or "flip_debug" in o for o in sets):  # wrong results by design: measurement only
+    os.environ["GOLHIP_MEASUREMENT"] = "1"
 best = {}
 for rep in range(a.reps):
     for case in a.cases.split(","):

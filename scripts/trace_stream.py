@@ -12,6 +12,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "game-of-life-distributed_amd")]
+os.environ["GOLHIP_MEASUREMENT"] = "1"  # flip_debug 1-3: wrong lists by design
 import golhip  # noqa: E402
 
 N, SEED, T = 5120, 0x5EED0005, 60

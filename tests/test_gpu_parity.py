@@ -659,3 +659,19 @@ def test_per_launch_paired_bands(coracle, N, rows, depth, wpl, rpw, paired):
         assert b.perf()["persist_launches"] == 0
         assert np.array_equal(b.snapshot_bytes(), want)
         assert b.alive_count() == (int((want == 255).sum()), turns)
+
+
+def test_wrong_result_options_need_measurement_consent(monkeypatch):
+    """options whose results are wrong by design (halo_skip,
+    flip_debug 1-3) are refused unless GOLHIP_MEASUREMENT=1; the exact ones
+    (flip_debug 4, the co-residency test hook) stay allowed."""
+    monkeypatch.delenv("GOLHIP_MEASUREMENT", raising=False)
+    with golhip.Board(64, 64) as b:
+        for k, v in (("halo_skip", 1), ("flip_debug", 1), ("flip_debug", 3)):
+            with pytest.raises(golhip.GolHipError, match="GOLHIP_MEASUREMENT"):
+                b.set_option(k, v)
+        b.set_option("flip_debug", 4)
+        b.set_option("halo_skip", 0)
+        monkeypatch.setenv("GOLHIP_MEASUREMENT", "1")
+        b.set_option("halo_skip", 1)
+        b.set_option("halo_skip", 0)
