@@ -328,6 +328,22 @@ __device__ __forceinline__ void stage(int t, Lanes<WPL> &x, uint32_t (&h0)[3][D]
     }
 }
 
+// The first half of a stage only: the entering row's 3-cell sums and centre
+// into the ring (its rule output would be garbage nobody reads: the exact
+// fill of GOL_SKEW_FILL6 == 2 runs this for input indices 2t and 2t + 1).
+template <int D, int R, int WPL>
+__device__ __forceinline__ void stage_rowsum(int t, const Lanes<WPL> &x, uint32_t (&h0)[3][D][WPL],
+                                             uint32_t (&h1)[3][D][WPL], uint32_t (&cc)[3][D][WPL]) {
+    uint32_t s0[WPL], s1[WPL];
+    row_sums<WPL>(x, s0, s1);
+#pragma unroll
+    for (int k = 0; k < WPL; ++k) {
+        h0[R][t][k] = s0[k];
+        h1[R][t][k] = s1[k];
+        cc[R][t][k] = x.w[k];
+    }
+}
+
 // Code layout.  On gfx950 the step kernels' 8-byte VALU instructions issue
 // ~20 % faster at addresses = 4 (mod 8) than at 0 (mod 8): the same kernel
 // shifted by one 4-byte instruction runs 65536^2 at 97 instead of 120 TCUPS,
@@ -1345,7 +1361,12 @@ __device__ __forceinline__ void push_group_hi(Lanes<WPL> &x0, Lanes<WPL> &x1, La
 // Rows i and i + 3 have the same ring slot but never the same stage in one
 // step, and row i + 3 overwrites row i's slot of stage t one step after row
 // i + 2 read it there.
-template <int D, int A, int WPL, typename Hook>
+// EXACT (GOL_SKEW_FILL6 == 2; P0 = the group's first input index, known at
+// compile time): row p runs stage t in full only from p = 2t + 2 on (its
+// output, generation t + 1 of row p - t - 1, is then inside the band's
+// parallelogram), only the row sums for p = 2t and 2t + 1 (read by the full
+// stages of the next two rows), and nothing below 2t.
+template <int D, int A, int WPL, int P0 = -1, typename Hook>
 __device__ __forceinline__ void push_group6_exp(Lanes<WPL> (&x)[6], uint32_t (&h0)[3][D][WPL],
                                                 uint32_t (&h1)[3][D][WPL], uint32_t (&cc)[3][D][WPL], int ii0,
                                                 Hook &&hook) {
@@ -1356,8 +1377,17 @@ __device__ __forceinline__ void push_group6_exp(Lanes<WPL> (&x)[6], uint32_t (&h
         static_for<6>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             if (s - i >= 0 && s - i < A) {
-                hook(s - i, ii0 + i, x[i]);
-                stage<D, i % 3, WPL>(s - i, x[i], h0, h1, cc);
+                const int t = s - i;
+                if constexpr (P0 < 0) {
+                    hook(t, ii0 + i, x[i]);
+                    stage<D, i % 3, WPL>(t, x[i], h0, h1, cc);
+                } else if (P0 + i >= 2 * t + 2) {
+                    hook(t, ii0 + i, x[i]);
+                    stage<D, i % 3, WPL>(t, x[i], h0, h1, cc);
+                } else if (P0 + i >= 2 * t) {
+                    hook(t, ii0 + i, x[i]);
+                    stage_rowsum<D, i % 3, WPL>(t, x[i], h0, h1, cc);
+                }
             }
         });
     }
@@ -1502,14 +1532,15 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
         xs[3] = vmov(load_next());
         xs[4] = vmov(load_next());
         xs[5] = vmov(load_next());
-        auto group6 = [&](auto a_tag, auto next6_tag) {
+        auto group6 = [&](auto a_tag, auto next6_tag, auto p0_tag) {
             constexpr int A = decltype(a_tag)::value;
             constexpr bool NEXT6 = decltype(next6_tag)::value;
             Lanes<WPL> n[6];
             static_for<(NEXT6 ? 6 : 3)>([&](auto ic) { n[decltype(ic)::value] = load_next(); });
             __builtin_amdgcn_sched_barrier(0);
             Lanes<WPL> y[6] = {xs[0], xs[1], xs[2], xs[3], xs[4], xs[5]};
-            push_group6_exp<D, A, WPL>(y, h0, h1, cc, k, hook);
+            constexpr int P0 = decltype(p0_tag)::value;
+            push_group6_exp<D, A, WPL, (GOL_SKEW_FILL6 >= 2 ? P0 : -1)>(y, h0, h1, cc, k, hook);
             if constexpr (A == D) static_for<6>([&](auto ic) {
                 constexpr int i = decltype(ic)::value;
                 emit(y[i], k + i - 2 * D);
@@ -1521,9 +1552,10 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
         static_for<SP::NPH>([&](auto j) {
             constexpr int J = decltype(j)::value;
             group6(std::integral_constant<int, SP::P(J)>(),
-                   std::integral_constant<bool, (J + 1 < SP::NPH) || LAST6>());
+                   std::integral_constant<bool, (J + 1 < SP::NPH) || LAST6>(), std::integral_constant<int, 6 * J>());
         });
-        if constexpr (LAST6) group6(std::integral_constant<int, D>(), std::false_type());
+        if constexpr (LAST6)
+            group6(std::integral_constant<int, D>(), std::false_type(), std::integral_constant<int, 6 * SP::NPH>());
         x0 = xs[0];
         x1 = xs[1];
         x2 = xs[2];
