@@ -1302,6 +1302,9 @@ __global__ __launch_bounds__(256) void gol_split_tri_kernel(SplitArgs p) {
 #ifndef GOL_SKEW_WAIT_TRACE
 #define GOL_SKEW_WAIT_TRACE 0  // diagnostic builds: per-wave load-wait ticks of K1w (option "trace")
 #endif
+#ifndef GOL_SKEW_HALF4
+#define GOL_SKEW_HALF4 0  // K1w half-wave tiles with four words per lane (A/B builds)
+#endif
 #ifndef GOL_SKEW_STORE_CPOL
 #define GOL_SKEW_STORE_CPOL 16  // K1w output stores sc1 (16384^2 +3.6 %, 8192-row strips +1.9 % in a round-3 A/B whose scratch data was not kept; 0 plain, 2 nt)
 #endif
@@ -2106,6 +2109,9 @@ static hipError_t dispatch_skew(int depth, int wpl, bool half, F &&f) {
     GOL_WCASE(8, 2) GOL_WCASE(12, 2) GOL_WCASE(16, 2) GOL_WCASE(20, 2) GOL_WCASE(6, 4) GOL_WCASE(8, 4)
     GOL_WCASE(9, 4) GOL_WCASE(16, 1) GOL_WCASE(32, 1)
     GOL_HCASE(16, 2) GOL_HCASE(20, 2)
+#if GOL_SKEW_HALF4
+    GOL_HCASE(8, 4) GOL_HCASE(9, 4)
+#endif
 #undef GOL_WCASE
 #undef GOL_HCASE
     return hipErrorInvalidValue;
@@ -2931,7 +2937,7 @@ const char *build_info() {
            " GOL_SKEW_STORE_CPOL=" GOL_STR(GOL_SKEW_STORE_CPOL) " GOL_PERSIST_WG_COUNT=" GOL_STR(GOL_PERSIST_WG_COUNT)
            " GOL_COMPACT_WPT=" GOL_STR(GOL_COMPACT_WPT) " GOL_SKEW_PREFETCH=" GOL_STR(GOL_SKEW_PREFETCH)
            " GOL_SKEW_FILL6=" GOL_STR(GOL_SKEW_FILL6) " GOL_SKEW_DRAIN6=" GOL_STR(GOL_SKEW_DRAIN6)
-           " GOL_SKEW_WAIT_TRACE=" GOL_STR(GOL_SKEW_WAIT_TRACE);
+           " GOL_SKEW_WAIT_TRACE=" GOL_STR(GOL_SKEW_WAIT_TRACE) " GOL_SKEW_HALF4=" GOL_STR(GOL_SKEW_HALF4);
 }
 
 }  // namespace golk

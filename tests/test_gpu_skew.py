@@ -209,6 +209,21 @@ def test_skew_half_tiles_match_oracle(coracle, depth, W, H, tx):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("depth", [9, 8])
+@pytest.mark.parametrize("W,H", [(16384, 1000), (5120, 2222), (3072, 1502), (2048, 818)])
+def test_skew_half_quad_tiles_match_oracle(coracle, depth, W, H):
+    """Half-wave tiles with four words per lane (30 stored lanes x 4 words a
+    half tile; builds with GOL_SKEW_HALF4)."""
+    if "GOL_SKEW_HALF4=1" not in golhip.load().golhip_build_info().decode():
+        pytest.skip("build without half-wave quad tiles")
+    board = coracle.fill_random(W, H, 0x5EED0047 + W + H + depth)
+    turns = 2 * depth + 5
+    want = coracle.run(board, turns)
+    got, p = run_skew(board, turns, depth, 4, skew_half=1)
+    assert p["skew_half_launches"] >= 2
+    assert np.array_equal(got, want)
+
+
 def test_skew_half_tiles_need_even_rows(coracle):
     """An odd number of rows cannot split into two equal halves: full tiles."""
     board = coracle.fill_random(16384, 1001, 0x5EED0042)
