@@ -1657,10 +1657,10 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
     }
     if constexpr (GOL_SKEW_WAIT_TRACE) {
         if (phase_tr && lane == 0) {
-            phase_tr[16] = wmain;  // (block, 16 + wave): main-loop wait ticks, groups
-            phase_tr[17] = nmain;
-            phase_tr[32] = wfill;  // (block, 24 + wave): fill wait ticks, groups
-            phase_tr[33] = nfill;
+            phase_tr[32] = wmain;  // (block, 32 + wave): main-loop wait ticks, groups
+            phase_tr[33] = nmain;
+            phase_tr[64] = wfill;  // (block, 48 + wave): fill wait ticks, groups
+            phase_tr[65] = nfill;
         }
     }
     if (phase_tr && lane == 0) phase_tr[1] = (unsigned long long)__builtin_amdgcn_s_memrealtime();  // main done
@@ -1791,18 +1791,20 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
     return cnt;
 }
 
-// K1w: one workgroup = one stack = tx tiles x (8 / tx) bands; wave w takes
-// tile w % tx and stack position w / tx (top to bottom).
-template <int D, int WPL, bool HALF = false>
-__global__ __launch_bounds__(512) void gol_skew_kernel(SkewArgs p) {
+// K1w: one workgroup = one stack = tx tiles x (NW / tx) bands; wave w takes
+// tile w % tx and stack position w / tx (top to bottom).  NW = 8 waves (two
+// per SIMD); NW = 12 (three per SIMD, round 4) for the depths whose
+// pipelines fit 168 VGPRs: wave w sits on SIMD w % 4 with age rank w / 4.
+template <int D, int WPL, bool HALF = false, int NW = 8>
+__global__ __launch_bounds__(NW * 64) void gol_skew_kernel(SkewArgs p) {
     using SP = SkewPlan<D>;
     constexpr int ROW = 64 * WPL;
-    __shared__ uint32_t s_exp[8][(SP::NEXP + 1) * ROW];
-    __shared__ int s_flag[8];
+    __shared__ uint32_t s_exp[NW][(SP::NEXP + 1) * ROW];
+    __shared__ int s_flag[NW];
     __shared__ unsigned long long s_cnt;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int sy = 8 / p.tx;
+    const int sy = NW / p.tx;
     const int tcols = (p.tiles_x + p.tx - 1) / p.tx;
     const int stack = blockIdx.x / tcols, tc = blockIdx.x - stack * tcols;
     const int tile = tc * p.tx + w % p.tx, pos = w / p.tx;
@@ -1810,7 +1812,7 @@ __global__ __launch_bounds__(512) void gol_skew_kernel(SkewArgs p) {
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
     if (tile >= p.tiles_x) return;  // wave-uniform, after the only barrier (its stack's waves all leave)
-    if (p.prio_young && w >= 4) __builtin_amdgcn_s_setprio(1);
+    if (NW == 8 && p.prio_young && w >= 4) __builtin_amdgcn_s_setprio(1);
     // HALF: the stacks split the first half of the rows; each wave's upper
     // lanes take the same band L / 2 rows further down (L even, host-checked)
     const int L = HALF ? p.base.rows_out / 2 : p.base.rows_out;
@@ -1829,7 +1831,7 @@ __global__ __launch_bounds__(512) void gol_skew_kernel(SkewArgs p) {
     const long long t_start = p.trace ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
     const uint32_t cnt = stream_skew<D, WPL, HALF>(p.base, ab, eb, tile, bottom, s_exp[w], bottom ? nullptr : s_exp[w + p.tx],
                                              &s_flag[w], bottom ? nullptr : &s_flag[w + p.tx], p.error,
-                                             (p.trace && blockIdx.x < 1024) ? p.trace + 8 + 2 * (blockIdx.x * 64 + 8 + w)
+                                             (p.trace && blockIdx.x < 1024) ? p.trace + 8 + 2 * (blockIdx.x * 64 + 16 + w)
                                                                             : nullptr,
                                              L);
     if (p.trace && lane == 0 && blockIdx.x < 1024) {
@@ -2101,11 +2103,14 @@ hipError_t launch_split(const SplitArgs &p, int depth, int wpl, hipStream_t s) {
 }
 
 template <typename F>
-static hipError_t dispatch_skew(int depth, int wpl, bool half, F &&f) {
+static hipError_t dispatch_skew(int depth, int wpl, bool half, int nw, F &&f) {
 #define GOL_WCASE(D, WP) \
-    if (!half && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP>);
+    if (nw == 8 && !half && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP>);
 #define GOL_HCASE(D, WP) \
-    if (half && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP, true>);
+    if (nw == 8 && half && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP, true>);
+#define GOL_NCASE(D, WP, H, N) \
+    if (nw == N && half == H && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP, H, N>);
+    GOL_NCASE(12, 2, false, 12) GOL_NCASE(12, 2, true, 12)
     GOL_WCASE(8, 2) GOL_WCASE(12, 2) GOL_WCASE(16, 2) GOL_WCASE(20, 2) GOL_WCASE(6, 4) GOL_WCASE(8, 4)
     GOL_WCASE(9, 4) GOL_WCASE(16, 1) GOL_WCASE(32, 1)
     GOL_HCASE(16, 2) GOL_HCASE(20, 2)
@@ -2114,25 +2119,27 @@ static hipError_t dispatch_skew(int depth, int wpl, bool half, F &&f) {
 #endif
 #undef GOL_WCASE
 #undef GOL_HCASE
+#undef GOL_NCASE
     return hipErrorInvalidValue;
 }
 
-bool skew_supported(int depth, int wpl, bool half) {
-    return dispatch_skew(depth, wpl, half, [](auto) { return hipSuccess; }) == hipSuccess;
+bool skew_supported(int depth, int wpl, bool half, int nw) {
+    return dispatch_skew(depth, wpl, half, nw, [](auto) { return hipSuccess; }) == hipSuccess;
 }
 
-int skew_blocks_per_cu(int depth, int wpl, bool half) {
+int skew_blocks_per_cu(int depth, int wpl, bool half, int nw) {
     int b = 0;
-    hipError_t e = dispatch_skew(depth, wpl, half, [&](auto kern) {
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 512, 0);
+    hipError_t e = dispatch_skew(depth, wpl, half, nw, [&](auto kern) {
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 64 * nw, 0);
     });
     return e == hipSuccess ? b : 0;
 }
 
 hipError_t launch_skew(const SkewArgs &p, int depth, int wpl, hipStream_t s) {
     const int tcols = (p.tiles_x + p.tx - 1) / p.tx;
-    return dispatch_skew(depth, wpl, p.half != 0, [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(tcols * p.nst), dim3(512), 0, s, p);
+    const int nw = p.nw > 0 ? p.nw : 8;
+    return dispatch_skew(depth, wpl, p.half != 0, nw, [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(tcols * p.nst), dim3(64 * nw), 0, s, p);
         return hipGetLastError();
     });
 }

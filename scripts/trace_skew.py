@@ -42,7 +42,7 @@ with golhip.Board(W, R, timing=True) as b:
     b.sync()
     p = b.perf()
     t = b.persist_trace_waves(256).astype(np.int64)  # (blocks, 64, 2)
-st, en = t[:, :8, 0], t[:, :8, 1]
+st, en = t[:, :16, 0], t[:, :16, 1]
 live = (st > 0) & (en > 0)
 blocks = np.nonzero(live.any(axis=1))[0]
 st, en, live = st[blocks], en[blocks], live[blocks]
@@ -53,13 +53,13 @@ res = {"case": a.case, "opts": a.opt, "launch_ms_event": p["step_kernel_ms"] / m
        "blocks": int(len(blocks)), "span_us": float(endr[live].max()),
        "start_spread_us": float((st[live].max() - t0) / 100.0)}
 pos = []
-for w in range(8):
+for w in range(16):
     m = live[:, w]
     if m.any():
         pos.append({"w": w, "dur_mean": round(float(dur[m, w].mean()), 2), "dur_min": round(float(dur[m, w].min()), 2),
                     "dur_max": round(float(dur[m, w].max()), 2), "end_mean": round(float(endr[m, w].mean()), 2)})
-# phase stamps (fill done, main loop done) of the same waves: slots 8..15
-fe, me = t[blocks, 8:16, 0], t[blocks, 8:16, 1]
+# phase stamps (fill done, main loop done) of the same waves: slots 16..31
+fe, me = t[blocks, 16:32, 0], t[blocks, 16:32, 1]
 ok = live & (fe > 0) & (me > 0)
 if ok.any():
     for q in pos:
@@ -69,8 +69,8 @@ if ok.any():
             q["fill_us"] = round(float(((fe[m, w] - st[m, w]) / 100.0).mean()), 2)
             q["main_us"] = round(float(((me[m, w] - fe[m, w]) / 100.0).mean()), 2)
             q["drain_us"] = round(float(((en[m, w] - me[m, w]) / 100.0).mean()), 2)
-# diagnostic builds (GOL_SKEW_WAIT_TRACE): load-wait ticks and groups, main loop (slots 16..23) and fill (24..31)
-wm, nm, wf, nf = t[blocks, 16:24, 0], t[blocks, 16:24, 1], t[blocks, 24:32, 0], t[blocks, 24:32, 1]
+# diagnostic builds (GOL_SKEW_WAIT_TRACE): load-wait ticks and groups, main loop (slots 32..47) and fill (48..63)
+wm, nm, wf, nf = t[blocks, 32:48, 0], t[blocks, 32:48, 1], t[blocks, 48:64, 0], t[blocks, 48:64, 1]
 if (nm > 0).any():
     for q in pos:
         w = q["w"]
@@ -86,5 +86,5 @@ res["positions"] = pos
 wg_end = np.where(live, endr, 0).max(axis=1)
 wg_mean = np.where(live, endr, 0).sum(axis=1) / np.maximum(1, live.sum(axis=1))
 res["wg_end_us"] = {"min": float(wg_end.min()), "mean": float(wg_end.mean()), "max": float(wg_end.max())}
-res["wg_idle_frac"] = float(((wg_end[:, None] - np.where(live, endr, wg_end[:, None])).sum()) / (wg_end.sum() * 8))
+res["wg_idle_frac"] = float(((wg_end[:, None] - np.where(live, endr, wg_end[:, None])).sum()) / (wg_end.sum() * np.maximum(1, live.sum(axis=1)).mean()))
 print(json.dumps(res))
