@@ -27,6 +27,16 @@ namespace golk {
 #define GOL_FILL_PHASES 4  // K1 fill phases: quarters (8: eighths, round-1 A/B, profiles/r1*)
 #endif
 
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>()), ...);
+}
+// f(integral_constant<int, i>) for i = 0 .. N-1, unrolled at compile time
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>());
+}
+
 // ---------------------------------------------------------------------------
 // bit-sliced helpers
 // ---------------------------------------------------------------------------
@@ -357,6 +367,9 @@ __device__ __forceinline__ void stage_rowsum(int t, const Lanes<WPL> &x, uint32_
 // tree before it happened to sit on the fast parity in every main loop; the
 // fix keeps it there whatever changes upstream of a loop (scripts/
 // loop_parity.py reports the parity of every hot loop of a build).
+#ifndef GOL_SPREAD
+#define GOL_SPREAD 0  // shift-spread schedule of the full groups (push_group_spread)
+#endif
 #ifndef GOL_PARITY_FIX
 #define GOL_PARITY_FIX 1  // profiles/r2lc: 16384^2 +1.2 %, the others within 0.6 % of the lucky layout
 #endif
@@ -375,10 +388,109 @@ __device__ __forceinline__ void parity_fix() {
 // interleave, which hides the VALU->DPP hazard of each stage's serial chain.
 // A < D is used while the pipeline fills: stage t only sees real rows from
 // input index 2t on, so later stages would only compute garbage.
+// Shift-spread schedule of a full group (GOL_SPREAD, two words per lane).
+// gfx950 issues the lane shifts (DPP moves, v_alignbit) at about half the
+// bitop3 rate, and a run of them back to back costs more than the same ones
+// spread between bitop3s: in the issue-rate probe (scripts/valu_probe.hip,
+// profiles/r2s, two waves per SIMD) 12 bitop3 + 4 shifts issued 0.38 wave
+// instructions per SIMD-cycle spread one shift every 3-4 bitop3s, 0.29
+// grouped.  The compiler groups them (every stage's four shifts are ready at
+// the start of a step: the main loop ran runs of 4 DPPs and 4 alignbits, 0.31
+// per SIMD-cycle).  So the group is emitted as a chain of units (row i,
+// stage t) in step order, each unit's 18 bitop3s (row sums, column sums,
+// rule) with the NEXT unit's four shifts placed between its chunks of 4-5,
+// pinned by sched barriers.  A unit whose predecessor is the same row (the
+// group's first and last steps) takes its shifts after it.
+struct SpreadUnit {
+    int row, stage;
+};
+template <int D>
+struct SpreadPlan {
+    SpreadUnit u[3 * D];
+    constexpr SpreadPlan() : u() {
+        int k = 0;
+        for (int s = 0; s < D + 2; ++s)
+            for (int i = 0; i < 3; ++i)
+                if (s - i >= 0 && s - i < D) u[k++] = {i, s - i};
+    }
+};
+struct Shifts2 {
+    uint32_t l1, west0, r0, east1;
+};
+// shift op j (0..3) of a two-word lane's stage input x
+__device__ __forceinline__ void shift_op(int j, const Lanes<2> &x, Shifts2 &sh) {
+    if (j == 0) sh.l1 = from_left_lane(x.w[1]);                         // left chunk's odd cells
+    if (j == 1) sh.west0 = __builtin_amdgcn_alignbit(x.w[1], sh.l1, 31);  // cell 2k-1
+    if (j == 2) sh.r0 = from_right_lane(x.w[0]);                        // right chunk's even cells
+    if (j == 3) sh.east1 = __builtin_amdgcn_alignbit(sh.r0, x.w[0], 1);   // cell 2k+2
+}
+// The 18 bitop3s of unit (row R, stage t) given its shifts; between(c) runs
+// after chunk c = 0..3 (chunks of 4, 5, 4, 5).
+template <int D, int R, typename B>
+__device__ __forceinline__ void stage_bits2(int t, Lanes<2> &x, const Shifts2 &sh, uint32_t (&h0)[3][D][2],
+                                            uint32_t (&h1)[3][D][2], uint32_t (&cc)[3][D][2], B &&between) {
+    constexpr int N = R, C = (R + 2) % 3, P = (R + 1) % 3;
+    h0[N][t][0] = bop<kXor3>(sh.west0, x.w[0], x.w[1]);
+    h1[N][t][0] = bop<kMaj>(sh.west0, x.w[0], x.w[1]);
+    h0[N][t][1] = bop<kXor3>(x.w[0], x.w[1], sh.east1);
+    h1[N][t][1] = bop<kMaj>(x.w[0], x.w[1], sh.east1);
+    between(0);
+    const uint32_t u00 = bop<kXor3>(h0[P][t][0], h0[C][t][0], h0[N][t][0]);
+    const uint32_t u10 = bop<kMaj>(h0[P][t][0], h0[C][t][0], h0[N][t][0]);
+    const uint32_t v00 = bop<kXor3>(h1[P][t][0], h1[C][t][0], h1[N][t][0]);
+    const uint32_t v10 = bop<kMaj>(h1[P][t][0], h1[C][t][0], h1[N][t][0]);
+    const uint32_t g10 = bop<kG1>(u10, v00, v10);
+    between(1);
+    const uint32_t g20 = bop<kG2>(u00, v10, cc[C][t][0]);
+    const uint32_t n0 = bop<kNext>(u00, g10, g20);
+    const uint32_t u01 = bop<kXor3>(h0[P][t][1], h0[C][t][1], h0[N][t][1]);
+    const uint32_t u11 = bop<kMaj>(h0[P][t][1], h0[C][t][1], h0[N][t][1]);
+    between(2);
+    const uint32_t v01 = bop<kXor3>(h1[P][t][1], h1[C][t][1], h1[N][t][1]);
+    const uint32_t v11 = bop<kMaj>(h1[P][t][1], h1[C][t][1], h1[N][t][1]);
+    const uint32_t g11 = bop<kG1>(u11, v01, v11);
+    const uint32_t g21 = bop<kG2>(u01, v11, cc[C][t][1]);
+    const uint32_t n1 = bop<kNext>(u01, g11, g21);
+    between(3);
+    cc[N][t][0] = x.w[0];
+    cc[N][t][1] = x.w[1];
+    x.w[0] = n0;
+    x.w[1] = n1;
+}
+template <int D>
+__device__ __forceinline__ void push_group_spread(Lanes<2> &x0, Lanes<2> &x1, Lanes<2> &x2, uint32_t (&h0)[3][D][2],
+                                                  uint32_t (&h1)[3][D][2], uint32_t (&cc)[3][D][2]) {
+    constexpr SpreadPlan<D> plan;
+    Lanes<2> *xs[3] = {&x0, &x1, &x2};
+    Shifts2 sh[2];
+    parity_fix<1>();
+    static_for<4>([&](auto j) { shift_op(decltype(j)::value, *xs[plan.u[0].row], sh[0]); });
+    static_for<3 * D>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        constexpr int R = plan.u[k].row, T = plan.u[k].stage;
+        constexpr bool has_next = k + 1 < 3 * D;
+        constexpr bool inter = has_next && plan.u[k + 1 < 3 * D ? k + 1 : k].row != R;
+        Shifts2 &me = sh[k & 1], &nx = sh[(k + 1) & 1];
+        Lanes<2> &xn = *xs[plan.u[has_next ? k + 1 : k].row];
+        stage_bits2<D, R>(T, *xs[R], me, h0, h1, cc, [&](int c) {
+            if constexpr (inter) {
+                __builtin_amdgcn_sched_barrier(0);
+                shift_op(c, xn, nx);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        });
+        if constexpr (has_next && !inter) static_for<4>([&](auto j) { shift_op(decltype(j)::value, xn, nx); });
+    });
+}
+
 template <int D, int A, int WPL>
 __device__ __forceinline__ void push_group(Lanes<WPL> &x0, Lanes<WPL> &x1, Lanes<WPL> &x2,
                                            uint32_t (&h0)[3][D][WPL], uint32_t (&h1)[3][D][WPL],
                                            uint32_t (&cc)[3][D][WPL]) {
+    if constexpr (GOL_SPREAD && WPL == 2 && A == D) {
+        push_group_spread<D>(x0, x1, x2, h0, h1, cc);
+        return;
+    }
     parity_fix<1>();
 #pragma unroll
     for (int s = 0; s < A + 2; ++s) {
@@ -1332,15 +1444,6 @@ struct SkewPlan {
     static_assert(NPH >= 1 && STEP % 3 == 0, "skew depth >= 4");
 };
 
-template <typename F, int... I>
-__device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<int, I...>) {
-    (f(std::integral_constant<int, I>()), ...);
-}
-// f(integral_constant<int, i>) for i = 0 .. N-1, unrolled at compile time
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F &&f) {
-    static_for_impl(f, std::make_integer_sequence<int, N>());
-}
 
 // push_group for the last stages only: the group's rows enter stage LO.
 template <int D, int LO, int WPL>
@@ -2944,7 +3047,8 @@ const char *build_info() {
            " GOL_SKEW_STORE_CPOL=" GOL_STR(GOL_SKEW_STORE_CPOL) " GOL_PERSIST_WG_COUNT=" GOL_STR(GOL_PERSIST_WG_COUNT)
            " GOL_COMPACT_WPT=" GOL_STR(GOL_COMPACT_WPT) " GOL_SKEW_PREFETCH=" GOL_STR(GOL_SKEW_PREFETCH)
            " GOL_SKEW_FILL6=" GOL_STR(GOL_SKEW_FILL6) " GOL_SKEW_DRAIN6=" GOL_STR(GOL_SKEW_DRAIN6)
-           " GOL_SKEW_WAIT_TRACE=" GOL_STR(GOL_SKEW_WAIT_TRACE) " GOL_SKEW_HALF4=" GOL_STR(GOL_SKEW_HALF4);
+           " GOL_SKEW_WAIT_TRACE=" GOL_STR(GOL_SKEW_WAIT_TRACE) " GOL_SKEW_HALF4=" GOL_STR(GOL_SKEW_HALF4)
+           " GOL_SPREAD=" GOL_STR(GOL_SPREAD);
 }
 
 }  // namespace golk
