@@ -86,20 +86,19 @@ hipError_t launch_split(const SplitArgs &p, int depth, int wpl, hipStream_t s);
 struct SkewArgs {
     StepArgs base;
     int tiles_x;
-    int tx;           // tiles per workgroup: 1 (stacks of nw bands) or 2 (stacks of nw / 2)
-    int nw;           // waves per workgroup: 8 (two per SIMD) or 12 (three per SIMD)
+    int tx;           // tiles per workgroup: 1 (stacks of 8 bands) or 2 (stacks of 4)
     int half;         // 1: half-wave tiles of 30 lanes (tiles_x counts them); each wave's upper lanes
                       //    run the same band of the stack rows_out / 2 further down (rows_out even)
     int nst;          // stacks per tile column
-    int wgt[12];      // band heights by stack position (relative weights)
+    int wgt[8];       // band heights by stack position (relative weights)
     int hcap;         // rows the stack's bottom band gives up (its drain is computed in full)
     int prio_young;   // 1: s_setprio 1 for waves 4..7 (the SIMD arbiter's age losers)
     unsigned *error;  // nullable, host-mapped: set if a band's imports never arrived (spin bound)
     unsigned long long *trace;  // nullable diagnostics: per wave (start, end) s_memrealtime at 8 + 2 (block * 64 + wave),
                                 // (fill done, main loop done) at 8 + 2 (block * 64 + 8 + wave)
 };
-bool skew_supported(int depth, int wpl, bool half = false, int nw = 8);
-int skew_blocks_per_cu(int depth, int wpl, bool half = false, int nw = 8);
+bool skew_supported(int depth, int wpl, bool half = false);
+int skew_blocks_per_cu(int depth, int wpl, bool half = false);
 hipError_t launch_skew(const SkewArgs &p, int depth, int wpl, hipStream_t s);
 
 // Persistent multi-super-step step kernel (torus, or a strip's extended rows

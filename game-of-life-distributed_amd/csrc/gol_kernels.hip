@@ -338,22 +338,6 @@ __device__ __forceinline__ void stage(int t, Lanes<WPL> &x, uint32_t (&h0)[3][D]
     }
 }
 
-// The first half of a stage only: the entering row's 3-cell sums and centre
-// into the ring (its rule output would be garbage nobody reads: the exact
-// fill of GOL_SKEW_FILL6 == 2 runs this for input indices 2t and 2t + 1).
-template <int D, int R, int WPL>
-__device__ __forceinline__ void stage_rowsum(int t, const Lanes<WPL> &x, uint32_t (&h0)[3][D][WPL],
-                                             uint32_t (&h1)[3][D][WPL], uint32_t (&cc)[3][D][WPL]) {
-    uint32_t s0[WPL], s1[WPL];
-    row_sums<WPL>(x, s0, s1);
-#pragma unroll
-    for (int k = 0; k < WPL; ++k) {
-        h0[R][t][k] = s0[k];
-        h1[R][t][k] = s1[k];
-        cc[R][t][k] = x.w[k];
-    }
-}
-
 // Code layout.  On gfx950 the step kernels' 8-byte VALU instructions issue
 // ~20 % faster at addresses = 4 (mod 8) than at 0 (mod 8): the same kernel
 // shifted by one 4-byte instruction runs 65536^2 at 97 instead of 120 TCUPS,
@@ -367,9 +351,6 @@ __device__ __forceinline__ void stage_rowsum(int t, const Lanes<WPL> &x, uint32_
 // tree before it happened to sit on the fast parity in every main loop; the
 // fix keeps it there whatever changes upstream of a loop (scripts/
 // loop_parity.py reports the parity of every hot loop of a build).
-#ifndef GOL_SPREAD
-#define GOL_SPREAD 0  // shift-spread schedule of the full groups (push_group_spread)
-#endif
 #ifndef GOL_PARITY_FIX
 #define GOL_PARITY_FIX 1  // profiles/r2lc: 16384^2 +1.2 %, the others within 0.6 % of the lucky layout
 #endif
@@ -388,109 +369,10 @@ __device__ __forceinline__ void parity_fix() {
 // interleave, which hides the VALU->DPP hazard of each stage's serial chain.
 // A < D is used while the pipeline fills: stage t only sees real rows from
 // input index 2t on, so later stages would only compute garbage.
-// Shift-spread schedule of a full group (GOL_SPREAD, two words per lane).
-// gfx950 issues the lane shifts (DPP moves, v_alignbit) at about half the
-// bitop3 rate, and a run of them back to back costs more than the same ones
-// spread between bitop3s: in the issue-rate probe (scripts/valu_probe.hip,
-// profiles/r2s, two waves per SIMD) 12 bitop3 + 4 shifts issued 0.38 wave
-// instructions per SIMD-cycle spread one shift every 3-4 bitop3s, 0.29
-// grouped.  The compiler groups them (every stage's four shifts are ready at
-// the start of a step: the main loop ran runs of 4 DPPs and 4 alignbits, 0.31
-// per SIMD-cycle).  So the group is emitted as a chain of units (row i,
-// stage t) in step order, each unit's 18 bitop3s (row sums, column sums,
-// rule) with the NEXT unit's four shifts placed between its chunks of 4-5,
-// pinned by sched barriers.  A unit whose predecessor is the same row (the
-// group's first and last steps) takes its shifts after it.
-struct SpreadUnit {
-    int row, stage;
-};
-template <int D>
-struct SpreadPlan {
-    SpreadUnit u[3 * D];
-    constexpr SpreadPlan() : u() {
-        int k = 0;
-        for (int s = 0; s < D + 2; ++s)
-            for (int i = 0; i < 3; ++i)
-                if (s - i >= 0 && s - i < D) u[k++] = {i, s - i};
-    }
-};
-struct Shifts2 {
-    uint32_t l1, west0, r0, east1;
-};
-// shift op j (0..3) of a two-word lane's stage input x
-__device__ __forceinline__ void shift_op(int j, const Lanes<2> &x, Shifts2 &sh) {
-    if (j == 0) sh.l1 = from_left_lane(x.w[1]);                         // left chunk's odd cells
-    if (j == 1) sh.west0 = __builtin_amdgcn_alignbit(x.w[1], sh.l1, 31);  // cell 2k-1
-    if (j == 2) sh.r0 = from_right_lane(x.w[0]);                        // right chunk's even cells
-    if (j == 3) sh.east1 = __builtin_amdgcn_alignbit(sh.r0, x.w[0], 1);   // cell 2k+2
-}
-// The 18 bitop3s of unit (row R, stage t) given its shifts; between(c) runs
-// after chunk c = 0..3 (chunks of 4, 5, 4, 5).
-template <int D, int R, typename B>
-__device__ __forceinline__ void stage_bits2(int t, Lanes<2> &x, const Shifts2 &sh, uint32_t (&h0)[3][D][2],
-                                            uint32_t (&h1)[3][D][2], uint32_t (&cc)[3][D][2], B &&between) {
-    constexpr int N = R, C = (R + 2) % 3, P = (R + 1) % 3;
-    h0[N][t][0] = bop<kXor3>(sh.west0, x.w[0], x.w[1]);
-    h1[N][t][0] = bop<kMaj>(sh.west0, x.w[0], x.w[1]);
-    h0[N][t][1] = bop<kXor3>(x.w[0], x.w[1], sh.east1);
-    h1[N][t][1] = bop<kMaj>(x.w[0], x.w[1], sh.east1);
-    between(0);
-    const uint32_t u00 = bop<kXor3>(h0[P][t][0], h0[C][t][0], h0[N][t][0]);
-    const uint32_t u10 = bop<kMaj>(h0[P][t][0], h0[C][t][0], h0[N][t][0]);
-    const uint32_t v00 = bop<kXor3>(h1[P][t][0], h1[C][t][0], h1[N][t][0]);
-    const uint32_t v10 = bop<kMaj>(h1[P][t][0], h1[C][t][0], h1[N][t][0]);
-    const uint32_t g10 = bop<kG1>(u10, v00, v10);
-    between(1);
-    const uint32_t g20 = bop<kG2>(u00, v10, cc[C][t][0]);
-    const uint32_t n0 = bop<kNext>(u00, g10, g20);
-    const uint32_t u01 = bop<kXor3>(h0[P][t][1], h0[C][t][1], h0[N][t][1]);
-    const uint32_t u11 = bop<kMaj>(h0[P][t][1], h0[C][t][1], h0[N][t][1]);
-    between(2);
-    const uint32_t v01 = bop<kXor3>(h1[P][t][1], h1[C][t][1], h1[N][t][1]);
-    const uint32_t v11 = bop<kMaj>(h1[P][t][1], h1[C][t][1], h1[N][t][1]);
-    const uint32_t g11 = bop<kG1>(u11, v01, v11);
-    const uint32_t g21 = bop<kG2>(u01, v11, cc[C][t][1]);
-    const uint32_t n1 = bop<kNext>(u01, g11, g21);
-    between(3);
-    cc[N][t][0] = x.w[0];
-    cc[N][t][1] = x.w[1];
-    x.w[0] = n0;
-    x.w[1] = n1;
-}
-template <int D>
-__device__ __forceinline__ void push_group_spread(Lanes<2> &x0, Lanes<2> &x1, Lanes<2> &x2, uint32_t (&h0)[3][D][2],
-                                                  uint32_t (&h1)[3][D][2], uint32_t (&cc)[3][D][2]) {
-    constexpr SpreadPlan<D> plan;
-    Lanes<2> *xs[3] = {&x0, &x1, &x2};
-    Shifts2 sh[2];
-    parity_fix<1>();
-    static_for<4>([&](auto j) { shift_op(decltype(j)::value, *xs[plan.u[0].row], sh[0]); });
-    static_for<3 * D>([&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        constexpr int R = plan.u[k].row, T = plan.u[k].stage;
-        constexpr bool has_next = k + 1 < 3 * D;
-        constexpr bool inter = has_next && plan.u[k + 1 < 3 * D ? k + 1 : k].row != R;
-        Shifts2 &me = sh[k & 1], &nx = sh[(k + 1) & 1];
-        Lanes<2> &xn = *xs[plan.u[has_next ? k + 1 : k].row];
-        stage_bits2<D, R>(T, *xs[R], me, h0, h1, cc, [&](int c) {
-            if constexpr (inter) {
-                __builtin_amdgcn_sched_barrier(0);
-                shift_op(c, xn, nx);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        });
-        if constexpr (has_next && !inter) static_for<4>([&](auto j) { shift_op(decltype(j)::value, xn, nx); });
-    });
-}
-
 template <int D, int A, int WPL>
 __device__ __forceinline__ void push_group(Lanes<WPL> &x0, Lanes<WPL> &x1, Lanes<WPL> &x2,
                                            uint32_t (&h0)[3][D][WPL], uint32_t (&h1)[3][D][WPL],
                                            uint32_t (&cc)[3][D][WPL]) {
-    if constexpr (GOL_SPREAD && WPL == 2 && A == D) {
-        push_group_spread<D>(x0, x1, x2, h0, h1, cc);
-        return;
-    }
     parity_fix<1>();
 #pragma unroll
     for (int s = 0; s < A + 2; ++s) {
@@ -1402,20 +1284,8 @@ __global__ __launch_bounds__(256) void gol_split_tri_kernel(SplitArgs p) {
 // generation D of [0, H) without wrapping the output; row strips: the
 // halo rows feed the top band's first D rows and the bottom band's drain.
 // ---------------------------------------------------------------------------
-#ifndef GOL_SKEW_PREFETCH
-#define GOL_SKEW_PREFETCH 1  // K1w main loop: load the rows 1 or 2 groups ahead
-#endif
-#ifndef GOL_SKEW_FILL6
-#define GOL_SKEW_FILL6 0  // K1w fill in six-row groups (push_group6_exp)
-#endif
-#ifndef GOL_SKEW_DRAIN6
-#define GOL_SKEW_DRAIN6 0  // K1w drain in six-row groups (push_group6_hi)
-#endif
 #ifndef GOL_SKEW_WAIT_TRACE
 #define GOL_SKEW_WAIT_TRACE 0  // diagnostic builds: per-wave load-wait ticks of K1w (option "trace")
-#endif
-#ifndef GOL_SKEW_HALF4
-#define GOL_SKEW_HALF4 0  // K1w half-wave tiles with four words per lane (A/B builds)
 #endif
 #ifndef GOL_SKEW_STORE_CPOL
 #define GOL_SKEW_STORE_CPOL 16  // K1w output stores sc1 (16384^2 +3.6 %, 8192-row strips +1.9 % in a round-3 A/B whose scratch data was not kept; 0 plain, 2 nt)
@@ -1457,61 +1327,6 @@ __device__ __forceinline__ void push_group_hi(Lanes<WPL> &x0, Lanes<WPL> &x1, La
         if (s < D) stage<D, 0, WPL>(s, x0, h0, h1, cc);
         if (s - 1 >= LO && s - 1 < D) stage<D, 1, WPL>(s - 1, x1, h0, h1, cc);
         if (s - 2 >= LO) stage<D, 2, WPL>(s - 2, x2, h0, h1, cc);
-    }
-}
-
-// push_group_exp for six rows at once (K1w fill, GOL_SKEW_FILL6): row i of
-// the group runs stage s - i at step s, so up to six independent rows share a
-// step (three in push_group) -- the fill's short groups (A = 3, 6, ...
-// stages) otherwise leave the SIMD without independent work at their ends.
-// Rows i and i + 3 have the same ring slot but never the same stage in one
-// step, and row i + 3 overwrites row i's slot of stage t one step after row
-// i + 2 read it there.
-// EXACT (GOL_SKEW_FILL6 == 2; P0 = the group's first input index, known at
-// compile time): row p runs stage t in full only from p = 2t + 2 on (its
-// output, generation t + 1 of row p - t - 1, is then inside the band's
-// parallelogram), only the row sums for p = 2t and 2t + 1 (read by the full
-// stages of the next two rows), and nothing below 2t.
-template <int D, int A, int WPL, int P0 = -1, typename Hook>
-__device__ __forceinline__ void push_group6_exp(Lanes<WPL> (&x)[6], uint32_t (&h0)[3][D][WPL],
-                                                uint32_t (&h1)[3][D][WPL], uint32_t (&cc)[3][D][WPL], int ii0,
-                                                Hook &&hook) {
-    parity_fix<1>();
-#pragma unroll
-    for (int s = 0; s < A + 5; ++s) {
-        if constexpr (WPL <= 2) parity_fix<1>();
-        static_for<6>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            if (s - i >= 0 && s - i < A) {
-                const int t = s - i;
-                if constexpr (P0 < 0) {
-                    hook(t, ii0 + i, x[i]);
-                    stage<D, i % 3, WPL>(t, x[i], h0, h1, cc);
-                } else if (P0 + i >= 2 * t + 2) {
-                    hook(t, ii0 + i, x[i]);
-                    stage<D, i % 3, WPL>(t, x[i], h0, h1, cc);
-                } else if (P0 + i >= 2 * t) {
-                    hook(t, ii0 + i, x[i]);
-                    stage_rowsum<D, i % 3, WPL>(t, x[i], h0, h1, cc);
-                }
-            }
-        });
-    }
-}
-
-// push_group_hi for six rows at once (K1w drain, GOL_SKEW_DRAIN6): the rows
-// enter stage LO, row i at step LO + i (see push_group6_exp).
-template <int D, int LO, int WPL>
-__device__ __forceinline__ void push_group6_hi(Lanes<WPL> (&x)[6], uint32_t (&h0)[3][D][WPL],
-                                               uint32_t (&h1)[3][D][WPL], uint32_t (&cc)[3][D][WPL]) {
-    parity_fix<1>();
-#pragma unroll
-    for (int s = LO; s < D + 5; ++s) {
-        parity_fix<2>();
-        static_for<6>([&](auto ic) {
-            constexpr int i = decltype(ic)::value;
-            if (s - i >= LO && s - i < D) stage<D, i % 3, WPL>(s - i, x[i], h0, h1, cc);
-        });
     }
 }
 
@@ -1626,50 +1441,8 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
             }
         }
     };
-    if constexpr (GOL_SKEW_FILL6 && SP::STEP == 3) {
-        // Six-row fill: each phase A = P(j) < D spans exactly the six input
-        // rows [6 j, 6 j + 6) (the rows below input index 2 A), and the last
-        // phase (A = D) rows [6 NPH, 2 D) rounded up to whole groups of three:
-        // one more six-row group when that is six rows, else the three-row
-        // loop.  Straight-line code (each group runs once); the loads of a
-        // group fetch exactly the rows of the next one.
-        constexpr int LAST6 = 2 * D - 6 * SP::NPH > 3;  // (2D - 6 NPH) in {4, 5, 6}: one six-row group
-        Lanes<WPL> xs[6] = {x0, x1, x2};
-        xs[3] = vmov(load_next());
-        xs[4] = vmov(load_next());
-        xs[5] = vmov(load_next());
-        auto group6 = [&](auto a_tag, auto next6_tag, auto p0_tag) {
-            constexpr int A = decltype(a_tag)::value;
-            constexpr bool NEXT6 = decltype(next6_tag)::value;
-            Lanes<WPL> n[6];
-            static_for<(NEXT6 ? 6 : 3)>([&](auto ic) { n[decltype(ic)::value] = load_next(); });
-            __builtin_amdgcn_sched_barrier(0);
-            Lanes<WPL> y[6] = {xs[0], xs[1], xs[2], xs[3], xs[4], xs[5]};
-            constexpr int P0 = decltype(p0_tag)::value;
-            push_group6_exp<D, A, WPL, (GOL_SKEW_FILL6 >= 2 ? P0 : -1)>(y, h0, h1, cc, k, hook);
-            if constexpr (A == D) static_for<6>([&](auto ic) {
-                constexpr int i = decltype(ic)::value;
-                emit(y[i], k + i - 2 * D);
-            });
-            __builtin_amdgcn_sched_barrier(0);
-            static_for<(NEXT6 ? 6 : 3)>([&](auto ic) { xs[decltype(ic)::value] = vmov(n[decltype(ic)::value]); });
-            k += 6;
-        };
-        static_for<SP::NPH>([&](auto j) {
-            constexpr int J = decltype(j)::value;
-            group6(std::integral_constant<int, SP::P(J)>(),
-                   std::integral_constant<bool, (J + 1 < SP::NPH) || LAST6>(), std::integral_constant<int, 6 * J>());
-        });
-        if constexpr (LAST6)
-            group6(std::integral_constant<int, D>(), std::false_type(), std::integral_constant<int, 6 * SP::NPH>());
-        x0 = xs[0];
-        x1 = xs[1];
-        x2 = xs[2];
-        if constexpr (!LAST6) fill(std::integral_constant<int, D>());
-    } else {
-        static_for<SP::NPH>([&](auto j) { fill(std::integral_constant<int, SP::P(decltype(j)::value)>()); });
-        fill(std::integral_constant<int, D>());
-    }
+    static_for<SP::NPH>([&](auto j) { fill(std::integral_constant<int, SP::P(decltype(j)::value)>()); });
+    fill(std::integral_constant<int, D>());
     if (phase_tr && lane == 0) phase_tr[0] = (unsigned long long)__builtin_amdgcn_s_memrealtime();  // fill done
     // exports done: this wave's LDS writes complete before the flag (LDS
     // operations of a wave complete in order; no wait on its global loads)
@@ -1683,79 +1456,27 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
     // main: every stage on board rows (the bottom band of a stack to the end)
     const int kmain = S + (self ? 2 * D : 2 * SP::P(0));
     for (int i = 0; i < GOL_LOOP_PAD; ++i) asm volatile("s_nop 0");
-    if constexpr (GOL_SKEW_PREFETCH >= 2) {
-        // loads two groups ahead: each group's rows have two groups of compute
-        // to land.  Two groups a body with the two load sets alternating (a
-        // register copy of a pending load would wait for it).
-        // An odd group count runs its first group as the one-ahead body (no
-        // exit in the middle of the loop: it would cost conservative waits).
-        if ((((kmain - k) + 2) / 3) & 1) {
-            const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
-            emit(q0, qoi);
-            emit(q1, qoi + 1);
-            emit(q2, qoi + 2);
-            __builtin_amdgcn_sched_barrier(0);
-            Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
-            push_group<D, D, WPL>(y0, y1, y2, h0, h1, cc);
-            q0 = y0;
-            q1 = y1;
-            q2 = y2;
-            qoi = k - 2 * D;
-            __builtin_amdgcn_sched_barrier(0);
-            x0 = vmov(n0);
-            x1 = vmov(n1);
-            x2 = vmov(n2);
-            k += 3;
-        }
-        Lanes<WPL> a0 = load_next(), a1 = load_next(), a2 = load_next(), b0, b1, b2;
-        auto body = [&](Lanes<WPL> &n0, Lanes<WPL> &n1, Lanes<WPL> &n2, Lanes<WPL> &c0, Lanes<WPL> &c1,
-                        Lanes<WPL> &c2) {
-            n0 = load_next();
-            n1 = load_next();
-            n2 = load_next();
-            emit(q0, qoi);
-            emit(q1, qoi + 1);
-            emit(q2, qoi + 2);
-            __builtin_amdgcn_sched_barrier(0);
-            Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
-            push_group<D, D, WPL>(y0, y1, y2, h0, h1, cc);
-            q0 = y0;
-            q1 = y1;
-            q2 = y2;
-            qoi = k - 2 * D;
-            __builtin_amdgcn_sched_barrier(0);
-            x0 = vmov(c0);
-            x1 = vmov(c1);
-            x2 = vmov(c2);
-            k += 3;
-        };
-        while (k < kmain) {  // an even number of groups is left
-            body(b0, b1, b2, a0, a1, a2);
-            body(a0, a1, a2, b0, b1, b2);
-        }
-    } else {
-        for (; k < kmain; k += 3) {
-            const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
-            emit(q0, qoi);
-            emit(q1, qoi + 1);
-            emit(q2, qoi + 2);
-            __builtin_amdgcn_sched_barrier(0);
-            Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
-            push_group<D, D, WPL>(y0, y1, y2, h0, h1, cc);
-            q0 = y0;
-            q1 = y1;
-            q2 = y2;
-            qoi = k - 2 * D;
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (GOL_SKEW_WAIT_TRACE) wt0 = __builtin_amdgcn_s_memrealtime();
-            x0 = vmov(n0);
-            x1 = vmov(n1);
-            x2 = vmov(n2);
-            if constexpr (GOL_SKEW_WAIT_TRACE) {
-                asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // the rows have landed
-                wmain += __builtin_amdgcn_s_memrealtime() - wt0;
-                ++nmain;
-            }
+    for (; k < kmain; k += 3) {
+        const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
+        emit(q0, qoi);
+        emit(q1, qoi + 1);
+        emit(q2, qoi + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
+        push_group<D, D, WPL>(y0, y1, y2, h0, h1, cc);
+        q0 = y0;
+        q1 = y1;
+        q2 = y2;
+        qoi = k - 2 * D;
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (GOL_SKEW_WAIT_TRACE) wt0 = __builtin_amdgcn_s_memrealtime();
+        x0 = vmov(n0);
+        x1 = vmov(n1);
+        x2 = vmov(n2);
+        if constexpr (GOL_SKEW_WAIT_TRACE) {
+            asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // the rows have landed
+            wmain += __builtin_amdgcn_s_memrealtime() - wt0;
+            ++nmain;
         }
     }
     if constexpr (GOL_SKEW_WAIT_TRACE) {
@@ -1826,67 +1547,10 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
                 x2 = vmov(n2);
             }
         };
-        if constexpr (GOL_SKEW_DRAIN6 && SP::STEP == 3) {
-            // Six-row drain: drain phase J spans exactly the six pushes
-            // [S + 2 P(J), S + 2 P(J + 1)); the last phase [S + 2 P(NPH-1), S + 2 D)
-            // is one six-row group when it is 4-6 pushes, else the three-row loop.
-            constexpr bool LAST6 = 2 * (D - SP::STEP * SP::NPH) > 3;
-            constexpr int N6 = LAST6 ? SP::NPH : SP::NPH - 1;  // phases run as six-row groups
-            Lanes<WPL> xs[6], qs[6];
-            {
-                Lanes<WPL> n[6];
-                imports(k + 3, n[3], n[4], n[5]);
-                xs[0] = x0;
-                xs[1] = x1;
-                xs[2] = x2;
-                static_for<3>([&](auto ic) { xs[3 + decltype(ic)::value] = vmov(n[3 + decltype(ic)::value]); });
-            }
-            qs[0] = q0;
-            qs[1] = q1;
-            qs[2] = q2;
-            int npend = 3;  // stores pending from the main loop
-            auto group6 = [&](auto lo_tag, auto next6_tag) {
-                constexpr int LO = decltype(lo_tag)::value;
-                constexpr bool NEXT6 = decltype(next6_tag)::value;
-                Lanes<WPL> n[6];
-                imports(k + 6, n[0], n[1], n[2]);
-                if constexpr (NEXT6) imports(k + 9, n[3], n[4], n[5]);
-                __builtin_amdgcn_sched_barrier(0);
-                Lanes<WPL> y[6] = {xs[0], xs[1], xs[2], xs[3], xs[4], xs[5]};
-                push_group6_hi<D, LO, WPL>(y, h0, h1, cc);
-                __builtin_amdgcn_sched_barrier(0);
-                static_for<6>([&](auto ic) {
-                    constexpr int i = decltype(ic)::value;
-                    if (i < npend) emit(qs[i], qoi + i);
-                    qs[i] = y[i];
-                });
-                npend = 6;
-                qoi = k - 2 * D;
-                __builtin_amdgcn_sched_barrier(0);
-                static_for<(NEXT6 ? 6 : 3)>([&](auto ic) { xs[decltype(ic)::value] = vmov(n[decltype(ic)::value]); });
-                k += 6;
-            };
-            static_for<N6>([&](auto j) {
-                constexpr int J = decltype(j)::value;
-                group6(std::integral_constant<int, SP::P(J)>(), std::integral_constant<bool, (J + 1 < N6)>());
-            });
-            if constexpr (!LAST6) {  // the last phase on three-row groups
-                static_for<6>([&](auto ic) { emit(qs[decltype(ic)::value], qoi + decltype(ic)::value); });
-                x0 = xs[0];
-                x1 = xs[1];
-                x2 = xs[2];
-                qoi = -8;  // nothing pending
-                drain(std::integral_constant<int, SP::P(SP::NPH - 1)>(), S + 2 * D);
-            } else {
-                static_for<6>([&](auto ic) { emit(qs[decltype(ic)::value], qoi + decltype(ic)::value); });
-                return cnt;
-            }
-        } else {
-            static_for<SP::NPH>([&](auto j) {
-                constexpr int J = decltype(j)::value;
-                drain(std::integral_constant<int, SP::P(J)>(), S + 2 * (J + 1 < SP::NPH ? SP::P(J + 1) : D));
-            });
-        }
+        static_for<SP::NPH>([&](auto j) {
+            constexpr int J = decltype(j)::value;
+            drain(std::integral_constant<int, SP::P(J)>(), S + 2 * (J + 1 < SP::NPH ? SP::P(J + 1) : D));
+        });
     }
     emit(q0, qoi);
     emit(q1, qoi + 1);
@@ -1894,20 +1558,18 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
     return cnt;
 }
 
-// K1w: one workgroup = one stack = tx tiles x (NW / tx) bands; wave w takes
-// tile w % tx and stack position w / tx (top to bottom).  NW = 8 waves (two
-// per SIMD); NW = 12 (three per SIMD, round 4) for the depths whose
-// pipelines fit 168 VGPRs: wave w sits on SIMD w % 4 with age rank w / 4.
-template <int D, int WPL, bool HALF = false, int NW = 8>
-__global__ __launch_bounds__(NW * 64) void gol_skew_kernel(SkewArgs p) {
+// K1w: one workgroup = one stack = tx tiles x (8 / tx) bands; wave w takes
+// tile w % tx and stack position w / tx (top to bottom).
+template <int D, int WPL, bool HALF = false>
+__global__ __launch_bounds__(512) void gol_skew_kernel(SkewArgs p) {
     using SP = SkewPlan<D>;
     constexpr int ROW = 64 * WPL;
-    __shared__ uint32_t s_exp[NW][(SP::NEXP + 1) * ROW];
-    __shared__ int s_flag[NW];
+    __shared__ uint32_t s_exp[8][(SP::NEXP + 1) * ROW];
+    __shared__ int s_flag[8];
     __shared__ unsigned long long s_cnt;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int sy = NW / p.tx;
+    const int sy = 8 / p.tx;
     const int tcols = (p.tiles_x + p.tx - 1) / p.tx;
     const int stack = blockIdx.x / tcols, tc = blockIdx.x - stack * tcols;
     const int tile = tc * p.tx + w % p.tx, pos = w / p.tx;
@@ -1915,7 +1577,7 @@ __global__ __launch_bounds__(NW * 64) void gol_skew_kernel(SkewArgs p) {
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
     if (tile >= p.tiles_x) return;  // wave-uniform, after the only barrier (its stack's waves all leave)
-    if (NW == 8 && p.prio_young && w >= 4) __builtin_amdgcn_s_setprio(1);
+    if (p.prio_young && w >= 4) __builtin_amdgcn_s_setprio(1);
     // HALF: the stacks split the first half of the rows; each wave's upper
     // lanes take the same band L / 2 rows further down (L even, host-checked)
     const int L = HALF ? p.base.rows_out / 2 : p.base.rows_out;
@@ -2206,43 +1868,35 @@ hipError_t launch_split(const SplitArgs &p, int depth, int wpl, hipStream_t s) {
 }
 
 template <typename F>
-static hipError_t dispatch_skew(int depth, int wpl, bool half, int nw, F &&f) {
+static hipError_t dispatch_skew(int depth, int wpl, bool half, F &&f) {
 #define GOL_WCASE(D, WP) \
-    if (nw == 8 && !half && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP>);
+    if (!half && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP>);
 #define GOL_HCASE(D, WP) \
-    if (nw == 8 && half && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP, true>);
-#define GOL_NCASE(D, WP, H, N) \
-    if (nw == N && half == H && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP, H, N>);
-    GOL_NCASE(12, 2, false, 12) GOL_NCASE(12, 2, true, 12)
+    if (half && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP, true>);
     GOL_WCASE(8, 2) GOL_WCASE(12, 2) GOL_WCASE(16, 2) GOL_WCASE(20, 2) GOL_WCASE(6, 4) GOL_WCASE(8, 4)
     GOL_WCASE(9, 4) GOL_WCASE(16, 1) GOL_WCASE(32, 1)
     GOL_HCASE(16, 2) GOL_HCASE(20, 2)
-#if GOL_SKEW_HALF4
-    GOL_HCASE(8, 4) GOL_HCASE(9, 4)
-#endif
 #undef GOL_WCASE
 #undef GOL_HCASE
-#undef GOL_NCASE
     return hipErrorInvalidValue;
 }
 
-bool skew_supported(int depth, int wpl, bool half, int nw) {
-    return dispatch_skew(depth, wpl, half, nw, [](auto) { return hipSuccess; }) == hipSuccess;
+bool skew_supported(int depth, int wpl, bool half) {
+    return dispatch_skew(depth, wpl, half, [](auto) { return hipSuccess; }) == hipSuccess;
 }
 
-int skew_blocks_per_cu(int depth, int wpl, bool half, int nw) {
+int skew_blocks_per_cu(int depth, int wpl, bool half) {
     int b = 0;
-    hipError_t e = dispatch_skew(depth, wpl, half, nw, [&](auto kern) {
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 64 * nw, 0);
+    hipError_t e = dispatch_skew(depth, wpl, half, [&](auto kern) {
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 512, 0);
     });
     return e == hipSuccess ? b : 0;
 }
 
 hipError_t launch_skew(const SkewArgs &p, int depth, int wpl, hipStream_t s) {
     const int tcols = (p.tiles_x + p.tx - 1) / p.tx;
-    const int nw = p.nw > 0 ? p.nw : 8;
-    return dispatch_skew(depth, wpl, p.half != 0, nw, [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(tcols * p.nst), dim3(64 * nw), 0, s, p);
+    return dispatch_skew(depth, wpl, p.half != 0, [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(tcols * p.nst), dim3(512), 0, s, p);
         return hipGetLastError();
     });
 }
@@ -3045,10 +2699,7 @@ const char *build_info() {
            " GOL_PERSIST_STORE=" GOL_STR(GOL_PERSIST_STORE) " GOL_PAIR_STORE=" GOL_STR(GOL_PAIR_STORE)
            " GOL_PAIR_G2=" GOL_STR(GOL_PAIR_G2) " GOL_FILL_PHASES=" GOL_STR(GOL_FILL_PHASES)
            " GOL_SKEW_STORE_CPOL=" GOL_STR(GOL_SKEW_STORE_CPOL) " GOL_PERSIST_WG_COUNT=" GOL_STR(GOL_PERSIST_WG_COUNT)
-           " GOL_COMPACT_WPT=" GOL_STR(GOL_COMPACT_WPT) " GOL_SKEW_PREFETCH=" GOL_STR(GOL_SKEW_PREFETCH)
-           " GOL_SKEW_FILL6=" GOL_STR(GOL_SKEW_FILL6) " GOL_SKEW_DRAIN6=" GOL_STR(GOL_SKEW_DRAIN6)
-           " GOL_SKEW_WAIT_TRACE=" GOL_STR(GOL_SKEW_WAIT_TRACE) " GOL_SKEW_HALF4=" GOL_STR(GOL_SKEW_HALF4)
-           " GOL_SPREAD=" GOL_STR(GOL_SPREAD);
+           " GOL_COMPACT_WPT=" GOL_STR(GOL_COMPACT_WPT) " GOL_SKEW_WAIT_TRACE=" GOL_STR(GOL_SKEW_WAIT_TRACE);
 }
 
 }  // namespace golk

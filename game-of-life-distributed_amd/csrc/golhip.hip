@@ -126,10 +126,7 @@ struct golhip {
     int skew_tx = 0;                // option "skew_tx": tiles per K1w workgroup (0: plan, 1 or 2)
     int skew_half = 0;              // option "skew_half": half-wave tiles (0: when fewer wave-rows, 1: whenever possible, -1: never)
     int skew_nst = 0;               // option "skew_nst" (measurement): stacks per tile column (0: plan)
-    int skew_bpc[kNumDepths][12] = {};  // K1w workgroups per CU by (depth, wpl, half, nw) (0: not queried)
-    int skew_waves = 8;             // option "skew_waves": waves per K1w workgroup (8: two per SIMD; 12: three,
-                                    // for the depths that have such an instance)
-    int skew_mid = 0;               // option "skew_mid": band height of the middle age rank (12-wave stacks), %
+    int skew_bpc[kNumDepths][6] = {};  // K1w workgroups per CU by (depth, wpl, half) (0: not queried)
     unsigned *skew_err = nullptr;      // host-mapped spin-bound flag of the K1w kernels
     unsigned *skew_err_dev = nullptr;
     int64_t skew_launches = 0;
@@ -653,10 +650,10 @@ int split_buffers(golhip_t h, golk::SplitArgs &sp, int depth, int wpl) {
 // band below's exports) and the stack's bottom band `hcap` rows shorter (it
 // computes its drain in full).  tx = 2 (stacks of 4
 // bands, two tiles a workgroup) when the tile count fits the CUs better.
-int skew_bpc(golhip_t h, int depth, int wpl, bool half, int nw = 8) {
-    int &c = h->skew_bpc[depth_index(depth)][(wpl == 4 ? 2 : wpl - 1) + (half ? 3 : 0) + (nw == 12 ? 6 : 0)];
+int skew_bpc(golhip_t h, int depth, int wpl, bool half) {
+    int &c = h->skew_bpc[depth_index(depth)][(wpl == 4 ? 2 : wpl - 1) + (half ? 3 : 0)];
     if (c == 0) {
-        const int b = golk::skew_blocks_per_cu(depth, wpl, half, nw);
+        const int b = golk::skew_blocks_per_cu(depth, wpl, half);
         c = b > 0 ? b : -1;
     }
     return c;
@@ -666,26 +663,24 @@ int skew_bpc(golhip_t h, int depth, int wpl, bool half, int nw = 8) {
 // and tile kind (no side effects); false if K1w does not apply.
 bool skew_dims(golhip_t h, int depth, int wpl, int L, golk::SkewArgs *sk) {
     if (!h->skew || h->W % 32 != 0 || !golk::skew_supported(depth, wpl)) return false;
-    // three waves per SIMD (12-wave stacks) where the option asks and an instance exists
-    const int nw = (h->skew_waves == 12 && golk::skew_supported(depth, wpl, false, 12)) ? 12 : 8;
     const int hcap = h->skew_hcap >= 0 ? h->skew_hcap : 3 * depth / 4;
     const int smin = depth + 3;
     // half-wave tiles (30 stored lanes a tile, two tiles a wave, the upper one
     // L / 2 rows down): when they need fewer wave-rows than 62-lane tiles
     // (16384^2: 4.5 vs 5 waves a row), or when forced; L must be even
-    const bool half_ok = h->skew_half >= 0 && L % 2 == 0 && golk::skew_supported(depth, wpl, true, nw);
+    const bool half_ok = h->skew_half >= 0 && L % 2 == 0 && golk::skew_supported(depth, wpl, true);
     int best_tx = 0, best_nst = 0, best_half = 0, best_tiles = 0;
     double best = 1e300;
     for (int half = 0; half <= (half_ok ? 1 : 0); ++half) {
         if (!half && half_ok && h->skew_half > 0) continue;  // forced
-        const int bpc = skew_bpc(h, depth, wpl, half, nw);
+        const int bpc = skew_bpc(h, depth, wpl, half);
         if (bpc < 1) continue;
         const int tiles = half ? (h->Ww + golk::kHalfTileValid * wpl - 1) / (golk::kHalfTileValid * wpl)
                                : golk::tb_tiles(h->Ww, wpl);
         const int Lh = half ? L / 2 : L;
         for (int tx = 1; tx <= 2; ++tx) {
             if (h->skew_tx && tx != h->skew_tx) continue;
-            const int sy = nw / tx, tcols = (tiles + tx - 1) / tx;
+            const int sy = 8 / tx, tcols = (tiles + tx - 1) / tx;
             // stacks of Lh / nst + hcap rows whose bands average at least smin + hcap
             // rows (the bottom band gives up hcap of them)
             const int nst = std::min(h->cu_count * bpc / tcols,
@@ -710,7 +705,6 @@ bool skew_dims(golhip_t h, int depth, int wpl, int L, golk::SkewArgs *sk) {
     }
     if (!best_tx) return false;
     sk->tiles_x = best_tiles;
-    sk->nw = nw;
     sk->tx = best_tx;
     sk->nst = best_nst;
     sk->half = best_half;
@@ -744,23 +738,13 @@ bool skew_plan(golhip_t h, int depth, int wpl, const golk::StepArgs &a, golk::Sk
         h->skew_err_dev = static_cast<unsigned *>(d);
         *h->skew_err = 0;
     }
-    const int sy = sk->nw / sk->tx;
+    const int sy = 8 / sk->tx;
     // The SIMD arbiter serves the older wave of a SIMD (waves 0..3) first: the
     // younger waves' bands are shorter so both finish together.  Measured
     // (round-3 skew_young sweeps, scripts/sweep_opts.py): two words per lane
-    // 66-70 %, quads at depth 9 76-82 %.  12-wave stacks: three age ranks
-    // (waves 0-3, 4-7, 8-11 of a SIMD), weights 100 / mid / young.
-    if (sk->nw == 12) {
-        const int young = h->skew_young > 0 ? h->skew_young : 70;
-        const int mid = h->skew_mid > 0 ? h->skew_mid : 85;
-        for (int q = 0; q < 12; ++q) {
-            const int rank = (q * sk->tx) / 4;
-            sk->wgt[q] = q >= sy ? 100 : rank == 0 ? 100 : rank == 1 ? mid : young;
-        }
-    } else {
-        const int young = h->skew_young > 0 ? h->skew_young : wpl == 4 ? 78 : 68;
-        for (int q = 0; q < 12; ++q) sk->wgt[q] = (q < sy && q * sk->tx >= 4) ? young : 100;
-    }
+    // 66-70 %, quads at depth 9 76-82 %.
+    const int young = h->skew_young > 0 ? h->skew_young : wpl == 4 ? 78 : 68;
+    for (int q = 0; q < 8; ++q) sk->wgt[q] = (q < sy && q * sk->tx >= 4) ? young : 100;
     sk->prio_young = h->skew_prio;
     sk->error = h->skew_err_dev;
     sk->trace = h->d_trace;
@@ -1706,17 +1690,6 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     if (!strcmp(key, "skew_half")) {
         if (value < -1 || value > 1) return fail(GOLHIP_EINVAL, "skew_half %lld", (long long)value);
         h->skew_half = (int)value;
-        return GOLHIP_OK;
-    }
-    if (!strcmp(key, "skew_waves")) {
-        if (value != 8 && value != 12) return fail(GOLHIP_EINVAL, "skew_waves %lld (8 or 12)", (long long)value);
-        h->skew_waves = (int)value;
-        for (int &c : h->auto_rpw) c = 0;
-        return GOLHIP_OK;
-    }
-    if (!strcmp(key, "skew_mid")) {
-        if (value < 0 || value > 400) return fail(GOLHIP_EINVAL, "skew_mid %lld", (long long)value);
-        h->skew_mid = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "skew_tx")) {

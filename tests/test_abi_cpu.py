@@ -125,7 +125,7 @@ def test_product_build_macros():
     info = golhip.load().golhip_build_info().decode()
     want = {"GOL_LOOP_PAD": "0", "GOL_PARITY_FIX": "1", "GOL_PERSIST_STORE": "6", "GOL_PAIR_STORE": "-1",
             "GOL_PAIR_G2": "0", "GOL_FILL_PHASES": "4", "GOL_SKEW_STORE_CPOL": "16", "GOL_PERSIST_WG_COUNT": "1",
-            "GOL_COMPACT_WPT": "4", "GOL_SKEW_PREFETCH": "1", "GOL_SKEW_FILL6": "0", "GOL_SKEW_DRAIN6": "0", "GOL_SKEW_WAIT_TRACE": "0", "GOL_SKEW_HALF4": "0", "GOL_SPREAD": "0"}
+            "GOL_COMPACT_WPT": "4", "GOL_SKEW_WAIT_TRACE": "0"}
     got = dict(kv.split("=", 1) for kv in info.split())
     assert got == want, info
 

@@ -209,51 +209,6 @@ def test_skew_half_tiles_match_oracle(coracle, depth, W, H, tx):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("W,H", [(2048, 1024), (8192, 331), (3968, 2500), (16384, 1600), (65536, 700)])
-@pytest.mark.parametrize("half", [-1, 1])
-def test_skew_three_waves_per_simd_match_oracle(coracle, W, H, half):
-    """12-wave stacks (option skew_waves=12: three waves per SIMD, depth 12),
-    full and half-wave tiles, torus seam and ragged columns."""
-    board = coracle.fill_random(W, H, 0x5EED0048 + W + H)
-    turns = 2 * 12 + 5
-    want = coracle.run(board, turns)
-    got, p = run_skew(board, turns, 12, 2, skew_waves=12, skew_half=half)
-    assert p["skew_launches"] >= 2
-    assert np.array_equal(got, want)
-
-
-@pytest.mark.parametrize("W,H", [(16384, 3000), (65536, 1200)])
-def test_skew_three_waves_rccl_ring_one_rank(coracle, W, H):
-    board = coracle.fill_random(W, H, 0x5EED0049 + W)
-    turns = 100
-    want = coracle.run(board, turns)
-    with golhip.Board(W, H) as b:
-        b.comm_init(golhip.unique_id(), 1, 0)
-        b.set_option("force_halo", 1)
-        b.set_option("skew", 2)
-        b.set_option("skew_waves", 12)
-        b.set_tb_depth(12)
-        b.load_bytes(board)
-        b.step(turns)
-        assert b.perf()["skew_launches"] >= 1
-        assert np.array_equal(b.snapshot_bytes(), want)
-
-
-@pytest.mark.parametrize("depth", [9, 8])
-@pytest.mark.parametrize("W,H", [(16384, 1000), (5120, 2222), (3072, 1502), (2048, 818)])
-def test_skew_half_quad_tiles_match_oracle(coracle, depth, W, H):
-    """Half-wave tiles with four words per lane (30 stored lanes x 4 words a
-    half tile; builds with GOL_SKEW_HALF4)."""
-    if "GOL_SKEW_HALF4=1" not in golhip.load().golhip_build_info().decode():
-        pytest.skip("build without half-wave quad tiles")
-    board = coracle.fill_random(W, H, 0x5EED0047 + W + H + depth)
-    turns = 2 * depth + 5
-    want = coracle.run(board, turns)
-    got, p = run_skew(board, turns, depth, 4, skew_half=1)
-    assert p["skew_half_launches"] >= 2
-    assert np.array_equal(got, want)
-
-
 def test_skew_half_tiles_need_even_rows(coracle):
     """An odd number of rows cannot split into two equal halves: full tiles."""
     board = coracle.fill_random(16384, 1001, 0x5EED0042)
