@@ -6,6 +6,7 @@
 #   trace[:<workload>]         rocprofv3 --kernel-trace --stats of that bench command
 #   pmc[:<workload>]           FETCH / WRITE / SQ passes (scripts/pmc_bench.sh)
 #   stalls[:<workload>]        SQ wait / active / instruction-mix passes (scripts/pmc_stalls.sh)
+#   selflaunch                 bench.py --gpus 2 on this box (fewer devices than ranks: JSON error, exit 2)
 #   py:<script args...>        any repo script, e.g. py:scripts/bench_strip.py (commas in
 #                              the argument list stand for spaces)
 # Every GPU step runs under its own time limit; the first failure ends the call.
@@ -47,6 +48,10 @@ for st in "$@"; do
       bash scripts/pmc_bench.sh $out ${arg:-65536} || exit 1 ;;
     stalls)
       bash scripts/pmc_stalls.sh $out gol_ --workload ${arg:-65536} || exit 1 ;;
+    selflaunch)
+      # bench.py --gpus 2 without a launcher on a 1-GPU box: must fail fast with a JSON error line (exit 2)
+      timeout -k 10 120 python -u bench.py --gpus 2 --steps 1 > $out/selflaunch.json 2> $out/selflaunch.err; rc=$?
+      cat $out/selflaunch.json; [ $rc -eq 2 ] || { echo "selflaunch exit $rc"; exit 1; } ;;
     py)
       a=${arg//,/ }
       timeout -k 10 600 python -u $a > $out/py_$(basename ${a%% *} .py).log 2>&1 \
