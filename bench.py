@@ -294,7 +294,7 @@ def events_main(a) -> None:
     wl = WORKLOADS[5120]
     N, tps = 5120, a.turns_per_step or wl["turns"]
     with open(FULLSIZE) as f:
-        rec = json.load(f)["c4"]
+        rec = c4 = json.load(f)["c4"]
     cap = 32 << 20
     # parity: turns 1..T of the fixture, pairs
     T = len(rec["flip_counts"])
@@ -386,7 +386,7 @@ def events_main(a) -> None:
                                   "peak_GBps": HBM_PEAK_GBS, "source": os.path.relpath(a.pmc, ROOT),
                                   "note": "FETCH_SIZE x2 + WRITE_SIZE; the entries go to page-locked host memory"}
     if a.e2e_turns > 0:
-        out["end_to_end"] = events_end_to_end(rec, a.e2e_turns)
+        out["end_to_end"] = events_end_to_end(c4, a.e2e_turns)
         parity["ok"] = parity["ok"] and out["end_to_end"]["parity"]
         out["parity"] = parity["ok"]
     if not a.no_cpu_baseline:
@@ -415,12 +415,13 @@ def events_end_to_end(rec: dict, T: int) -> dict:
     with tempfile.TemporaryDirectory() as root:
         write_images(root, {f"{N}x{N}": board})
         del board
-        t0 = time.perf_counter()
-        r = golhip.Run(T, 8, N, N, root, events_cap=1000)
-        counts, last, final_alive, flips, digests = r.drain(T, N)
-        err = r.wait()
-        r.close()
-        dt = time.perf_counter() - t0
+        with StdoutToStderr():
+            t0 = time.perf_counter()
+            r = golhip.Run(T, 8, N, N, root, events_cap=1000)
+            counts, last, final_alive, flips, digests = r.drain(T, N)
+            err = r.wait()
+            r.close()
+            dt = time.perf_counter() - t0
     ok = (not err and last == T and [int(x) for x in flips] == rec["flip_counts"][:T]
           and [f"{int(x):016x}" for x in digests] == rec["flip_digests"][:T]
           and counts["CellFlipped"] == rec["initial_alive"] + sum(rec["flip_counts"][:T]))
@@ -565,6 +566,26 @@ def launch_ranks(a, cmd: list | None = None, n_devices: int | None = None) -> in
     return 0
 
 
+class StdoutToStderr:
+    """The host mirror prints the io goroutine's "File ... done!" lines
+    (io.go:86, :125) on the C stdout; during the timed runs they go to stderr
+    so the bench's stdout holds only its JSON line."""
+
+    def __enter__(self):
+        import ctypes
+        self.libc = ctypes.CDLL(None)
+        sys.stdout.flush()
+        self.libc.fflush(None)
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        self.libc.fflush(None)
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def write_images(root: str, names: dict) -> None:
     """images/<name>.pgm under `root` (the reference's io.go reads them from images/)."""
     from oracle.oracle import pgm_bytes
@@ -600,8 +621,8 @@ def run_main(a) -> None:
     with tempfile.TemporaryDirectory() as root:
         write_images(root, {"512x512": board})
 
-        def one():
-            r = golhip.Run(T, 8, N, N, root)
+        def one(cap):
+            r = golhip.Run(T, 8, N, N, root, events_cap=cap)
             counts, last, final_alive, _, _ = r.drain(0, 0)
             err = r.wait()
             r.close()
@@ -609,14 +630,22 @@ def run_main(a) -> None:
                 raise RuntimeError(err)
             return counts, last, final_alive
 
-        for _ in range(max(1, a.warmup)):
-            one()
-        times, res = [], None
-        for _ in range(a.steps):
-            t0 = time.perf_counter()
-            res = one()
-            times.append(time.perf_counter() - t0)
+        with StdoutToStderr():
+            for _ in range(max(1, a.warmup)):
+                one(0)
+            times, res = [], None
+            for _ in range(a.steps):
+                t0 = time.perf_counter()
+                res = one(0)
+                times.append(time.perf_counter() - t0)
+            btimes = []  # main.go's capacity-1000 events channel (main.go:53)
+            for _ in range(a.steps):
+                t0 = time.perf_counter()
+                bres = one(1000)
+                btimes.append(time.perf_counter() - t0)
         counts, last, final_alive = res
+        if bres != res:
+            raise RuntimeError(f"buffered run differs: {bres} vs {res}")
         with open(os.path.join(root, "out", f"{N}x{N}x{T}.pgm"), "rb") as f:
             sha = hashlib.sha256(f.read()).hexdigest()
     dt = sum(times)
@@ -636,6 +665,10 @@ def run_main(a) -> None:
                             "PGM write, close"},
         "runs_per_s": round(a.steps / dt, 2),
         "ms_per_run_min": round(min(times) * 1e3, 3),
+        "events_channel": "unbuffered (gol_test.go:15-47's make(chan gol.Event)): every send waits for the receive",
+        "buffered_1000": {"gcups": round(N * N * T * a.steps / sum(btimes) / 1e9, 4),
+                          "ms_per_run": round(sum(btimes) / a.steps * 1e3, 3),
+                          "note": "main.go:53's make(chan gol.Event, 1000), same events, same parity"},
     }
     if not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_config0()

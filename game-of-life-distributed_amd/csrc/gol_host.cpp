@@ -601,16 +601,20 @@ int golrun_drain(golrun_t r, golrun_drain_stats_t *st, uint64_t *flips, uint64_t
         z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
         return z ^ (z >> 31);
     };
-    gol::Event e;
-    while (r->events.recv(e)) {  // main.go:59-66, until close
-        const int k = (int)e.kind;
-        if (k >= 0 && k < 6) st->count[k]++;
-        if (e.kind == gol::EventKind::TurnComplete) st->last_turn = e.CompletedTurns;
-        if (e.kind == gol::EventKind::FinalTurnComplete) st->final_alive = (int64_t)e.Alive.size();
-        if (e.kind != gol::EventKind::CellFlipped || e.CompletedTurns < 1 || e.CompletedTurns > turns_cap) continue;
-        const int64_t t = e.CompletedTurns - 1;
-        const uint64_t i = flips ? ++flips[t] : 0;
-        if (digests) digests[t] += mix(i) * ((uint64_t)e.Cell.Y * (uint64_t)width + (uint64_t)e.Cell.X + 1);
+    std::vector<gol::Event> batch;
+    batch.reserve(1024);
+    while (r->events.recv_batch(batch, 1024)) {  // main.go:59-66, until close (every event, in order)
+        for (const gol::Event &e : batch) {
+            const int k = (int)e.kind;
+            if (k >= 0 && k < 6) st->count[k]++;
+            if (e.kind == gol::EventKind::TurnComplete) st->last_turn = e.CompletedTurns;
+            if (e.kind == gol::EventKind::FinalTurnComplete) st->final_alive = (int64_t)e.Alive.size();
+            if (e.kind != gol::EventKind::CellFlipped || e.CompletedTurns < 1 || e.CompletedTurns > turns_cap)
+                continue;
+            const int64_t t = e.CompletedTurns - 1;
+            const uint64_t i = flips ? ++flips[t] : 0;
+            if (digests) digests[t] += mix(i) * ((uint64_t)e.Cell.Y * (uint64_t)width + (uint64_t)e.Cell.X + 1);
+        }
     }
     return GOLHIP_OK;
 }

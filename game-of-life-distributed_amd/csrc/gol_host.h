@@ -123,6 +123,29 @@ class Chan {
         take(out);
         return true;
     }
+    // Blocks for the first value like recv, then takes every value already
+    // queued too (at most `max`), in order: one lock per batch for a
+    // consumer of a buffered channel (main.go's capacity-1000 events
+    // channel).  Returns the count; 0 once closed and drained.
+    size_t recv_batch(std::vector<T> &out, size_t max) {
+        out.clear();
+        spin([&] { return closed_a_.load(std::memory_order_acquire) ||
+                          sent_a_.load(std::memory_order_acquire) != received_a_.load(std::memory_order_acquire); });
+        std::unique_lock<std::mutex> lk(mu_);
+        if (!closed_ && q_.empty()) {
+            ++recv_sleepers_;
+            recv_cv_.wait(lk, [&] { return closed_ || !q_.empty(); });
+            --recv_sleepers_;
+        }
+        while (!q_.empty() && out.size() < max) {
+            out.push_back(std::move(q_.front()));
+            q_.pop_front();
+        }
+        received_ += out.size();
+        received_a_.store(received_, std::memory_order_release);
+        if (send_sleepers_ && !out.empty()) send_cv_.notify_all();
+        return out.size();
+    }
     // Non-blocking receive: 1 = got one, 0 = empty, -1 = closed and drained.
     int try_recv(T &out) {
         std::lock_guard<std::mutex> lk(mu_);

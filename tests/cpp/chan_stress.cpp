@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <thread>
 #include <vector>
+#include <vector>
 
 #include "gol_host.h"
 
@@ -28,12 +29,22 @@ static int run(size_t cap, int senders, int per_sender) {
         ch.close();
     });
     int64_t v, n = 0;
-    while (ch.recv(v)) {
+    std::vector<int64_t> batch;
+    auto take = [&](int64_t v) {
         const int s = (int)(v >> 32), i = (int)(v & 0xffffffff);
         if (s < 0 || s >= senders || next[s] != i) order_errors++;
         else next[s]++;
         received_count++;
         n++;
+    };
+    for (bool more = true; more;) {  // alternate single and batched receives
+        if (n % 2 == 0) {
+            more = ch.recv(v);
+            if (more) take(v);
+        } else {
+            more = ch.recv_batch(batch, 5) > 0;
+            for (int64_t x : batch) take(x);
+        }
     }
     closer.join();
     if (n != (int64_t)senders * per_sender || order_errors.load()) {
