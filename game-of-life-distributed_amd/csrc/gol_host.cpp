@@ -398,6 +398,8 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
         FlipBuffer fb;
         if (opt.cell_events) fb.grow((uint64_t)std::min<int64_t>(W * H * std::min<int64_t>(batch, 4), 64ll << 20));
         std::vector<uint64_t> counts((size_t)batch);
+        constexpr uint64_t kFlipChunk = 4096;
+        std::vector<Event> flip_evs;
         int64_t t = 0;
         while (t < p.Turns && !quit.load()) {
             const int64_t want = std::min<int64_t>(batch, p.Turns - t);
@@ -425,16 +427,23 @@ void Run(Params p, Chan<Event> *events, Chan<char32_t> *keyPresses, const RunOpt
             for (int64_t i = 0; i < done; ++i) {
                 const int64_t completed = t0 + i + 1;  // quirks: the reference's 0-based turn (:113, :171, :216)
                 if (opt.cell_events) {
-                    for (uint64_t e = off; e < off + counts[(size_t)i]; ++e) {  // initializeAliveCells (:212-220)
-                        const uint64_t idx = fb.p[e];
-                        Event ev;
-                        ev.kind = EventKind::CellFlipped;
-                        ev.CompletedTurns = quirks ? completed - 1 : completed;
-                        ev.Cell.X = quirks ? (int64_t)(idx / W) : (int64_t)(idx % W);
-                        ev.Cell.Y = quirks ? (int64_t)(idx % W) : (int64_t)(idx / W);
-                        send(ev);
+                    // initializeAliveCells (:212-220): the turn's list, in order, sent in
+                    // chunks (Chan::send_batch: one lock a chunk on a buffered channel)
+                    const uint64_t n = counts[(size_t)i];
+                    for (uint64_t e0 = off; e0 < off + n && events; e0 += kFlipChunk) {
+                        const uint64_t m = std::min<uint64_t>(kFlipChunk, off + n - e0);
+                        flip_evs.resize(m);
+                        for (uint64_t j = 0; j < m; ++j) {
+                            const uint64_t idx = fb.p[e0 + j];
+                            Event &ev = flip_evs[j];
+                            ev.kind = EventKind::CellFlipped;
+                            ev.CompletedTurns = quirks ? completed - 1 : completed;
+                            ev.Cell.X = quirks ? (int64_t)(idx / W) : (int64_t)(idx % W);
+                            ev.Cell.Y = quirks ? (int64_t)(idx % W) : (int64_t)(idx / W);
+                        }
+                        events->send_batch(flip_evs.data(), m);
                     }
-                    off += counts[(size_t)i];
+                    off += n;
                 }
                 if (opt.turn_events) {
                     Event ev;

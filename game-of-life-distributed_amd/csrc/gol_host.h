@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
@@ -109,6 +110,41 @@ class Chan {
         }
         return true;
     }
+    // Sends v[0..n) in order, as n sends would (false if the channel closed on
+    // the way).  A buffered channel takes them in chunks of its free room
+    // under one lock and one wake-up each, so a turn's CellFlipped list
+    // does not pay a lock round trip per event; an unbuffered one keeps
+    // the rendezvous per value.  Other senders may interleave between
+    // chunks, as between any two Go sends.
+    bool send_batch(T *v, size_t n) {
+        if (cap_ == 0) {
+            for (size_t i = 0; i < n; ++i)
+                if (!send(std::move(v[i]))) return false;
+            return true;
+        }
+        size_t i = 0;
+        while (i < n) {
+            std::unique_lock<std::mutex> lk(mu_);
+            if (!closed_ && q_.size() >= cap_) {
+                lk.unlock();
+                spin([&] { return closed_a_.load(std::memory_order_acquire) ||
+                                  sent_a_.load(std::memory_order_acquire) -
+                                          received_a_.load(std::memory_order_acquire) < cap_; });
+                lk.lock();
+                ++send_sleepers_;
+                send_cv_.wait(lk, [&] { return closed_ || q_.size() < cap_; });
+                --send_sleepers_;
+            }
+            if (closed_) return false;
+            const size_t k = std::min(n - i, cap_ - q_.size());
+            for (size_t j = 0; j < k; ++j) q_.push_back(std::move(v[i + j]));
+            i += k;
+            sent_ += k;
+            sent_a_.store(sent_, std::memory_order_release);
+            if (recv_sleepers_) recv_cv_.notify_one();
+        }
+        return true;
+    }
     // Blocks; false once closed and drained (a `range` loop ends).
     bool recv(T &out) {
         spin([&] { return closed_a_.load(std::memory_order_acquire) ||
@@ -166,14 +202,18 @@ class Chan {
     }
 
    private:
-    // Spin up to ~50 us for `ready`; true if it became true meanwhile.
+    // Spin up to ~100 us for `ready` (a partner thread that is running answers
+    // well within that; sleeping and being woken costs ~10 us a side); true
+    // if it became true meanwhile.
     template <typename F>
     static bool spin(F &&ready) {
-        for (int i = 0; i < 2048; ++i) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int i = 0;; ++i) {
             if (ready()) return true;
             __builtin_ia32_pause();
+            if ((i & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(100))
+                return ready();
         }
-        return ready();
     }
     void take(T &out) {  // mu_ held, q_ not empty
         out = std::move(q_.front());
@@ -189,8 +229,11 @@ class Chan {
     bool closed_ = false;
     uint64_t sent_ = 0, received_ = 0;
     int send_sleepers_ = 0, recv_sleepers_ = 0;
-    std::atomic<uint64_t> sent_a_{0}, received_a_{0};
-    std::atomic<bool> closed_a_{false};
+    // Each spun-on word on a line of its own: the sender writes sent_a_, the
+    // receiver received_a_, and neither should bounce the mutex's line.
+    alignas(64) std::atomic<uint64_t> sent_a_{0};
+    alignas(64) std::atomic<uint64_t> received_a_{0};
+    alignas(64) std::atomic<bool> closed_a_{false};
 };
 
 // Host-mirror options beyond the Go API (all default to the reference's

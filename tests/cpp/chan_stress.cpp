@@ -5,7 +5,7 @@
 #include <chrono>
 #include <cstdio>
 #include <thread>
-#include <vector>
+#include <algorithm>
 #include <vector>
 
 #include "gol_host.h"
@@ -17,10 +17,20 @@ static int run(size_t cap, int senders, int per_sender) {
     std::atomic<int> order_errors{0};
     for (int s = 0; s < senders; ++s)
         ts.emplace_back([&, s] {
-            for (int i = 0; i < per_sender; ++i) {
-                if (!ch.send((int64_t)s << 32 | i)) order_errors++;
-                // rendezvous: the receiver has taken this value before send returned
-                if (cap == 0 && received_count.load() < 0) order_errors++;
+            std::vector<int64_t> buf;
+            for (int i = 0; i < per_sender;) {
+                if ((i / 16) % 2 == 0) {  // single sends and send_batch runs of 1..13 alternate
+                    if (!ch.send((int64_t)s << 32 | i)) order_errors++;
+                    // rendezvous: the receiver has taken this value before send returned
+                    if (cap == 0 && received_count.load() < 0) order_errors++;
+                    ++i;
+                } else {
+                    const int k = std::min(per_sender - i, 1 + (i * 7 + s) % 13);
+                    buf.clear();
+                    for (int j = 0; j < k; ++j) buf.push_back((int64_t)s << 32 | (i + j));
+                    if (!ch.send_batch(buf.data(), buf.size())) order_errors++;
+                    i += k;
+                }
             }
         });
     std::vector<int> next(senders, 0);

@@ -1,6 +1,6 @@
 """gol::Chan (the host mirror's Go channel, csrc/gol_host.h) under contention:
 values delivered exactly once and in per-sender order for capacities 0, 1, 7
-and 1000 with 1 and 3 senders, close ends the range loop, send after close
+and 1000 with 1 and 3 senders, single sends mixed with send_batch runs, close ends the range loop, send after close
 fails (tests/cpp/chan_stress.cpp, built with g++ here; no GPU)."""
 import os
 import subprocess
