@@ -81,6 +81,7 @@ class Chan {
     explicit Chan(size_t cap = 0) : cap_(cap) {}
     // Returns false if the channel is closed (Go would panic).
     bool send(T v) {
+        if (cap_ == 0) return send0(std::move(v));
         std::unique_lock<std::mutex> lk(mu_);
         const size_t room = std::max<size_t>(cap_, 1);
         if (!closed_ && q_.size() >= room) {
@@ -95,19 +96,9 @@ class Chan {
         }
         if (closed_) return false;
         q_.push_back(std::move(v));
-        const uint64_t ticket = ++sent_;
+        ++sent_;
         sent_a_.store(sent_, std::memory_order_release);
         if (recv_sleepers_) recv_cv_.notify_one();
-        if (cap_ == 0) {
-            lk.unlock();
-            if (spin([&] { return received_a_.load(std::memory_order_acquire) >= ticket ||
-                                  closed_a_.load(std::memory_order_acquire); }))
-                return true;
-            lk.lock();
-            ++send_sleepers_;
-            send_cv_.wait(lk, [&] { return received_ >= ticket || closed_; });
-            --send_sleepers_;
-        }
         return true;
     }
     // Sends v[0..n) in order, as n sends would (false if the channel closed on
@@ -147,6 +138,7 @@ class Chan {
     }
     // Blocks; false once closed and drained (a `range` loop ends).
     bool recv(T &out) {
+        if (cap_ == 0) return recv0(out);
         spin([&] { return closed_a_.load(std::memory_order_acquire) ||
                           sent_a_.load(std::memory_order_acquire) != received_a_.load(std::memory_order_acquire); });
         std::unique_lock<std::mutex> lk(mu_);
@@ -165,6 +157,12 @@ class Chan {
     // channel).  Returns the count; 0 once closed and drained.
     size_t recv_batch(std::vector<T> &out, size_t max) {
         out.clear();
+        if (cap_ == 0) {  // at most the one value a sender offers
+            T v;
+            if (max == 0 || !recv0(v)) return 0;
+            out.push_back(std::move(v));
+            return 1;
+        }
         spin([&] { return closed_a_.load(std::memory_order_acquire) ||
                           sent_a_.load(std::memory_order_acquire) != received_a_.load(std::memory_order_acquire); });
         std::unique_lock<std::mutex> lk(mu_);
@@ -184,6 +182,17 @@ class Chan {
     }
     // Non-blocking receive: 1 = got one, 0 = empty, -1 = closed and drained.
     int try_recv(T &out) {
+        if (cap_ == 0) {
+            std::lock_guard<std::mutex> rg(recv_mu_);
+            const uint64_t q = seq_.load(std::memory_order_acquire);
+            if (q & 1) {
+                out = std::move(slot_);
+                seq_.store(q + 1, std::memory_order_release);
+                wake(send_sleepers0_, send_cv_);
+                return 1;
+            }
+            return closed_a_.load(std::memory_order_acquire) ? -1 : 0;
+        }
         std::lock_guard<std::mutex> lk(mu_);
         if (q_.empty()) return closed_ ? -1 : 0;
         take(out);
@@ -202,6 +211,56 @@ class Chan {
     }
 
    private:
+    // ---- capacity 0: the rendezvous.  One slot and a sequence word (odd =
+    // a value waits in the slot); senders queue on send_mu_, receivers on
+    // recv_mu_, so a hand-off between one sender and one receiver moves only
+    // the slot's and the sequence word's cache lines (~1.5 us a value with a
+    // shared mutex and counters before).  A side that waits past the spin
+    // sleeps on mu_'s condition variables (wait0 / wake).
+    bool send0(T v) {
+        std::lock_guard<std::mutex> sg(send_mu_);
+        if (closed_a_.load(std::memory_order_acquire)) return false;
+        const uint64_t q = seq_.load(std::memory_order_relaxed);  // even: the previous value was taken
+        slot_ = std::move(v);
+        seq_.store(q + 1, std::memory_order_release);
+        wake(recv_sleepers0_, recv_cv_);
+        // Go: the send completes when a receiver has the value
+        wait0([&] { return seq_.load(std::memory_order_acquire) != q + 1 || closed_a_.load(std::memory_order_acquire); },
+              send_sleepers0_, send_cv_);
+        return true;
+    }
+    bool recv0(T &out) {
+        std::lock_guard<std::mutex> rg(recv_mu_);
+        wait0([&] { return (seq_.load(std::memory_order_acquire) & 1) || closed_a_.load(std::memory_order_acquire); },
+              recv_sleepers0_, recv_cv_);
+        const uint64_t q = seq_.load(std::memory_order_acquire);
+        if (!(q & 1)) return false;  // closed, nothing offered
+        out = std::move(slot_);
+        seq_.store(q + 1, std::memory_order_release);
+        wake(send_sleepers0_, send_cv_);
+        return true;
+    }
+    // Sleep until `ready` (after the spin).  With wake(): the sleeper counts
+    // itself, then re-checks; the waker publishes, then reads the count (both
+    // behind seq_cst fences), so one of them sees the other's write, and a
+    // waker that sees a sleeper takes mu_ first, so the notify cannot fall
+    // between the sleeper's check and its wait.
+    template <typename F>
+    void wait0(F &&ready, std::atomic<int> &sleepers, std::condition_variable &cv) {
+        if (spin(ready)) return;
+        std::unique_lock<std::mutex> lk(mu_);
+        sleepers.fetch_add(1, std::memory_order_relaxed);
+        std::atomic_thread_fence(std::memory_order_seq_cst);
+        while (!ready()) cv.wait(lk);
+        sleepers.fetch_sub(1, std::memory_order_relaxed);
+    }
+    void wake(std::atomic<int> &sleepers, std::condition_variable &cv) {
+        std::atomic_thread_fence(std::memory_order_seq_cst);
+        if (sleepers.load(std::memory_order_relaxed) > 0) {
+            { std::lock_guard<std::mutex> lk(mu_); }
+            cv.notify_all();
+        }
+    }
     // Spin up to ~100 us for `ready` (a partner thread that is running answers
     // well within that; sleeping and being woken costs ~10 us a side); true
     // if it became true meanwhile.
@@ -234,6 +293,13 @@ class Chan {
     alignas(64) std::atomic<uint64_t> sent_a_{0};
     alignas(64) std::atomic<uint64_t> received_a_{0};
     alignas(64) std::atomic<bool> closed_a_{false};
+    // capacity 0 (send0 / recv0)
+    alignas(64) std::mutex send_mu_;
+    alignas(64) std::mutex recv_mu_;
+    alignas(64) std::atomic<uint64_t> seq_{0};
+    T slot_{};
+    alignas(64) std::atomic<int> send_sleepers0_{0};
+    alignas(64) std::atomic<int> recv_sleepers0_{0};
 };
 
 // Host-mirror options beyond the Go API (all default to the reference's
