@@ -129,6 +129,36 @@ int persist_blocks_per_cu(int depth, int wpl, int nw);
 bool plan_persist(int Ww, int rows, int depth, int cus, int wpl, int units, PersistArgs *p, int force_tx = 0);
 hipError_t launch_persist(const PersistArgs &p, int depth, int wpl, hipStream_t s);
 
+// Resident LDS bands (K1r, gol_kernels.hip; small tori).  Workgroup b of nb
+// keeps the full-width rows [b rows / nb, (b + 1) rows / nb) of the torus in
+// LDS, with D halo rows on each side, and runs super-steps of D turns there;
+// between super-steps it publishes its top and bottom D rows to `edge` and
+// takes its neighbours' (write-through stores and loads, one flag per
+// workgroup).  Every band needs >= D rows.  W % 128 == 0; wpl 1 (canonical
+// words) or 2 (interleaved pairs).
+struct LdsBandArgs {
+    const uint32_t *src;   // generation 0: rows x Ww words
+    uint32_t *dst;         // the last generation (the other buffer)
+    uint32_t *edge;        // lds_band_edge_words(nb, D, Ww)
+    unsigned *progress;    // nb words, zeroed: super-steps whose edges are published
+    unsigned *error;       // zeroed; set on a spin timeout (every workgroup then drains)
+    unsigned long long *alive;  // nullable: += popcount of the last generation
+    long long timeout_ticks;    // s_memrealtime ticks (100 MHz) a wait may take
+    int Ww, rows, nb, D, turns;
+    int hmax;              // ceil(rows / nb)
+    int xcd;               // 1: consecutive bands on one XCD (nb % 8 == 0)
+    int nt;                // threads per workgroup: 512 or 1024
+    int stride;            // LDS words per row: lds_band_stride (>= Ww)
+    unsigned long long *trace;  // nullable: [0..3] += ticks in compute, publish, wait, halo load; [4] += workgroups
+};
+__host__ __device__ inline int64_t lds_band_edge_words(int nb, int D, int Ww) { return 4ll * nb * D * Ww; }
+inline int64_t lds_band_lds_bytes(int hmax, int D, int stride) { return 2ll * (hmax + 2 * D + 3) * stride * 4; }
+// Resident workgroups per CU at that LDS size (0: does not fit).
+// The LDS row stride for Ww-word rows: an instantiated compile-time stride >= Ww, else Ww.
+int lds_band_stride(int Ww, int wpl, int nt);
+int lds_band_blocks_per_cu(int wpl, int nt, int stride, int64_t lds_bytes);
+hipError_t launch_lds_band(const LdsBandArgs &p, int wpl, hipStream_t s);
+
 hipError_t launch_pack(const uint8_t *bytes, uint32_t *words, int W, int Ww, int rows, hipStream_t s);
 // il: the words are in the interleaved pair layout of the wpl = 2 step kernels
 // (W % 64 == 0); pack / fill_random / load write canonical words, which the

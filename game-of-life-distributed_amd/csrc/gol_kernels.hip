@@ -1770,6 +1770,302 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// K1r: resident LDS bands (small tori, one workgroup of 8 waves per CU).
+//
+// Boards up to ~8192^2 hold too few cells per wave for the register
+// pipelines: K1w's bands there are 20-40 rows against a 20-stage pipeline,
+// K1p recomputes 2 D halo rows per 16-row band.  K1r keeps each band in LDS
+// instead.  Workgroup b owns the full-width rows [r0, r0 + h) and holds them
+// with D halo rows above and below (R = h + 2D rows, two buffers); a
+// super-step runs D turns in LDS, turn t computing rows [t, R - t) (the
+// halo rows go stale one row a turn), with the column wrap of the torus
+// taken in LDS, so there are no halo lanes and no tiles.  Between
+// super-steps the band's top and bottom D rows go to global memory and the
+// neighbours' come back: Guideline 16's write-through hand-off (sc1 buffer
+// stores, every wave's vmcnt(0), a barrier, one sc1 flag store; the
+// consumer's wave 0 polls both neighbours' flags with sc1 loads, a barrier,
+// then sc1 buffer loads), no cache-wide fence.  The edge buffers alternate
+// by super-step parity: the wait for a neighbour's super-step j flag also
+// proves it read our j - 1 edges, which the slot we overwrite held.
+// Per row and word: three LDS loads (own word or pair, one neighbour word
+// each side), the row sums (9 - 2 LUTs of stage()), the column sums and the
+// rule, one LDS store.  Every wait is bounded (error word, all drain).
+// ---------------------------------------------------------------------------
+template <int WPL>
+struct LdsRow {
+    uint32_t s0[WPL], s1[WPL], c[WPL];
+};
+// A row's words as loaded: the lane's own word (pair) and one neighbour word on each side.
+template <int WPL>
+struct LdsRaw {
+    uint32_t c[WPL], l, r;
+};
+
+// The lane's word (pair) of an LDS row and the one neighbour word on each
+// side its row sums need: three ds_reads.  (Taking the neighbour words from
+// the adjacent lanes by DPP instead, with only the wave-edge lanes reading
+// theirs, saved the 2-way bank conflicts of every-second-word reads but ran
+// 8192^2 at 24-26 instead of 31-32 TCUPS: load -> DPP -> alignbit is a longer
+// dependent chain at two waves per SIMD; profiles/r4o.)
+template <int WPL>
+__device__ __forceinline__ LdsRaw<WPL> lds_load(const uint32_t *row, int o, int ol, int orr) {
+    LdsRaw<WPL> x;
+    if constexpr (WPL == 1) {
+        x.c[0] = row[o];
+    } else {
+        const uint2 v = *reinterpret_cast<const uint2 *>(row + o);
+        x.c[0] = v.x;
+        x.c[1] = v.y;
+    }
+    x.l = row[ol];   // wpl 1: the left word; 2: the left pair's odd cells (bit 31 = its cell 63)
+    x.r = row[orr];  // wpl 1: the right word; 2: the right pair's even cells (bit 0 = its cell 0)
+    return x;
+}
+
+template <int WPL>
+__device__ __forceinline__ void lds_sums(const LdsRaw<WPL> &x, LdsRow<WPL> &s) {
+    uint32_t west[WPL], east[WPL];
+    if constexpr (WPL == 1) {
+        west[0] = __builtin_amdgcn_alignbit(x.c[0], x.l, 31);  // cell b-1 (bit 31 of the left word for b = 0)
+        east[0] = __builtin_amdgcn_alignbit(x.r, x.c[0], 1);   // cell b+1
+    } else {
+        west[0] = __builtin_amdgcn_alignbit(x.c[1], x.l, 31);  // cell 2k-1
+        east[0] = x.c[1];                                      // cell 2k+1
+        west[1] = x.c[0];                                      // cell 2k
+        east[1] = __builtin_amdgcn_alignbit(x.r, x.c[0], 1);   // cell 2k+2
+    }
+#pragma unroll
+    for (int k = 0; k < WPL; ++k) {
+        s.c[k] = x.c[k];
+        s.s0[k] = bop<kXor3>(west[k], x.c[k], east[k]);
+        s.s1[k] = bop<kMaj>(west[k], x.c[k], east[k]);
+    }
+}
+
+typedef unsigned v4u32 __attribute__((ext_vector_type(4)));
+constexpr int kCpolSc1 = 16;  // buffer load/store aux bit: sc1 (write-through store, L1-bypassing load)
+
+// S > 0: LDS rows S words apart (>= Ww, a compile-time stride: the row
+// loop's loads and stores of consecutive rows take immediate offsets); 0: Ww.
+template <int WPL, int NT, int S>
+__global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
+    extern __shared__ uint4 lds_band_smem[];
+    uint32_t *const L0 = reinterpret_cast<uint32_t *>(lds_band_smem);
+    const int Ww = p.Ww, D = p.D, nb = p.nb;
+    const int LS = S > 0 ? S : Ww;  // LDS row stride (words)
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // blocks are dealt round-robin over the 8 XCDs: give each XCD a run of
+    // consecutive bands so most neighbours share an L2 (speed only)
+    const int b = (p.xcd && nb % 8 == 0) ? (int)(blockIdx.x % 8) * (nb / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+    const int r0 = (int)((int64_t)b * p.rows / nb);
+    const int h = (int)((int64_t)(b + 1) * p.rows / nb) - r0;
+    const int R = h + 2 * D;
+    const int Rmax = p.hmax + 2 * D + 3;  // + 3 spare rows for the row loop's prefetch
+    uint32_t *A = L0, *B = L0 + (size_t)Rmax * LS;
+    const int up = (b + nb - 1) % nb, down = (b + 1) % nb;
+    __shared__ int s_abort;
+    if (threadIdx.x == 0) s_abort = 0;
+
+    // generation 0: board rows r0 - D .. r0 + h + D - 1 (mod rows), 16-B words
+    const int q4 = Ww / 4;
+    for (int i = threadIdx.x; i < R * q4; i += NT) {
+        const int r = i / q4, c = i - r * q4;
+        int br = r0 - D + r;
+        br = ((br % p.rows) + p.rows) % p.rows;
+        reinterpret_cast<uint4 *>(A + (size_t)r * LS)[c] = reinterpret_cast<const uint4 *>(p.src + (size_t)br * Ww)[c];
+    }
+    __syncthreads();
+
+    const __amdgpu_buffer_rsrc_t ers = __builtin_amdgcn_make_buffer_rsrc(
+        p.edge, (short)0, (int)(lds_band_edge_words(nb, D, Ww) * 4), 0x00020000);
+    const int P = Ww / WPL;               // words (wpl 1) or pairs per row
+    const int K = max(1, NT / P);        // row runs per column
+    const int units = P * K;
+    const int J = (p.turns + D - 1) / D;
+    const int eq4 = D * q4;               // 16-B granules of one edge side
+    // diagnostics (option "trace"): s_memrealtime ticks summed over the
+    // workgroups in compute, publish, neighbour wait and halo load
+    long long tr[4] = {0, 0, 0, 0}, tr_t = p.trace ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
+    auto lap = [&](int k) {
+        if (p.trace) {
+            const long long now = (long long)__builtin_amdgcn_s_memrealtime();
+            tr[k] += now - tr_t;
+            tr_t = now;
+        }
+    };
+    for (int j = 0; j < J; ++j) {
+        if (j > 0) {
+            // neighbours' super-step j edges (generation j D)
+            if (w == 0) {
+                const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+                const int nbr = lane == 0 ? up : down;
+                for (;;) {
+                    const unsigned v = lane < 2 ? __hip_atomic_load(&p.progress[nbr], __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT)
+                                                : (unsigned)j;
+                    if (__all(v >= (unsigned)j)) break;
+                    const unsigned err = __hip_atomic_load(p.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (err || (long long)__builtin_amdgcn_s_memrealtime() - t0 > p.timeout_ticks) {
+                        if (lane == 0) {
+                            atomicOr(p.error, 1u);
+                            s_abort = 1;
+                        }
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            __syncthreads();
+            if (s_abort) return;  // uniform over the workgroup
+            lap(2);
+            const int slot = j & 1;
+            const int eu = (((slot * nb + up) * 2 + 1) * eq4) * 16;    // up's bottom D rows -> rows [0, D)
+            const int ed = (((slot * nb + down) * 2 + 0) * eq4) * 16;  // down's top D rows -> rows [D + h, R)
+            for (int i = threadIdx.x; i < 2 * eq4; i += NT) {
+                const bool top = i < eq4;
+                const int g = top ? i : i - eq4;
+                const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(ers, (top ? eu : ed) + g * 16, 0, kCpolSc1);
+                uint32_t *dstw = A + (size_t)(top ? 0 : D + h) * LS + 4 * (g % q4) + (size_t)(g / q4) * LS;
+                *reinterpret_cast<uint4 *>(dstw) = make_uint4(v.x, v.y, v.z, v.w);
+            }
+            __syncthreads();
+            lap(3);
+        }
+        const int Dj = min(D, p.turns - j * D);
+        // the last, shorter super-step needs only Dj halo rows of the D
+        const int skip = D - Dj;
+        for (int t = 1; t <= Dj; ++t) {
+            const int lo_t = skip + t, hi_t = R - skip - t;
+            const int len = (hi_t - lo_t + K - 1) / K;
+            for (int u = threadIdx.x; u < units; u += NT) {
+                const int k = u / P, c = u - k * P;
+                const int lo = lo_t + k * len, hi = min(lo + len, hi_t);
+                if (lo >= hi) continue;
+                const int cl = c == 0 ? P - 1 : c - 1, cr = c == P - 1 ? 0 : c + 1;
+                const int o = WPL * c, ol = WPL == 1 ? cl : 2 * cl + 1, orr = WPL * cr;
+                // rows r - 1, r, r + 1 in s[(q + 0..2) % 3]; the words of rows r + 1 and
+                // r + 2 already loaded (n1, n2) while row r is computed: the LDS
+                // latency hides behind a row's rule (two waves per SIMD hide little)
+                // the raw words of row r0 + q + 1 in x[q], of r0 + q + 2 in x[q + 1]
+                // (in flight); row r0 + q + 3 goes to x[q + 2] (indices mod 3, all
+                // static in the unrolled body: no register copies, no early waits).
+                // Rows past R - 1 land in the buffer's 3 spare rows (never used).
+                LdsRow<WPL> s[3];
+                LdsRaw<WPL> x[3];
+                lds_sums<WPL>(lds_load<WPL>(A + (lo - 1) * LS, o, ol, orr), s[0]);
+                lds_sums<WPL>(lds_load<WPL>(A + lo * LS, o, ol, orr), s[1]);
+                x[0] = lds_load<WPL>(A + (lo + 1) * LS, o, ol, orr);
+                x[1] = lds_load<WPL>(A + (lo + 2) * LS, o, ol, orr);
+                const uint32_t *ld = A + (lo + 3) * LS;
+                uint32_t *st = B + lo * LS + o;
+                for (int r0 = lo; r0 < hi; r0 += 3) {
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+                        if (r0 + q < hi) {
+                            lds_sums<WPL>(x[q], s[(q + 2) % 3]);
+                            x[(q + 2) % 3] = lds_load<WPL>(ld + q * LS, o, ol, orr);
+                            const LdsRow<WPL> &a = s[q % 3], &b = s[(q + 1) % 3], &n = s[(q + 2) % 3];
+                            uint32_t out[WPL];
+#pragma unroll
+                            for (int m = 0; m < WPL; ++m)
+                                out[m] = rule_word(a.s0[m], a.s1[m], b.s0[m], b.s1[m], n.s0[m], n.s1[m], b.c[m]);
+                            if constexpr (WPL == 1)
+                                st[q * LS] = out[0];
+                            else
+                                *reinterpret_cast<uint2 *>(st + q * LS) = make_uint2(out[0], out[1]);
+                        }
+                    }
+                    ld += 3 * LS;
+                    st += 3 * LS;
+                }
+            }
+            __syncthreads();
+            uint32_t *T = A;
+            A = B;
+            B = T;
+        }
+        lap(0);
+        if (j + 1 < J) {
+            // publish generation (j + 1) D: rows [D, 2D) (side 0) and [h, h + D) (side 1)
+            const int slot = (j + 1) & 1;
+            const int e0 = (((slot * nb + b) * 2) * eq4) * 16;
+            for (int i = threadIdx.x; i < 2 * eq4; i += NT) {
+                const bool top = i < eq4;
+                const int g = top ? i : i - eq4;
+                const uint4 v = *reinterpret_cast<const uint4 *>(A + (size_t)(top ? D : h) * LS + 4 * (g % q4) + (size_t)(g / q4) * LS);
+                __builtin_amdgcn_raw_buffer_store_b128((v4u32){v.x, v.y, v.z, v.w}, ers,
+                                                       e0 + (top ? 0 : eq4 * 16) + g * 16, 0, kCpolSc1);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0)
+                __hip_atomic_store(&p.progress[b], (unsigned)(j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            lap(1);
+        }
+    }
+    if (p.trace && threadIdx.x == 0) {
+        for (int k = 0; k < 4; ++k) atomicAdd(&p.trace[k], (unsigned long long)tr[k]);
+        atomicAdd(&p.trace[4], 1ull);
+    }
+    // the band's last generation: rows [D, D + h) of A -> board rows [r0, r0 + h)
+    uint32_t cnt = 0;
+    for (int i = threadIdx.x; i < h * q4; i += NT) {
+        const int r = i / q4, c = i - r * q4;
+        const uint4 v = reinterpret_cast<const uint4 *>(A + (size_t)(D + r) * LS)[c];
+        reinterpret_cast<uint4 *>(p.dst + (size_t)(r0 + r) * Ww)[c] = v;
+        cnt += __builtin_popcount(v.x) + __builtin_popcount(v.y) + __builtin_popcount(v.z) + __builtin_popcount(v.w);
+    }
+    if (p.alive) {
+        const uint32_t tot = wave_sum_u32(cnt);
+        if (lane == 0 && tot) atomicAdd(p.alive, (unsigned long long)tot);
+    }
+}
+
+template <typename F>
+static hipError_t dispatch_lds_band(int wpl, int nt, int stride, F &&f) {
+#define GOL_LCASE(WP, NT, S) \
+    if (wpl == WP && nt == NT && stride == S) return f(gol_lds_band_kernel<WP, NT, S>, NT);
+    GOL_LCASE(2, 512, 0) GOL_LCASE(2, 512, 128) GOL_LCASE(2, 512, 256) GOL_LCASE(2, 1024, 0) GOL_LCASE(2, 1024, 256)
+    GOL_LCASE(1, 512, 0) GOL_LCASE(1, 1024, 0)
+#undef GOL_LCASE
+    return hipErrorInvalidValue;
+}
+// The template stride of the kernel that runs LDS rows `stride` words apart:
+// that stride where instantiated, else 0 (the runtime-stride kernel, stride == Ww).
+static int lds_tmpl_stride(int wpl, int nt, int stride) {
+    return dispatch_lds_band(wpl, nt, stride, [](auto, int) { return hipSuccess; }) == hipSuccess ? stride : 0;
+}
+int lds_band_stride(int Ww, int wpl, int nt) {
+    for (int S : {128, 256})
+        if (Ww <= S && lds_tmpl_stride(wpl, nt, S) == S) return S;
+    return Ww;
+}
+
+int lds_band_blocks_per_cu(int wpl, int nt, int stride, int64_t lds_bytes) {
+    int n = 0;
+    hipError_t e = dispatch_lds_band(wpl, nt, lds_tmpl_stride(wpl, nt, stride), [&](auto kern, int t) {
+        hipError_t r = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+        return r == hipSuccess ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, t, (size_t)lds_bytes) : r;
+    });
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+hipError_t launch_lds_band(const LdsBandArgs &p, int wpl, hipStream_t s) {
+    const size_t bytes = (size_t)lds_band_lds_bytes(p.hmax, p.D, p.stride);
+    const int S = lds_tmpl_stride(wpl, p.nt, p.stride);
+    if (S == 0 && p.stride != p.Ww) return hipErrorInvalidValue;
+    return dispatch_lds_band(wpl, p.nt, S, [&](auto kern, int t) {
+        hipLaunchKernelGGL(kern, dim3(p.nb), dim3(t), bytes, s, p);
+        return hipGetLastError();
+    });
+}
+
 // ---- host-side dispatch over (depth, fill skip, words per lane) ----------
 // Depths 1, 2, 4, 6, 8, 12, 16, 20 (and 24, 32 for WPL = 1: depth 24 at
 // WPL = 2 would exceed 256 VGPRs; WPL = 4 stops at 9, an extra depth of its

@@ -126,11 +126,23 @@ struct golhip {
     int skew_tx = 0;                // option "skew_tx": tiles per K1w workgroup (0: plan, 1 or 2)
     int skew_half = 0;              // option "skew_half": half-wave tiles (0: when fewer wave-rows, 1: whenever possible, -1: never)
     int skew_nst = 0;               // option "skew_nst" (measurement): stacks per tile column (0: plan)
+    int lds_bpc[4] = {};               // K1r workgroups per CU by (wpl, 512 / 1024 threads) at lds_bpc_bytes of LDS
+    int64_t lds_bpc_bytes[4] = {};
+    int lds_bpc_stride[4] = {};
     int skew_bpc[kNumDepths][6] = {};  // K1w workgroups per CU by (depth, wpl, half) (0: not queried)
     unsigned *skew_err = nullptr;      // host-mapped spin-bound flag of the K1w kernels
     unsigned *skew_err_dev = nullptr;
     int64_t skew_launches = 0;
     int64_t skew_half_launches = 0;
+    int lds_band = -1;              // option "lds_band": resident LDS bands K1r (1 on where it fits, 0 off, -1 auto)
+    int lds_depth = 0;              // option "lds_depth": turns per K1r super-step (0: plan)
+    int lds_xcd = 1;                // option "lds_xcd": consecutive K1r bands on one XCD
+    int lds_waves = 8;              // option "lds_waves": K1r waves per workgroup (8 or 16)
+    int lds_wg_cu = 1;              // option "lds_wg_cu": K1r bands (workgroups) per CU (1 or 2)
+    int lds_stride = 1;             // option "lds_stride": K1r LDS rows at a compile-time stride where instantiated
+    uint32_t *lds_edge = nullptr;   // K1r edge rows (golk::lds_band_edge_words)
+    int64_t lds_edge_cap = 0;
+    int64_t lds_launches = 0;
     int persistent = -1;        // option "persistent": K1p for long torus runs (1 on, 0 off, -1 auto)
     int wpl_opt = 0;            // option "wpl": words per lane (0 = auto, 1, 2, 4)
     int persist_depth = 0;      // option "persist_depth" (0: tb_depth)
@@ -372,6 +384,7 @@ int persist_nw_for(golhip_t h, int depth, int wpl) {
 constexpr int64_t kPersistAutoMaxBytes = 64ll << 20;
 int wpl_per_launch(golhip_t h);
 bool skew_fills(golhip_t h);
+bool lds_fits(golhip_t h, int wpl, golk::LdsBandArgs *out = nullptr);
 bool persist_on(golhip_t h) {
     // a multi-rank ring never runs the resident kernel (try_persist_halo):
     // plan words per lane and halos for the per-launch kernels that do run
@@ -392,6 +405,7 @@ int wpl_for(golhip_t h) {
     if (h->wpl_opt == 1 || h->wpl_opt == 2) return h->wpl_opt;
     if (h->wpl_opt == 4) return h->W % 128 == 0 ? 4 : 2;
     if ((!h->torus() && !h->comm) || !persist_on(h)) return wpl_per_launch(h);
+    if (lds_fits(h, 2)) return 2;  // K1r: pairs (11 slots a word-turn against 15)
     auto best = [&](int wpl) {
         const int d = default_depth(h, wpl);
         const int def = golk::persist_waves_for(d, wpl);
@@ -976,7 +990,7 @@ bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int w
     }
     p.nw = nw;
     if (!h->d_sync) {
-        if (hipMalloc(&h->d_sync, (size_t)(h->dev_cu + 2) * sizeof(unsigned)) != hipSuccess ||
+        if (hipMalloc(&h->d_sync, (size_t)(2 * h->dev_cu + 2) * sizeof(unsigned)) != hipSuccess ||
             hipHostMalloc(&h->h_err, sizeof(unsigned), hipHostMallocDefault) != hipSuccess) {
             *rc = fail(GOLHIP_ENOMEM, "persistent sync words");
             return false;
@@ -1056,11 +1070,125 @@ bool take_guard(golhip_t h, int *rc) {
     return true;
 }
 
+// The K1r plan of this torus at `wpl` words per lane (no side effects):
+// one band per CU of at least D rows, both LDS buffers of a band in one
+// workgroup's LDS, every workgroup resident.  Depth: the option, else 12
+// (profiles/r4k-r4n sweeps: 8192^2 31.8 TCUPS at 12 vs 31.7 at 8 and 30.6 at
+// 16; 5120^2 17.9 vs 17.0 and 17.7; 4096^2 13.4 vs 13.0 and 13.6), at most
+// the row count.  False if K1r does not apply.
+bool lds_fits(golhip_t h, int wpl, golk::LdsBandArgs *out) {
+    if (h->lds_band == 0 || !h->torus() || h->W % 128 != 0 || (wpl == 2 && h->W % 64 != 0)) return false;
+    if (h->nranks > 1) return false;
+    const int D = h->lds_depth > 0 ? h->lds_depth : std::min(12, h->rows);
+    if (h->rows < D || D < 1) return false;
+    const int nt = 64 * h->lds_waves;
+    // one progress word per band after d_sync's error word (2 dev_cu + 2 words)
+    const int nb = std::min(std::min(h->cu_count, h->dev_cu) * h->lds_wg_cu, h->rows / D);
+    if (nb < 1) return false;
+    const int hmax = (h->rows + nb - 1) / nb;
+    int stride = h->lds_stride ? golk::lds_band_stride(h->Ww, wpl, nt) : h->Ww;
+    if (golk::lds_band_lds_bytes(hmax, D, stride) > 160 * 1024 - 256) stride = h->Ww;  // the padded rows do not fit
+    const int64_t bytes = golk::lds_band_lds_bytes(hmax, D, stride);
+    if (bytes > 160 * 1024 - 256) return false;  // (the kernel's few static LDS bytes)
+    const int slot = (wpl == 2 ? 1 : 0) + (nt == 1024 ? 2 : 0);
+    int &bpc = h->lds_bpc[slot];
+    if (bpc == 0 || h->lds_bpc_bytes[slot] != bytes || h->lds_bpc_stride[slot] != stride) {
+        bpc = std::max(0, golk::lds_band_blocks_per_cu(wpl, nt, stride, bytes));
+        h->lds_bpc_bytes[slot] = bytes;
+        h->lds_bpc_stride[slot] = stride;
+    }
+    if ((int64_t)nb > (int64_t)bpc * h->cu_count) return false;
+    if (out) {
+        out->Ww = h->Ww;
+        out->rows = h->rows;
+        out->nb = nb;
+        out->D = D;
+        out->hmax = hmax;
+        out->xcd = h->lds_xcd;
+        out->nt = nt;
+        out->stride = stride;
+    }
+    return true;
+}
+
+// Torus: all `left` turns as one K1r launch (under the step guard, like
+// K1p); returns the turns run (0 if K1r does not apply).
+int64_t try_lds(golhip_t h, int64_t left, bool count_last, int *rc) {
+    *rc = GOLHIP_OK;
+    if (left < 2 || left > INT32_MAX || !(h->il == 0 || h->il == 2)) return 0;
+    const int wpl = h->il == 2 ? 2 : 1;
+    golk::LdsBandArgs p{};
+    if (!lds_fits(h, wpl, &p)) return 0;
+    const int64_t ew = golk::lds_band_edge_words(p.nb, p.D, p.Ww);
+    if (ew > h->lds_edge_cap) {
+        if (hipFree(h->lds_edge) != hipSuccess) {
+            *rc = fail(GOLHIP_EHIP, "hipFree (K1r edges)");
+            return 0;
+        }
+        h->lds_edge = nullptr;
+        h->lds_edge_cap = 0;
+        if (hipMalloc(&h->lds_edge, (size_t)ew * 4) != hipSuccess) {
+            h->lds_edge = nullptr;
+            return 0;
+        }
+        h->lds_edge_cap = ew;
+    }
+    if (!h->d_sync) {
+        if (hipMalloc(&h->d_sync, (size_t)(2 * h->dev_cu + 2) * sizeof(unsigned)) != hipSuccess ||
+            hipHostMalloc(&h->h_err, sizeof(unsigned), hipHostMallocDefault) != hipSuccess) {
+            *rc = fail(GOLHIP_ENOMEM, "resident sync words");
+            return 0;
+        }
+        *h->h_err = 0;
+    }
+    if (!take_guard(h, rc)) return 0;
+    const bool count = count_last;
+    hipError_t e = count ? hipMemsetAsync(h->d_scalars, 0, sizeof(unsigned long long), h->stream) : hipSuccess;
+    if (e == hipSuccess) e = hipMemsetAsync(h->d_sync, 0, (size_t)(p.nb + 1) * sizeof(unsigned), h->stream);
+    p.src = h->cur_rows();
+    p.dst = h->prev_rows();
+    p.edge = h->lds_edge;
+    p.error = h->d_sync;
+    p.progress = h->d_sync + 1;
+    p.alive = count ? h->d_scalars : nullptr;
+    p.timeout_ticks = h->persist_timeout_ticks;
+    p.turns = (int)left;
+    p.trace = h->d_trace;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (e == hipSuccess && (h->flags & GOLHIP_FLAG_TIMING)) {
+        e0 = take_event(h);
+        e1 = take_event(h);
+        if (e0 && e1) e = hipEventRecord(e0, h->stream);
+    }
+    if (e == hipSuccess) e = golk::launch_lds_band(p, wpl, h->stream);
+    if (e == hipSuccess && e1) {
+        e = hipEventRecord(e1, h->stream);
+        h->ev_pending.push_back({e0, e1, 1});
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(h->h_err, h->d_sync, sizeof(unsigned), hipMemcpyDeviceToHost, h->stream);
+    if (e != hipSuccess) {
+        *rc = fail(GOLHIP_EHIP, "resident LDS-band launch: %s", hipGetErrorString(e));
+        return 0;
+    }
+    h->persist_pending = true;
+    h->halo_ready = 0;
+    h->cur ^= 1;
+    h->last_variant = 4;
+    h->turns += left;
+    h->persist_turns += left;
+    h->persist_launches++;
+    h->lds_launches++;
+    if (count) h->alive_turn = h->turns;
+    return left;
+}
+
 // Torus: J super-steps of `depth` turns in one resident launch; returns the
 // turns run (0 if the persistent path does not apply).
 int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     *rc = GOLHIP_OK;
     if (!persist_on(h) || h->W % 32 != 0 || !h->torus()) return 0;
+    if (int64_t n = try_lds(h, left, count_last, rc)) return n;
+    if (*rc) return 0;
     const int wpl = wpl_for(h);
     const int depth = persist_depth_for(h, wpl);
     if (depth < 4 || golk::persist_blocks_per_cu(depth, wpl, persist_nw_for(h, depth, wpl)) < 1) return 0;
@@ -1516,6 +1644,7 @@ int golhip_destroy(golhip_t h) {
     HIP_RC(hipFree(h->backup));
     HIP_RC(hipFree(h->split_exp));
     HIP_RC(hipFree(h->split_meet));
+    HIP_RC(hipFree(h->lds_edge));
     if (h->h_err) HIP_RC(hipHostFree(h->h_err));
     if (h->skew_err) HIP_RC(hipHostFree(h->skew_err));
     if (h->own_stream && h->stream) HIP_RC(hipStreamDestroy(h->stream));
@@ -1695,6 +1824,36 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     if (!strcmp(key, "skew_tx")) {
         if (value < 0 || value > 2) return fail(GOLHIP_EINVAL, "skew_tx %lld", (long long)value);
         h->skew_tx = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "lds_band")) {
+        if (value < -1 || value > 1) return fail(GOLHIP_EINVAL, "lds_band %lld", (long long)value);
+        h->lds_band = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "lds_depth")) {
+        if (value < 0 || value > 64) return fail(GOLHIP_EINVAL, "lds_depth %lld", (long long)value);
+        h->lds_depth = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "lds_waves")) {
+        if (value != 8 && value != 16) return fail(GOLHIP_EINVAL, "lds_waves %lld not 8 or 16", (long long)value);
+        h->lds_waves = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "lds_wg_cu")) {
+        if (value < 1 || value > 2) return fail(GOLHIP_EINVAL, "lds_wg_cu %lld", (long long)value);
+        h->lds_wg_cu = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "lds_stride")) {
+        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "lds_stride %lld", (long long)value);
+        h->lds_stride = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "lds_xcd")) {
+        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "lds_xcd %lld", (long long)value);
+        h->lds_xcd = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "split")) {
@@ -1907,7 +2066,7 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     const int64_t persist_turns0 = h->persist_turns, persist_launches0 = h->persist_launches;
     const int64_t step_launches0 = h->step_launches, step_turns0 = h->step_turns;
     const int64_t split_launches0 = h->split_launches, skew_launches0 = h->skew_launches;
-    const int64_t skew_half_launches0 = h->skew_half_launches;
+    const int64_t skew_half_launches0 = h->skew_half_launches, lds_launches0 = h->lds_launches;
     const size_t ev0 = h->ev_pending.size();
     const int64_t halo_exchanges0 = h->halo_exchanges, halo_bytes0 = h->halo_bytes;
     int rc = step_locked(h, nturns, want_flips);
@@ -1935,6 +2094,7 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     h->split_launches = split_launches0;
     h->skew_launches = skew_launches0;
     h->skew_half_launches = skew_half_launches0;
+    h->lds_launches = lds_launches0;
     h->halo_exchanges = halo_exchanges0;
     h->halo_bytes = halo_bytes0;
     if (h->ev_pending.size() >= ev0) {  // the abandoned attempt's launch timings (unless drained meanwhile)
@@ -2284,6 +2444,7 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     out->halo_ms = h->halo_ms;
     out->overlap_launches = h->overlap_launches;
     out->skew_half_launches = h->skew_half_launches;
+    out->lds_launches = h->lds_launches;
     out->words_per_lane = h->W % 32 == 0 ? wpl_for(h) : 0;
     out->persist_depth = h->W % 32 == 0 ? persist_depth_for(h, wpl_for(h)) : 0;
     return GOLHIP_OK;
@@ -2327,6 +2488,7 @@ int golhip_perf_reset(golhip_t h) {
     h->halo_ms = 0;
     h->overlap_launches = 0;
     h->skew_half_launches = 0;
+    h->lds_launches = 0;
     return GOLHIP_OK;
 }
 

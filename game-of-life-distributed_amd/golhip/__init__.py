@@ -60,6 +60,7 @@ class Perf(ctypes.Structure):
         ("halo_ms", ctypes.c_double),
         ("overlap_launches", ctypes.c_int64),
         ("skew_half_launches", ctypes.c_int64),
+        ("lds_launches", ctypes.c_int64),
     ]
 
     def as_dict(self) -> dict:

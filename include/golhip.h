@@ -92,6 +92,8 @@ typedef struct golhip_perf {
                                  exchange (side stream) and interior rows (option
                                  "overlap")                                     */
     int64_t skew_half_launches; /* of skew_launches, those on half-wave tiles    */
+    int64_t lds_launches;     /* of persist_launches, those that ran resident LDS
+                                 bands (gol_lds_band_kernel, kernel_variant 4)  */
 } golhip_perf_t;
 
 /* ---- library ---------------------------------------------------------- */
@@ -152,6 +154,12 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * (default -1 = auto: off where the skewed band stacks fill the CUs, else on
  * for buffers of at most 64 MiB; 1 on, 0 off): resident multi-super-step kernel for long runs on a
  * whole torus (never in a multi-rank ring);
+ * "lds_band" (default -1 = auto: on wherever the resident kernel runs and a
+ * band of >= lds_depth full-width rows per CU fits both its LDS buffers;
+ * 1 the same, 0 off): resident LDS bands (gol_lds_band_kernel, W % 128 == 0;
+ * under the same guard and timeout as the resident kernel); "lds_depth"
+ * (0 = plan): turns per LDS-band super-step; "lds_xcd" (1): consecutive
+ * bands on one XCD;
  * "persist_depth" (default 0 = tb_depth): turns per super-step;
  * "persist_half" (default 1): a remainder of half a super-step runs as the
  * resident kernel's last, half-depth super-step;

@@ -223,22 +223,26 @@ def test_step_flips_truncates_and_advances(fixtures):
 
 # ------------------------------------------------------------ resident-kernel guard
 @pytest.mark.parametrize("N,depth,wpl", [(4096, 16, 1), (2048, 8, 2)])
-def test_persistent_timeout_restores_and_reruns(coracle, N, depth, wpl):
-    """A resident launch whose workgroups give up waiting (a 1 us bound stands
-    in for a co-tenant kernel holding CUs) is detected, the board restored and
-    the step re-run on the per-launch kernels: the result is still exact."""
+@pytest.mark.parametrize("lds", [0, 1])
+def test_persistent_timeout_restores_and_reruns(coracle, N, depth, wpl, lds):
+    """A resident launch (K1p, or K1r's LDS bands) whose workgroups give up
+    waiting (a 1 us bound stands in for a co-tenant kernel holding CUs) is
+    detected, the board restored and the step re-run on the per-launch
+    kernels: the result is still exact."""
     board = coracle.fill_random(N, N // 2, 0x5EED0023)
     turns = 6 * depth + 3
     want = coracle.run(board, turns)
     with golhip.Board(N, N // 2) as b:
         b.set_option("persistent", 1)
+        b.set_option("lds_band", lds)
+        b.set_option("lds_depth", depth)
         b.set_option("wpl", wpl)
         b.set_tb_depth(depth)
         b.set_option("persist_timeout_us", 1)
         b.load_bytes(board)
         b.step(turns)
         p = b.perf()
-        assert p["persist_fallbacks"] == 1 and p["persist_launches"] == 0
+        assert p["persist_fallbacks"] == 1 and p["persist_launches"] == 0 and p["lds_launches"] == 0
         assert np.array_equal(b.snapshot_bytes(), want)
         assert b.alive_count() == (int((want == 255).sum()), turns)
         b.step(10)

@@ -394,6 +394,7 @@ def test_persistent_waves_per_workgroup(coracle, N, depth, wpl, nw):
     want = coracle.run(board, turns)
     with golhip.Board(N, N // 2) as b:
         b.set_option("persistent", 1)
+        b.set_option("lds_band", 0)  # K1p itself (K1r: tests/test_gpu_lds.py)
         b.set_option("wpl", wpl)
         b.set_option("persist_waves", nw)
         b.set_tb_depth(depth)
@@ -564,6 +565,7 @@ def test_persistent_half_last_super_step(coracle, N, depth, wpl, half):
     want = coracle.run(board, turns)
     with golhip.Board(N, N) as b:
         b.set_option("persistent", 1)
+        b.set_option("lds_band", 0)  # K1p itself (K1r: tests/test_gpu_lds.py)
         b.set_option("persist_half", half)
         b.set_option("wpl", wpl)
         b.set_tb_depth(depth)
@@ -607,6 +609,7 @@ def test_persistent_unequal_bands(coracle, N, depth, wpl, nw, split, tx):
         b.set_option("age_split", split)
         b.set_option("persist_wg_tx", tx)
         b.set_option("persistent", 1)
+        b.set_option("lds_band", 0)  # K1p itself (K1r: tests/test_gpu_lds.py)
         b.set_tb_depth(depth)
         b.load_bytes(board)
         b.step(turns)
@@ -630,6 +633,7 @@ def test_persistent_paired_bands(coracle, N, rows, depth, wpl, nw, tx):
         b.set_option("persist_wg_tx", tx)
         b.set_option("paired_bands", 1)
         b.set_option("persistent", 1)
+        b.set_option("lds_band", 0)  # K1p itself (K1r: tests/test_gpu_lds.py)
         b.set_tb_depth(depth)
         b.load_bytes(board)
         b.step(turns)
