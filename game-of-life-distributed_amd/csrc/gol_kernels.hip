@@ -1960,26 +1960,34 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
                 x[1] = lds_load<WPL>(A + (lo + 2) * LS, o, ol, orr);
                 const uint32_t *ld = A + (lo + 3) * LS;
                 uint32_t *st = B + lo * LS + o;
-                for (int r0 = lo; r0 < hi; r0 += 3) {
+                // one row of the rotation (q static): its sums from the prefetched words,
+                // the prefetch of row r + 3, the rule, the store
+                auto row = [&](auto qc) {
+                    constexpr int q = decltype(qc)::value;
+                    lds_sums<WPL>(x[q], s[(q + 2) % 3]);
+                    x[(q + 2) % 3] = lds_load<WPL>(ld + q * LS, o, ol, orr);
+                    const LdsRow<WPL> &a = s[q % 3], &b = s[(q + 1) % 3], &n = s[(q + 2) % 3];
+                    uint32_t out[WPL];
 #pragma unroll
-                    for (int q = 0; q < 3; ++q) {
-                        if (r0 + q < hi) {
-                            lds_sums<WPL>(x[q], s[(q + 2) % 3]);
-                            x[(q + 2) % 3] = lds_load<WPL>(ld + q * LS, o, ol, orr);
-                            const LdsRow<WPL> &a = s[q % 3], &b = s[(q + 1) % 3], &n = s[(q + 2) % 3];
-                            uint32_t out[WPL];
-#pragma unroll
-                            for (int m = 0; m < WPL; ++m)
-                                out[m] = rule_word(a.s0[m], a.s1[m], b.s0[m], b.s1[m], n.s0[m], n.s1[m], b.c[m]);
-                            if constexpr (WPL == 1)
-                                st[q * LS] = out[0];
-                            else
-                                *reinterpret_cast<uint2 *>(st + q * LS) = make_uint2(out[0], out[1]);
-                        }
-                    }
+                    for (int m = 0; m < WPL; ++m)
+                        out[m] = rule_word(a.s0[m], a.s1[m], b.s0[m], b.s1[m], n.s0[m], n.s1[m], b.c[m]);
+                    if constexpr (WPL == 1)
+                        st[q * LS] = out[0];
+                    else
+                        *reinterpret_cast<uint2 *>(st + q * LS) = make_uint2(out[0], out[1]);
+                };
+                // whole groups of three rows with no branch between them (the
+                // scheduler interleaves three independent rows), then at most two
+                int r0 = lo;
+                for (; r0 + 3 <= hi; r0 += 3) {
+                    row(std::integral_constant<int, 0>{});
+                    row(std::integral_constant<int, 1>{});
+                    row(std::integral_constant<int, 2>{});
                     ld += 3 * LS;
                     st += 3 * LS;
                 }
+                if (r0 < hi) row(std::integral_constant<int, 0>{});
+                if (r0 + 1 < hi) row(std::integral_constant<int, 1>{});
             }
             __syncthreads();
             uint32_t *T = A;
