@@ -36,7 +36,7 @@ for st in "$@"; do
       wl=${arg:-65536}
       timeout -k 10 400 python -u bench.py --workload $wl > $out/bench_$wl.json 2> $out/bench_$wl.err \
         || { tail $out/bench_$wl.err; cat $out/bench_$wl.json; exit 1; }
-      python3 -c "import json; d=json.load(open('$out/bench_$wl.json')); print('$wl', d['value'], d['parity'], d['roofline'].get('avg_launch_ms'), d['roofline'].get('frac'))" ;;
+      python3 -c "import json; d=json.load(open('$out/bench_$wl.json')); print('$wl', d['value'], d['parity'], d.get('roofline', {}).get('avg_launch_ms'), d.get('roofline', {}).get('frac'))" ;;
     trace)
       wl=${arg:-65536}
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$out/trace_$wl -o run \
