@@ -1934,82 +1934,128 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
             lap(3);
         }
         const int Dj = min(D, p.turns - j * D);
-        // the last, shorter super-step needs only Dj halo rows of the D
-        const int skip = D - Dj;
-        for (int t = 1; t <= Dj; ++t) {
-            const int lo_t = skip + t, hi_t = R - skip - t;
-            const int len = (hi_t - lo_t + K - 1) / K;
+        const bool more = j + 1 < J;
+        // One run of rows [lo, hi) of pair (word) column c: the new generation
+        // of those rows from Ab into Bb.
+        auto run_rows = [&](const uint32_t *Ab, uint32_t *Bb, int lo, int hi, int c) {
+            const int cl = c == 0 ? P - 1 : c - 1, cr = c == P - 1 ? 0 : c + 1;
+            const int o = WPL * c, ol = WPL == 1 ? cl : 2 * cl + 1, orr = WPL * cr;
+            // rows r - 1, r, r + 1 in s[(q + 0..2) % 3]; the words of rows r + 1 and
+            // r + 2 already loaded (n1, n2) while row r is computed: the LDS
+            // latency hides behind a row's rule (two waves per SIMD hide little)
+            // the raw words of row r0 + q + 1 in x[q], of r0 + q + 2 in x[q + 1]
+            // (in flight); row r0 + q + 3 goes to x[q + 2] (indices mod 3, all
+            // static in the unrolled body: no register copies, no early waits).
+            // Rows past R - 1 land in the buffer's 3 spare rows (never used).
+            LdsRow<WPL> s[3];
+            LdsRaw<WPL> x[3];
+            lds_sums<WPL>(lds_load<WPL>(Ab + (lo - 1) * LS, o, ol, orr), s[0]);
+            lds_sums<WPL>(lds_load<WPL>(Ab + lo * LS, o, ol, orr), s[1]);
+            x[0] = lds_load<WPL>(Ab + (lo + 1) * LS, o, ol, orr);
+            x[1] = lds_load<WPL>(Ab + (lo + 2) * LS, o, ol, orr);
+            const uint32_t *ld = Ab + (lo + 3) * LS;
+            uint32_t *st = Bb + lo * LS + o;
+            // one row of the rotation (q static): its sums from the prefetched words,
+            // the prefetch of row r + 3, the rule, the store
+            auto row = [&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                lds_sums<WPL>(x[q], s[(q + 2) % 3]);
+                x[(q + 2) % 3] = lds_load<WPL>(ld + q * LS, o, ol, orr);
+                const LdsRow<WPL> &a = s[q % 3], &b = s[(q + 1) % 3], &n = s[(q + 2) % 3];
+                uint32_t out[WPL];
+#pragma unroll
+                for (int m = 0; m < WPL; ++m)
+                    out[m] = rule_word(a.s0[m], a.s1[m], b.s0[m], b.s1[m], n.s0[m], n.s1[m], b.c[m]);
+                if constexpr (WPL == 1)
+                    st[q * LS] = out[0];
+                else
+                    *reinterpret_cast<uint2 *>(st + q * LS) = make_uint2(out[0], out[1]);
+            };
+            // whole groups of three rows with no branch between them (the
+            // scheduler interleaves three independent rows), then at most two
+            int r0 = lo;
+            for (; r0 + 3 <= hi; r0 += 3) {
+                row(std::integral_constant<int, 0>{});
+                row(std::integral_constant<int, 1>{});
+                row(std::integral_constant<int, 2>{});
+                ld += 3 * LS;
+                st += 3 * LS;
+            }
+            if (r0 < hi) row(std::integral_constant<int, 0>{});
+            if (r0 + 1 < hi) row(std::integral_constant<int, 1>{});
+        };
+        // One turn over the rows [lo0, hi0) and [lo1, hi1) (either may be empty):
+        // K runs per column over the two ranges laid end to end, then a barrier.
+        auto do_turn = [&](const uint32_t *Ab, uint32_t *Bb, int lo0, int hi0, int lo1, int hi1) {
+            const int n0 = max(0, hi0 - lo0), n = n0 + max(0, hi1 - lo1);
+            const int len = (n + K - 1) / K;
             for (int u = threadIdx.x; u < units; u += NT) {
                 const int k = u / P, c = u - k * P;
-                const int lo = lo_t + k * len, hi = min(lo + len, hi_t);
-                if (lo >= hi) continue;
-                const int cl = c == 0 ? P - 1 : c - 1, cr = c == P - 1 ? 0 : c + 1;
-                const int o = WPL * c, ol = WPL == 1 ? cl : 2 * cl + 1, orr = WPL * cr;
-                // rows r - 1, r, r + 1 in s[(q + 0..2) % 3]; the words of rows r + 1 and
-                // r + 2 already loaded (n1, n2) while row r is computed: the LDS
-                // latency hides behind a row's rule (two waves per SIMD hide little)
-                // the raw words of row r0 + q + 1 in x[q], of r0 + q + 2 in x[q + 1]
-                // (in flight); row r0 + q + 3 goes to x[q + 2] (indices mod 3, all
-                // static in the unrolled body: no register copies, no early waits).
-                // Rows past R - 1 land in the buffer's 3 spare rows (never used).
-                LdsRow<WPL> s[3];
-                LdsRaw<WPL> x[3];
-                lds_sums<WPL>(lds_load<WPL>(A + (lo - 1) * LS, o, ol, orr), s[0]);
-                lds_sums<WPL>(lds_load<WPL>(A + lo * LS, o, ol, orr), s[1]);
-                x[0] = lds_load<WPL>(A + (lo + 1) * LS, o, ol, orr);
-                x[1] = lds_load<WPL>(A + (lo + 2) * LS, o, ol, orr);
-                const uint32_t *ld = A + (lo + 3) * LS;
-                uint32_t *st = B + lo * LS + o;
-                // one row of the rotation (q static): its sums from the prefetched words,
-                // the prefetch of row r + 3, the rule, the store
-                auto row = [&](auto qc) {
-                    constexpr int q = decltype(qc)::value;
-                    lds_sums<WPL>(x[q], s[(q + 2) % 3]);
-                    x[(q + 2) % 3] = lds_load<WPL>(ld + q * LS, o, ol, orr);
-                    const LdsRow<WPL> &a = s[q % 3], &b = s[(q + 1) % 3], &n = s[(q + 2) % 3];
-                    uint32_t out[WPL];
-#pragma unroll
-                    for (int m = 0; m < WPL; ++m)
-                        out[m] = rule_word(a.s0[m], a.s1[m], b.s0[m], b.s1[m], n.s0[m], n.s1[m], b.c[m]);
-                    if constexpr (WPL == 1)
-                        st[q * LS] = out[0];
-                    else
-                        *reinterpret_cast<uint2 *>(st + q * LS) = make_uint2(out[0], out[1]);
-                };
-                // whole groups of three rows with no branch between them (the
-                // scheduler interleaves three independent rows), then at most two
-                int r0 = lo;
-                for (; r0 + 3 <= hi; r0 += 3) {
-                    row(std::integral_constant<int, 0>{});
-                    row(std::integral_constant<int, 1>{});
-                    row(std::integral_constant<int, 2>{});
-                    ld += 3 * LS;
-                    st += 3 * LS;
-                }
-                if (r0 < hi) row(std::integral_constant<int, 0>{});
-                if (r0 + 1 < hi) row(std::integral_constant<int, 1>{});
+                const int v0 = k * len, v1 = min(v0 + len, n);
+                if (v0 >= v1) continue;
+                if (v0 < n0) run_rows(Ab, Bb, lo0 + v0, lo0 + min(v1, n0), c);
+                if (v1 > n0) run_rows(Ab, Bb, lo1 + max(v0, n0) - n0, lo1 + v1 - n0, c);
             }
             __syncthreads();
-            uint32_t *T = A;
-            A = B;
-            B = T;
-        }
-        lap(0);
-        if (j + 1 < J) {
-            // publish generation (j + 1) D: rows [D, 2D) (side 0) and [h, h + D) (side 1)
+        };
+        // Edge rows of generation (j + 1) D from F: [D, 2D) (side 0) and [h, h + D)
+        // (side 1) to slot (j + 1) & 1, write-through; signal() waits for them
+        // (every wave's vmcnt(0), a barrier) and raises the flag.
+        auto publish = [&](const uint32_t *F) {
             const int slot = (j + 1) & 1;
             const int e0 = (((slot * nb + b) * 2) * eq4) * 16;
             for (int i = threadIdx.x; i < 2 * eq4; i += NT) {
                 const bool top = i < eq4;
                 const int g = top ? i : i - eq4;
-                const uint4 v = *reinterpret_cast<const uint4 *>(A + (size_t)(top ? D : h) * LS + 4 * (g % q4) + (size_t)(g / q4) * LS);
+                const uint4 v = *reinterpret_cast<const uint4 *>(F + (size_t)(top ? D : h) * LS + 4 * (g % q4) + (size_t)(g / q4) * LS);
                 __builtin_amdgcn_raw_buffer_store_b128((v4u32){v.x, v.y, v.z, v.w}, ers,
                                                        e0 + (top ? 0 : eq4 * 16) + g * 16, 0, kCpolSc1);
             }
+        };
+        auto signal = [&]() {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (threadIdx.x == 0)
                 __hip_atomic_store(&p.progress[b], (unsigned)(j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        };
+        if (p.split && Dj == D) {
+            // Boundary first: turn t computes the top rows [t, 3D - t) and the bottom
+            // rows [h - D + t, h + 2D - t) (the only rows the edges depend on), the
+            // edges leave, and the interior [3D - t, h - D + t) follows while they
+            // travel.  Turn t of the interior reads turn t - 1's rows 3D - t - 1 ..
+            // 3D - t and h - D + t - 1 .. h - D + t from the edge phase: still in the
+            // turn-(t - 1) buffer, since the edge phase's turn t + 1 stopped at row
+            // 3D - t - 2 (started at h - D + t + 1).  Turn t's buffer is A for even
+            // t, B for odd.
+            for (int t = 1; t <= D; ++t)
+                do_turn((t & 1) ? A : B, (t & 1) ? B : A, t, 3 * D - t, h - D + t, h + 2 * D - t);
+            uint32_t *F = (D & 1) ? B : A;
+            lap(0);
+            if (more) publish(F);
+            lap(1);
+            for (int t = 1; t <= D; ++t) {
+                do_turn((t & 1) ? A : B, (t & 1) ? B : A, 3 * D - t, h - D + t, 0, 0);
+                if (t == 1 && more) signal();
+            }
+            if (F != A) {
+                B = A;
+                A = F;
+            }
+            lap(0);
+        } else {
+            // the last, shorter super-step needs only Dj halo rows of the D
+            const int skip = D - Dj;
+            for (int t = 1; t <= Dj; ++t) {
+                do_turn(A, B, skip + t, R - skip - t, 0, 0);
+                uint32_t *T = A;
+                A = B;
+                B = T;
+            }
+            lap(0);
+            if (more) {
+                publish(A);
+                signal();
+            }
             lap(1);
         }
     }

@@ -135,3 +135,21 @@ def test_lds_band_variants(coracle, W, H, opts):
     got, p = run_lds(board, turns, 8, **opts)
     assert p["lds_launches"] == 1
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("wpl", [1, 2])
+@pytest.mark.parametrize("depth", [1, 2, 3, 4, 5, 8, 12])
+@pytest.mark.parametrize("W,H", [(1024, 1024), (2048, 1003), (8192, 8192), (5120, 5120), (640, 384)])
+def test_lds_band_split_matches_oracle(coracle, wpl, depth, W, H):
+    """Boundary-first super-steps (option lds_split): the edge rows' D turns
+    first, their publish, then the interior while they travel.  Bands of
+    4D - 2 rows and more split cleanly; shorter ones compute the overlap of
+    the two edge regions twice (same values) and have no interior."""
+    if W * H > 2048 * 2048 and depth not in (3, 5, 8):
+        pytest.skip("large boards at a few depths")
+    board = coracle.fill_random(W, H, 0x5EED0047 + W + H + depth)
+    turns = 3 * depth + 2  # two full super-steps and a short one
+    want = coracle.run(board, turns)
+    got, p = run_lds(board, turns, depth, wpl, lds_split=1)
+    assert p["lds_launches"] == 1
+    assert np.array_equal(got, want)
