@@ -153,3 +153,20 @@ def test_lds_band_split_matches_oracle(coracle, wpl, depth, W, H):
     got, p = run_lds(board, turns, depth, wpl, lds_split=1)
     assert p["lds_launches"] == 1
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("W,H", [(128, 3), (128, 5), (256, 4), (256, 13), (384, 12), (128, 1000)])
+def test_lds_band_tiny_boards(coracle, W, H):
+    """Rows of 2-6 pairs (many runs a wave, neighbours across the row's wrap in
+    one run) and boards shorter than the default depth (D = H rows, one band)."""
+    board = coracle.fill_random(W, H, 0x5EED0048 + W + H)
+    turns = 37
+    want = coracle.run(board, turns)
+    with golhip.Board(W, H) as b:
+        b.set_option("persistent", 1)
+        b.load_bytes(board)
+        b.step(turns)
+        assert b.perf()["lds_launches"] == 1
+        got = b.snapshot_bytes()
+        assert b.alive_count() == (int((want == 255).sum()), turns)
+    assert np.array_equal(got, want)
