@@ -150,6 +150,7 @@ struct LdsBandArgs {
     int nt;                // threads per workgroup: 512 or 1024
     int stride;            // LDS words per row: lds_band_stride (>= Ww)
     int split;             // 1: full super-steps compute their edge rows first, publish, then the interior
+    int fault;             // tests: band 0 never publishes, so its neighbours' waits time out
     unsigned long long *trace;  // nullable: [0..3] += ticks in compute, publish, wait, halo load; [4] += workgroups
 };
 __host__ __device__ inline int64_t lds_band_edge_words(int nb, int D, int Ww) { return 4ll * nb * D * Ww; }

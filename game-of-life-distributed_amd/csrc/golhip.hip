@@ -141,6 +141,7 @@ struct golhip {
     int lds_wg_cu = 1;              // option "lds_wg_cu": K1r bands (workgroups) per CU (1 or 2)
     int lds_stride = 1;             // option "lds_stride": K1r LDS rows at a compile-time stride where instantiated
     int lds_split = 0;              // option "lds_split": K1r super-steps compute and publish their edge rows first
+    int lds_fault = 0;              // option "lds_fault" (tests): K1r band 0 never publishes its edges
     uint32_t *lds_edge = nullptr;   // K1r edge rows (golk::lds_band_edge_words)
     int64_t lds_edge_cap = 0;
     int64_t lds_launches = 0;
@@ -1109,6 +1110,7 @@ bool lds_fits(golhip_t h, int wpl, golk::LdsBandArgs *out) {
         out->nt = nt;
         out->stride = stride;
         out->split = h->lds_split;
+        out->fault = h->lds_fault;
     }
     return true;
 }
@@ -1846,6 +1848,11 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     if (!strcmp(key, "lds_wg_cu")) {
         if (value < 1 || value > 2) return fail(GOLHIP_EINVAL, "lds_wg_cu %lld", (long long)value);
         h->lds_wg_cu = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "lds_fault")) {
+        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "lds_fault %lld", (long long)value);
+        h->lds_fault = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "lds_split")) {

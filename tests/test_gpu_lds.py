@@ -170,3 +170,24 @@ def test_lds_band_tiny_boards(coracle, W, H):
         got = b.snapshot_bytes()
         assert b.alive_count() == (int((want == 255).sum()), turns)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("split", [0, 1])
+def test_lds_band_wait_timeout(coracle, split):
+    """Band 0 never publishes its edges (test hook lds_fault): its neighbours'
+    flag waits reach the bound, every workgroup drains, and the step is
+    restored and re-run on the per-launch kernels, exactly."""
+    board = coracle.fill_random(2048, 1024, 0x5EED004A)
+    want = coracle.run(board, 51)
+    with golhip.Board(2048, 1024) as b:
+        b.set_option("persistent", 1)
+        b.set_option("lds_split", split)
+        b.set_option("lds_fault", 1)
+        b.set_option("lds_depth", 8)
+        b.set_option("persist_timeout_us", 2000)
+        b.load_bytes(board)
+        b.step(51)
+        p = b.perf()
+        got = b.snapshot_bytes()
+    assert p["persist_fallbacks"] == 1 and p["lds_launches"] == 0
+    assert np.array_equal(got, want)
