@@ -158,8 +158,14 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * band of >= lds_depth full-width rows per CU fits both its LDS buffers;
  * 1 the same, 0 off): resident LDS bands (gol_lds_band_kernel, W % 128 == 0;
  * under the same guard and timeout as the resident kernel); "lds_depth"
- * (0 = plan): turns per LDS-band super-step; "lds_xcd" (1): consecutive
- * bands on one XCD;
+ * (0 = plan: 12, at most the rows): turns per LDS-band super-step; "lds_xcd"
+ * (1): consecutive bands on one XCD; "lds_stride" (1): LDS rows at a
+ * compile-time stride where one is instantiated; "lds_waves" (8 or 16) and
+ * "lds_wg_cu" (1 or 2): waves per workgroup and bands per CU; "lds_split" (0):
+ * full super-steps compute and publish their edge rows before the interior
+ * (measured slower); "lds_fault" (0, tests): band 0 never
+ * publishes its edges, so its neighbours' bounded waits time out and the step
+ * is restored and re-run;
  * "persist_depth" (default 0 = tb_depth): turns per super-step;
  * "persist_half" (default 1): a remainder of half a super-step runs as the
  * resident kernel's last, half-depth super-step;
