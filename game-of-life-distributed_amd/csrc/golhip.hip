@@ -1084,6 +1084,15 @@ bool lds_fits(golhip_t h, int wpl, golk::LdsBandArgs *out) {
     const int D = h->lds_depth > 0 ? h->lds_depth : std::min(12, h->rows);
     if (h->rows < D || D < 1) return false;
     const int nt = 64 * h->lds_waves;
+    // auto: only where the rows' pairs (words) keep >= 90 % of the threads busy
+    // (runs of whole columns: 512 / P runs each; 12288 x 2048 = 192 pairs a row
+    // keeps 384 of 512 and ran 11.0 vs K1p's 13.0 TCUPS, while 1024^2 .. 8192^2,
+    // 3072^2 and 8192 x 4096 run 1.3-2.1x K1p, profiles/r4x)
+    if (h->lds_band < 0) {
+        const int64_t P = h->Ww / wpl, units = P * std::max<int64_t>(1, nt / P);
+        const int64_t slots = (units + nt - 1) / nt * nt;  // passes x threads
+        if (10 * units < 9 * slots) return false;
+    }
     // one progress word per band after d_sync's error word (2 dev_cu + 2 words)
     const int nb = std::min(std::min(h->cu_count, h->dev_cu) * h->lds_wg_cu, h->rows / D);
     if (nb < 1) return false;

@@ -191,3 +191,19 @@ def test_lds_band_wait_timeout(coracle, split):
         got = b.snapshot_bytes()
     assert p["persist_fallbacks"] == 1 and p["lds_launches"] == 0
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("W,H,lds", [(12288, 2048, 0), (5120, 1280, 1), (3072, 3072, 1)])
+def test_lds_band_auto_choice(coracle, W, H, lds):
+    """The auto plan runs K1r only where a row's pairs keep >= 90 % of the
+    threads busy (12288 wide: 192 pairs, 384 of 512 threads: K1p, which was
+    faster there); the result is exact either way."""
+    board = coracle.fill_random(W, H, 0x5EED004B + W)
+    want = coracle.run(board, 40)
+    with golhip.Board(W, H) as b:
+        b.load_bytes(board)
+        b.step(40)
+        p = b.perf()
+        got = b.snapshot_bytes()
+    assert p["lds_launches"] == lds and p["persist_launches"] == 1
+    assert np.array_equal(got, want)
