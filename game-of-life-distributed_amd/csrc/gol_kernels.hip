@@ -1789,8 +1789,11 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
 // by super-step parity: the wait for a neighbour's super-step j flag also
 // proves it read our j - 1 edges, which the slot we overwrite held.
 // Per row and word: three LDS loads (own word or pair, one neighbour word
-// each side), the row sums (9 - 2 LUTs of stage()), the column sums and the
-// rule, one LDS store.  Every wait is bounded (error word, all drain).
+// each side), the row sums (2 LUTs, and a funnel shift per pair side), the
+// column sums and the rule (7 LUTs), one LDS store; each buffer has 3 spare
+// rows for the row loop's prefetch.  Option lds_split runs a full super-step
+// boundary first (edge rows, publish, interior).  Every wait
+// is bounded (error word, all drain).
 // ---------------------------------------------------------------------------
 template <int WPL>
 struct LdsRow {
