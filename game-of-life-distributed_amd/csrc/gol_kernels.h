@@ -151,6 +151,8 @@ struct LdsBandArgs {
     int stride;            // LDS words per row: lds_band_stride (>= Ww)
     int split;             // 1: full super-steps compute their edge rows first, publish, then the interior
     int fault;             // tests: band 0 never publishes, so its neighbours' waits time out
+    int pre;               // > 0: full super-steps run their first `pre` turns on the interior rows
+                           //      while the halos travel (lds_pre)
     unsigned long long *trace;  // nullable: [0..3] += ticks in compute, publish, wait, halo load; [4] += workgroups
 };
 __host__ __device__ inline int64_t lds_band_edge_words(int nb, int D, int Ww) { return 4ll * nb * D * Ww; }

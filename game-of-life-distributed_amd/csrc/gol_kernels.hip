@@ -1898,44 +1898,8 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
             tr_t = now;
         }
     };
+    bool pending = false;  // lds_pre: our last edges are out, their flag not yet raised
     for (int j = 0; j < J; ++j) {
-        if (j > 0) {
-            // neighbours' super-step j edges (generation j D)
-            if (w == 0) {
-                const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-                const int nbr = lane == 0 ? up : down;
-                for (;;) {
-                    const unsigned v = lane < 2 ? __hip_atomic_load(&p.progress[nbr], __ATOMIC_RELAXED,
-                                                                    __HIP_MEMORY_SCOPE_AGENT)
-                                                : (unsigned)j;
-                    if (__all(v >= (unsigned)j)) break;
-                    const unsigned err = __hip_atomic_load(p.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (err || (long long)__builtin_amdgcn_s_memrealtime() - t0 > p.timeout_ticks) {
-                        if (lane == 0) {
-                            atomicOr(p.error, 1u);
-                            s_abort = 1;
-                        }
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-            __syncthreads();
-            if (s_abort) return;  // uniform over the workgroup
-            lap(2);
-            const int slot = j & 1;
-            const int eu = (((slot * nb + up) * 2 + 1) * eq4) * 16;    // up's bottom D rows -> rows [0, D)
-            const int ed = (((slot * nb + down) * 2 + 0) * eq4) * 16;  // down's top D rows -> rows [D + h, R)
-            for (int i = threadIdx.x; i < 2 * eq4; i += NT) {
-                const bool top = i < eq4;
-                const int g = top ? i : i - eq4;
-                const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(ers, (top ? eu : ed) + g * 16, 0, kCpolSc1);
-                uint32_t *dstw = A + (size_t)(top ? 0 : D + h) * LS + 4 * (g % q4) + (size_t)(g / q4) * LS;
-                *reinterpret_cast<uint4 *>(dstw) = make_uint4(v.x, v.y, v.z, v.w);
-            }
-            __syncthreads();
-            lap(3);
-        }
         const int Dj = min(D, p.turns - j * D);
         const bool more = j + 1 < J;
         // One run of rows [lo, hi) of pair (word) column c: the new generation
@@ -2016,13 +1980,93 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
                                                        e0 + (top ? 0 : eq4 * 16) + g * 16, 0, kCpolSc1);
             }
         };
-        auto signal = [&]() {
-            if (p.fault && b == 0) return;
+        auto signal = [&](unsigned v) {  // progress = v: the edges of generation v D are out
+            if (p.fault && b == 0) return;   // (b is uniform over the workgroup)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (threadIdx.x == 0)
-                __hip_atomic_store(&p.progress[b], (unsigned)(j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&p.progress[b], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         };
+        // Neighbours' super-step j edges (generation j D) into the halo rows of A;
+        // false if the wait timed out (every workgroup drains).
+        auto wait_halos = [&]() -> bool {
+            // neighbours' super-step j edges (generation j D)
+            if (w == 0) {
+                const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+                const int nbr = lane == 0 ? up : down;
+                for (;;) {
+                    const unsigned v = lane < 2 ? __hip_atomic_load(&p.progress[nbr], __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT)
+                                                : (unsigned)j;
+                    if (__all(v >= (unsigned)j)) break;
+                    const unsigned err = __hip_atomic_load(p.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (err || (long long)__builtin_amdgcn_s_memrealtime() - t0 > p.timeout_ticks) {
+                        if (lane == 0) {
+                            atomicOr(p.error, 1u);
+                            s_abort = 1;
+                        }
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            __syncthreads();
+            if (s_abort) return false;  // uniform over the workgroup
+            lap(2);
+            const int slot = j & 1;
+            const int eu = (((slot * nb + up) * 2 + 1) * eq4) * 16;    // up's bottom D rows -> rows [0, D)
+            const int ed = (((slot * nb + down) * 2 + 0) * eq4) * 16;  // down's top D rows -> rows [D + h, R)
+            for (int i = threadIdx.x; i < 2 * eq4; i += NT) {
+                const bool top = i < eq4;
+                const int g = top ? i : i - eq4;
+                const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(ers, (top ? eu : ed) + g * 16, 0, kCpolSc1);
+                uint32_t *dstw = A + (size_t)(top ? 0 : D + h) * LS + 4 * (g % q4) + (size_t)(g / q4) * LS;
+                *reinterpret_cast<uint4 *>(dstw) = make_uint4(v.x, v.y, v.z, v.w);
+            }
+            __syncthreads();
+            lap(3);
+            return true;
+        };
+        // interior first (option lds_pre = k): the first k turns of a full
+        // super-step run on the rows that need no halo, [D + t, D + h - t), while
+        // the neighbours' edges travel (and the previous edges' signal goes out
+        // after the first of them); then the halo-adjacent rows of those turns,
+        // [t, D + t) and [D + h - t, R - t), then whole turns.  Turn t's halo-side
+        // rows read turn t - 1's interior rows D + t - 1, D + t (bottom: D + h - t
+        // - 1, D + h - t), which the interior turns t + 1, t + 3, .. (same buffer)
+        // never reach.  Turn t's buffer is A for even t, B for odd.
+        const int pre = (j > 0 && Dj == D && !p.split) ? min(p.pre, D) : 0;
+        if (pre > 0) {
+            for (int t = 1; t <= pre; ++t) {
+                do_turn((t & 1) ? A : B, (t & 1) ? B : A, D + t, D + h - t, 0, 0);
+                if (t == 1 && pending) {
+                    signal((unsigned)j);
+                    pending = false;
+                }
+            }
+            lap(0);
+            if (!wait_halos()) return;
+            for (int t = 1; t <= pre; ++t)
+                do_turn((t & 1) ? A : B, (t & 1) ? B : A, t, D + t, D + h - t, R - t);
+            for (int t = pre + 1; t <= D; ++t) do_turn((t & 1) ? A : B, (t & 1) ? B : A, t, R - t, 0, 0);
+            uint32_t *F = (D & 1) ? B : A;
+            if (F != A) {
+                B = A;
+                A = F;
+            }
+            lap(0);
+            if (more) {
+                publish(A);
+                pending = true;  // signalled after the next super-step's first interior turn
+            }
+            lap(1);
+            continue;
+        }
+        if (pending) {
+            signal((unsigned)j);
+            pending = false;
+        }
+        if (j > 0 && !wait_halos()) return;
         if (p.split && Dj == D) {
             // Boundary first: turn t computes the top rows [t, 3D - t) and the bottom
             // rows [h - D + t, h + 2D - t) (the only rows the edges depend on), the
@@ -2040,7 +2084,7 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
             lap(1);
             for (int t = 1; t <= D; ++t) {
                 do_turn((t & 1) ? A : B, (t & 1) ? B : A, 3 * D - t, h - D + t, 0, 0);
-                if (t == 1 && more) signal();
+                if (t == 1 && more) signal((unsigned)(j + 1));
             }
             if (F != A) {
                 B = A;
@@ -2059,7 +2103,12 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
             lap(0);
             if (more) {
                 publish(A);
-                signal();
+                // the next super-step signals after its first interior turn when it
+                // runs interior first (full, lds_pre), else now
+                if (p.pre > 0 && !p.split && min(D, p.turns - (j + 1) * D) == D)
+                    pending = true;
+                else
+                    signal((unsigned)(j + 1));
             }
             lap(1);
         }

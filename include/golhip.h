@@ -163,7 +163,9 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * compile-time stride where one is instantiated; "lds_waves" (8 or 16) and
  * "lds_wg_cu" (1 or 2): waves per workgroup and bands per CU; "lds_split" (0):
  * full super-steps compute and publish their edge rows before the interior
- * (measured slower); "lds_fault" (0, tests): band 0 never
+ * (measured slower); "lds_pre" (2): a full super-step's
+ * first turns run on the rows that need no halo while the halos travel;
+ * "lds_fault" (0, tests): band 0 never
  * publishes its edges, so its neighbours' bounded waits time out and the step
  * is restored and re-run;
  * "persist_depth" (default 0 = tb_depth): turns per super-step;

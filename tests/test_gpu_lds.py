@@ -207,3 +207,48 @@ def test_lds_band_auto_choice(coracle, W, H, lds):
         got = b.snapshot_bytes()
     assert p["lds_launches"] == lds and p["persist_launches"] == 1
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("pre", [1, 2, 3, 12])
+@pytest.mark.parametrize("W,H,depth", [(1024, 1024, 8), (2048, 1003, 12), (8192, 8192, 12), (5120, 5120, 12),
+                                       (640, 384, 5), (2048, 2055, 8), (256, 13, 4)])
+def test_lds_band_interior_first(coracle, pre, W, H, depth):
+    """Interior-first super-steps (option lds_pre): the first `pre` turns on the
+    rows that need no halo while the edges travel (the previous flag raised
+    after the first of them), then those turns' halo-side rows, then whole
+    turns; a short last super-step runs whole turns.  Several steps on one
+    handle; pre >= the band height leaves no interior at the later turns."""
+    if W * H > 2048 * 2048 and pre not in (2, 3):
+        pytest.skip("large boards at two values")
+    board = coracle.fill_random(W, H, 0x5EED004C + W + H + pre)
+    steps = [3 * depth + 2, 2 * depth, 7]
+    want = coracle.run(board, sum(steps))
+    with golhip.Board(W, H) as b:
+        b.set_option("persistent", 1)
+        b.set_option("lds_band", 1)
+        b.set_option("lds_pre", pre)
+        b.set_option("lds_depth", depth)
+        b.load_bytes(board)
+        for n in steps:
+            b.step(n)
+        p = b.perf()
+        got = b.snapshot_bytes()
+    assert p["lds_launches"] == 3 and p["persist_fallbacks"] == 0
+    assert np.array_equal(got, want)
+
+
+def test_lds_band_interior_first_timeout(coracle):
+    board = coracle.fill_random(2048, 1024, 0x5EED004D)
+    want = coracle.run(board, 51)
+    with golhip.Board(2048, 1024) as b:
+        b.set_option("persistent", 1)
+        b.set_option("lds_pre", 2)
+        b.set_option("lds_fault", 1)
+        b.set_option("lds_depth", 8)
+        b.set_option("persist_timeout_us", 2000)
+        b.load_bytes(board)
+        b.step(51)
+        p = b.perf()
+        got = b.snapshot_bytes()
+    assert p["persist_fallbacks"] == 1 and p["lds_launches"] == 0
+    assert np.array_equal(got, want)
