@@ -184,10 +184,10 @@ class Chan {
     int try_recv(T &out) {
         if (cap_ == 0) {
             std::lock_guard<std::mutex> rg(recv_mu_);
-            const uint64_t q = seq_.load(std::memory_order_acquire);
+            const uint64_t q = box_.seq.load(std::memory_order_acquire);
             if (q & 1) {
-                out = std::move(slot_);
-                seq_.store(q + 1, std::memory_order_release);
+                out = std::move(box_.value);
+                box_.seq.store(q + 1, std::memory_order_release);
                 wake(send_sleepers0_, send_cv_);
                 return 1;
             }
@@ -220,23 +220,23 @@ class Chan {
     bool send0(T v) {
         std::lock_guard<std::mutex> sg(send_mu_);
         if (closed_a_.load(std::memory_order_acquire)) return false;
-        const uint64_t q = seq_.load(std::memory_order_relaxed);  // even: the previous value was taken
-        slot_ = std::move(v);
-        seq_.store(q + 1, std::memory_order_release);
+        const uint64_t q = box_.seq.load(std::memory_order_relaxed);  // even: the previous value was taken
+        box_.value = std::move(v);
+        box_.seq.store(q + 1, std::memory_order_release);
         wake(recv_sleepers0_, recv_cv_);
         // Go: the send completes when a receiver has the value
-        wait0([&] { return seq_.load(std::memory_order_acquire) != q + 1 || closed_a_.load(std::memory_order_acquire); },
+        wait0([&] { return box_.seq.load(std::memory_order_acquire) != q + 1 || closed_a_.load(std::memory_order_acquire); },
               send_sleepers0_, send_cv_);
         return true;
     }
     bool recv0(T &out) {
         std::lock_guard<std::mutex> rg(recv_mu_);
-        wait0([&] { return (seq_.load(std::memory_order_acquire) & 1) || closed_a_.load(std::memory_order_acquire); },
+        wait0([&] { return (box_.seq.load(std::memory_order_acquire) & 1) || closed_a_.load(std::memory_order_acquire); },
               recv_sleepers0_, recv_cv_);
-        const uint64_t q = seq_.load(std::memory_order_acquire);
+        const uint64_t q = box_.seq.load(std::memory_order_acquire);
         if (!(q & 1)) return false;  // closed, nothing offered
-        out = std::move(slot_);
-        seq_.store(q + 1, std::memory_order_release);
+        out = std::move(box_.value);
+        box_.seq.store(q + 1, std::memory_order_release);
         wake(send_sleepers0_, send_cv_);
         return true;
     }
@@ -293,11 +293,14 @@ class Chan {
     alignas(64) std::atomic<uint64_t> sent_a_{0};
     alignas(64) std::atomic<uint64_t> received_a_{0};
     alignas(64) std::atomic<bool> closed_a_{false};
-    // capacity 0 (send0 / recv0)
+    // capacity 0 (send0 / recv0): the sequence word shares a cache line with
+    // the start of the slot, so a hand-off moves the slot's lines and no other
     alignas(64) std::mutex send_mu_;
     alignas(64) std::mutex recv_mu_;
-    alignas(64) std::atomic<uint64_t> seq_{0};
-    T slot_{};
+    struct alignas(64) Slot {
+        std::atomic<uint64_t> seq{0};
+        T value{};
+    } box_;
     alignas(64) std::atomic<int> send_sleepers0_{0};
     alignas(64) std::atomic<int> recv_sleepers0_{0};
 };
