@@ -425,7 +425,7 @@ def board_hash_np(words: np.ndarray, row0: int = 0) -> int:
 # --------------------------------------------------------------------------
 # host mirror of gol.Run (libgolhost.so, include/golrun.h)
 # --------------------------------------------------------------------------
-HOST_LIB_PATH = os.path.join(HERE, "libgolhost.so")
+HOST_LIB_PATH = os.environ.get("GOLHOST_LIB") or os.path.join(HERE, "libgolhost.so")  # A/B builds
 FLAG_KEYS, FLAG_REF_QUIRKS, FLAG_NO_CELL_EVENTS, FLAG_NO_TURN_EVENTS = 0x1, 0x2, 0x4, 0x8
 ALIVE_CELLS_COUNT, IMAGE_OUTPUT_COMPLETE, STATE_CHANGE, CELL_FLIPPED, TURN_COMPLETE, FINAL_TURN_COMPLETE = range(6)
 PAUSED, EXECUTING, QUITTING = range(3)
