@@ -120,6 +120,7 @@ struct PersistArgs {
     unsigned *error;          // set on a spin timeout
     long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
     unsigned long long *trace; // nullable diagnostics (golhip_persist_trace)
+    int fault;                // tests: workgroup 0 never reports progress (its neighbours time out)
 };
 int persist_waves_for(int depth, int wpl);
 int persist_blocks_per_cu(int depth, int wpl, int nw);

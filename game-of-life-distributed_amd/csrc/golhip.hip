@@ -141,7 +141,8 @@ struct golhip {
     int lds_wg_cu = 1;              // option "lds_wg_cu": K1r bands (workgroups) per CU (1 or 2)
     int lds_stride = 1;             // option "lds_stride": K1r LDS rows at a compile-time stride where instantiated
     int lds_split = 0;              // option "lds_split": K1r super-steps compute and publish their edge rows first
-    int lds_fault = 0;              // option "lds_fault" (tests): K1r band 0 never publishes its edges
+    int resident_fault = 0;         // option "resident_fault" (tests): K1r band 0 / K1p workgroup 0 never report
+                                    // (their neighbours' bounded waits time out: the restore-and-re-run path)
     int lds_pre = 2;                // option "lds_pre": K1r interior-first turns while the halos travel
                                     // (profiles/r4pre: 8192^2 31.4 -> 33.9 TCUPS at 2; 1: 33.2, 3: 33.1, 4: 32.3)
     uint32_t *lds_edge = nullptr;   // K1r edge rows (golk::lds_band_edge_words)
@@ -1017,6 +1018,7 @@ bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int w
     p.progress = h->d_sync + 1;
     p.timeout_ticks = h->persist_timeout_ticks;
     p.trace = h->d_trace;
+    p.fault = h->resident_fault;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (e == hipSuccess && (h->flags & GOLHIP_FLAG_TIMING)) {
         e0 = take_event(h);
@@ -1121,7 +1123,7 @@ bool lds_fits(golhip_t h, int wpl, golk::LdsBandArgs *out) {
         out->nt = nt;
         out->stride = stride;
         out->split = h->lds_split;
-        out->fault = h->lds_fault;
+        out->fault = h->resident_fault;
         out->pre = h->lds_pre;
     }
     return true;
@@ -1867,9 +1869,9 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         h->lds_pre = (int)value;
         return GOLHIP_OK;
     }
-    if (!strcmp(key, "lds_fault")) {
-        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "lds_fault %lld", (long long)value);
-        h->lds_fault = (int)value;
+    if (!strcmp(key, "resident_fault")) {
+        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "resident_fault %lld", (long long)value);
+        h->resident_fault = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "lds_split")) {

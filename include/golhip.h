@@ -165,9 +165,9 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * full super-steps compute and publish their edge rows before the interior
  * (measured slower); "lds_pre" (2): a full super-step's
  * first turns run on the rows that need no halo while the halos travel;
- * "lds_fault" (0, tests): band 0 never
- * publishes its edges, so its neighbours' bounded waits time out and the step
- * is restored and re-run;
+ * "resident_fault" (0, tests): the resident kernels' band / workgroup 0 never
+ * reports, so its neighbours' bounded waits time out and the step is restored
+ * and re-run;
  * "persist_depth" (default 0 = tb_depth): turns per super-step;
  * "persist_half" (default 1): a remainder of half a super-step runs as the
  * resident kernel's last, half-depth super-step;

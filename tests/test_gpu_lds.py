@@ -174,7 +174,7 @@ def test_lds_band_tiny_boards(coracle, W, H):
 
 @pytest.mark.parametrize("split", [0, 1])
 def test_lds_band_wait_timeout(coracle, split):
-    """Band 0 never publishes its edges (test hook lds_fault): its neighbours'
+    """Band 0 never publishes its edges (test hook resident_fault): its neighbours'
     flag waits reach the bound, every workgroup drains, and the step is
     restored and re-run on the per-launch kernels, exactly."""
     board = coracle.fill_random(2048, 1024, 0x5EED004A)
@@ -182,7 +182,7 @@ def test_lds_band_wait_timeout(coracle, split):
     with golhip.Board(2048, 1024) as b:
         b.set_option("persistent", 1)
         b.set_option("lds_split", split)
-        b.set_option("lds_fault", 1)
+        b.set_option("resident_fault", 1)
         b.set_option("lds_depth", 8)
         b.set_option("persist_timeout_us", 2000)
         b.load_bytes(board)
@@ -243,7 +243,7 @@ def test_lds_band_interior_first_timeout(coracle):
     with golhip.Board(2048, 1024) as b:
         b.set_option("persistent", 1)
         b.set_option("lds_pre", 2)
-        b.set_option("lds_fault", 1)
+        b.set_option("resident_fault", 1)
         b.set_option("lds_depth", 8)
         b.set_option("persist_timeout_us", 2000)
         b.load_bytes(board)
