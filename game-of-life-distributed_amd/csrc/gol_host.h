@@ -132,7 +132,12 @@ class Chan {
             i += k;
             sent_ += k;
             sent_a_.store(sent_, std::memory_order_release);
-            if (recv_sleepers_) recv_cv_.notify_one();
+            // k values queued: wake every sleeping receiver when more than one
+            // can take something (Go channels allow several consumers)
+            if (recv_sleepers_) {
+                if (k > 1) recv_cv_.notify_all();
+                else recv_cv_.notify_one();
+            }
         }
         return true;
     }
@@ -183,7 +188,10 @@ class Chan {
     // Non-blocking receive: 1 = got one, 0 = empty, -1 = closed and drained.
     int try_recv(T &out) {
         if (cap_ == 0) {
-            std::lock_guard<std::mutex> rg(recv_mu_);
+            // a receiver blocked in recv0 holds recv_mu_ for its whole wait: then
+            // the offer (if any) is that receiver's, and this call must not block
+            std::unique_lock<std::mutex> rg(recv_mu_, std::try_to_lock);
+            if (!rg.owns_lock()) return closed_a_.load(std::memory_order_acquire) ? -1 : 0;
             const uint64_t q = box_.seq.load(std::memory_order_acquire);
             if (q & 1) {
                 out = std::move(box_.value);

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "gol_limits.h"
+
 namespace golk {
 
 // Physical board buffers hold `rows + 2*kHalo` rows of Ww uint32 words; local

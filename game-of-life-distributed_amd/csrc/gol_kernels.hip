@@ -1886,7 +1886,7 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
     const int P = Ww / WPL;               // words (wpl 1) or pairs per row
     const int K = max(1, NT / P);        // row runs per column
     const int units = P * K;
-    const int J = (p.turns + D - 1) / D;
+    const int J = (int)(((int64_t)p.turns + D - 1) / D);  // turns <= kResidentMaxTurns (gol_limits.h)
     const int eq4 = D * q4;               // 16-B granules of one edge side
     // diagnostics (option "trace"): s_memrealtime ticks summed over the
     // workgroups in compute, publish, neighbour wait and halo load

@@ -1062,6 +1062,7 @@ int persist_depth_for(golhip_t h, int wpl) {
 // if there is no room for the copy: then no resident launch this step.
 bool take_guard(golhip_t h, int *rc) {
     *rc = GOLHIP_OK;
+    if (h->guarded) return true;  // a step of several resident launches keeps its first copy
     const size_t bytes = (size_t)h->local_words() * 4;
     if (!h->backup && hipMalloc(&h->backup, bytes) != hipSuccess) {
         h->backup = nullptr;
@@ -1133,7 +1134,8 @@ bool lds_fits(golhip_t h, int wpl, golk::LdsBandArgs *out) {
 // K1p); returns the turns run (0 if K1r does not apply).
 int64_t try_lds(golhip_t h, int64_t left, bool count_last, int *rc) {
     *rc = GOLHIP_OK;
-    if (left < 2 || left > INT32_MAX || !(h->il == 0 || h->il == 2)) return 0;
+    if (left < 2 || !(h->il == 0 || h->il == 2)) return 0;
+    const int64_t run = golk::resident_turns(left);  // 32-bit super-step arithmetic in the kernel
     const int wpl = h->il == 2 ? 2 : 1;
     golk::LdsBandArgs p{};
     if (!lds_fits(h, wpl, &p)) return 0;
@@ -1160,7 +1162,7 @@ int64_t try_lds(golhip_t h, int64_t left, bool count_last, int *rc) {
         *h->h_err = 0;
     }
     if (!take_guard(h, rc)) return 0;
-    const bool count = count_last;
+    const bool count = count_last && run == left;
     hipError_t e = count ? hipMemsetAsync(h->d_scalars, 0, sizeof(unsigned long long), h->stream) : hipSuccess;
     if (e == hipSuccess) e = hipMemsetAsync(h->d_sync, 0, (size_t)(p.nb + 1) * sizeof(unsigned), h->stream);
     p.src = h->cur_rows();
@@ -1170,7 +1172,7 @@ int64_t try_lds(golhip_t h, int64_t left, bool count_last, int *rc) {
     p.progress = h->d_sync + 1;
     p.alive = count ? h->d_scalars : nullptr;
     p.timeout_ticks = h->persist_timeout_ticks;
-    p.turns = (int)left;
+    p.turns = (int)run;
     p.trace = h->d_trace;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (e == hipSuccess && (h->flags & GOLHIP_FLAG_TIMING)) {
@@ -1192,12 +1194,12 @@ int64_t try_lds(golhip_t h, int64_t left, bool count_last, int *rc) {
     h->halo_ready = 0;
     h->cur ^= 1;
     h->last_variant = 4;
-    h->turns += left;
-    h->persist_turns += left;
+    h->turns += run;
+    h->persist_turns += run;
     h->persist_launches++;
     h->lds_launches++;
     if (count) h->alive_turn = h->turns;
-    return left;
+    return run;
 }
 
 // Torus: J super-steps of `depth` turns in one resident launch; returns the
@@ -1210,7 +1212,7 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     const int wpl = wpl_for(h);
     const int depth = persist_depth_for(h, wpl);
     if (depth < 4 || golk::persist_blocks_per_cu(depth, wpl, persist_nw_for(h, depth, wpl)) < 1) return 0;
-    int64_t J = left / depth;
+    int64_t J = golk::resident_turns(left) / depth;  // (32-bit super-step counts in the kernel)
     if (J < 2) return 0;
     // a remainder of exactly depth / 2 turns (1000 = 62 x 16 + 8) becomes a
     // last, half-depth super-step
@@ -2031,9 +2033,15 @@ int step_locked(golhip_t h, int64_t nturns, int32_t want_flips) {
     // whole board run as a one-rank RCCL ring
     const bool halo = h->comm && (h->nranks > 1 || h->force_halo);
     if (!halo) {
-        int rc = GOLHIP_OK;
-        left -= try_persist(h, left - tail, tail == 0, &rc);
-        if (rc) return rc;
+        // resident launches while they apply (more than one only past
+        // golk::kResidentMaxTurns turns), then per-launch kernels for the rest
+        for (;;) {
+            int rc = GOLHIP_OK;
+            const int64_t n = try_persist(h, left - tail, tail == 0, &rc);
+            if (rc) return rc;
+            if (n <= 0) break;
+            left -= n;
+        }
     } else if (h->nranks == 1 && persist_on(h) && h->W % 32 == 0 && !h->guarded) {
         int rc = GOLHIP_OK;  // one-rank ring that may run resident launches: guard the step
         take_guard(h, &rc);

@@ -151,8 +151,9 @@ void oracle_fill_random(uint8_t *w, int W, int H, uint64_t seed) {
  *   - the distributor gathers every row's list and scatters 255s into the new
  *     board (:145-155);
  *   - initializeAliveCells compares old and new boards under the lock (:164).
- * The row channel is an atomic row counter here; the flip events are
- * counted, not delivered (events are the caller's cost, not the engine's).
+ * The row channel is an atomic row counter here.  oracle_run_workerpool counts
+ * the flip events ("engine only"); gol_port_events.cpp delivers every event
+ * through the host mirror's channel, as gol.Run does ("with events").
  * -------------------------------------------------------------------------*/
 typedef struct { int32_t x, y; } cell_t;
 
@@ -188,34 +189,42 @@ static void *pool_worker(void *arg) {
     return NULL;
 }
 
+/* One turn of the worker pool (:118-173 without the event sends): returns the
+ * freshly allocated next world (:139-142); the caller frees `world`. */
+uint8_t *oracle_pool_turn(const uint8_t *world, int W, int H, int threads, pthread_t *tid) {
+    size_t n = (size_t)W * H;
+    int nworkers = threads + 1;
+    pool_t p;
+    p.world = world; p.W = W; p.H = H;
+    atomic_init(&p.next_row, 0);
+    p.row_cells = (cell_t **)calloc((size_t)H, sizeof(cell_t *));
+    p.row_len = (int *)calloc((size_t)H, sizeof(int));
+    for (int i = 0; i < nworkers; i++) pthread_create(&tid[i], NULL, pool_worker, &p);
+    uint8_t *nw = (uint8_t *)calloc(n, 1);                       /* :139-142 */
+    for (int i = 0; i < nworkers; i++) pthread_join(tid[i], NULL);
+    for (int r = 0; r < H; r++) {                                /* gather + scatter :145-155 */
+        for (int k = 0; k < p.row_len[r]; k++)
+            nw[(size_t)p.row_cells[r][k].x * W + p.row_cells[r][k].y] = ALIVE;
+        free(p.row_cells[r]);
+    }
+    free(p.row_cells);
+    free(p.row_len);
+    return nw;
+}
+
 /* Runs `turns` turns in place with the worker-pool structure; returns the total
  * number of CellFlipped events the reference would have sent (or -1). */
 int64_t oracle_run_workerpool(uint8_t *board, int W, int H, long turns, int threads) {
     size_t n = (size_t)W * H;
-    int nworkers = threads + 1;
-    pthread_t *tid = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nworkers);
+    pthread_t *tid = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)(threads + 1));
     int64_t flips = 0;
     uint8_t *world = (uint8_t *)malloc(n);
     memcpy(world, board, n);
     for (long t = 0; t < turns; t++) {
-        pool_t p;
-        p.world = world; p.W = W; p.H = H;
-        atomic_init(&p.next_row, 0);
-        p.row_cells = (cell_t **)calloc((size_t)H, sizeof(cell_t *));
-        p.row_len = (int *)calloc((size_t)H, sizeof(int));
-        for (int i = 0; i < nworkers; i++) pthread_create(&tid[i], NULL, pool_worker, &p);
-        uint8_t *nw = (uint8_t *)calloc(n, 1);                       /* :139-142 */
-        for (int i = 0; i < nworkers; i++) pthread_join(tid[i], NULL);
-        for (int r = 0; r < H; r++) {                                /* gather + scatter :145-155 */
-            for (int k = 0; k < p.row_len[r]; k++)
-                nw[(size_t)p.row_cells[r][k].x * W + p.row_cells[r][k].y] = ALIVE;
-            free(p.row_cells[r]);
-        }
+        uint8_t *nw = oracle_pool_turn(world, W, H, threads, tid);
         for (size_t i = 0; i < n; i++) flips += nw[i] != world[i];   /* initializeAliveCells :212-220 */
         free(world);
         world = nw;
-        free(p.row_cells);
-        free(p.row_len);
     }
     memcpy(board, world, n);
     free(world);

@@ -161,6 +161,9 @@ class COracle:
         lib.oracle_run_workerpool.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int]
         lib.oracle_run_workerpool.restype = ctypes.c_int64
         u64p = ctypes.POINTER(ctypes.c_uint64)
+        lib.oracle_run_workerpool_events.argtypes = [u8p, ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int,
+                                                     ctypes.c_int, u64p, i64p, i64p, ctypes.c_char_p]
+        lib.oracle_run_workerpool_events.restype = ctypes.c_int
         lib.fastcpu_pack.argtypes = [u8p, ctypes.c_int, ctypes.c_int, u64p]
         lib.fastcpu_unpack.argtypes = [u64p, ctypes.c_int, ctypes.c_int, u8p]
         lib.fastcpu_run.argtypes = [u64p, ctypes.c_int, ctypes.c_int, ctypes.c_long, ctypes.c_int]
@@ -234,6 +237,25 @@ class COracle:
             raise MemoryError("oracle_run_workerpool")
         return b, flips
 
+    EVENT_NAMES = ["AliveCellsCount", "ImageOutputComplete", "StateChange", "CellFlipped", "TurnComplete",
+                   "FinalTurnComplete"]
+
+    def run_workerpool_events(self, board: np.ndarray, turns: int, threads: int, events_cap: int = 0,
+                              out_pgm: str | None = None):
+        """The port as gol.Run runs it, every event through a channel of
+        capacity `events_cap` drained by main.go's loop
+        (gol_port_events.cpp).  Returns (board, counts by event name, last
+        TurnComplete, len(FinalTurnComplete.Alive))."""
+        b = np.ascontiguousarray(board, dtype=np.uint8).copy()
+        H, W = b.shape
+        counts = np.zeros(6, dtype=np.uint64)
+        last, fin = ctypes.c_int64(), ctypes.c_int64()
+        rc = self.lib.oracle_run_workerpool_events(self._p(b), W, H, turns, threads, events_cap,
+                                                   self._p(counts, ctypes.c_uint64), ctypes.byref(last),
+                                                   ctypes.byref(fin), out_pgm.encode() if out_pgm else None)
+        if rc != 0:
+            raise RuntimeError("oracle_run_workerpool_events failed")
+        return b, {self.EVENT_NAMES[k]: int(counts[k]) for k in range(6)}, last.value, fin.value
 
     # -- bit-packed OpenMP comparator (gol_fastcpu.c), W % 64 == 0
     def pack64(self, board: np.ndarray) -> np.ndarray:

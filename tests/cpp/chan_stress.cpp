@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <thread>
 #include <algorithm>
+#include <atomic>
 #include <vector>
 
 #include "gol_host.h"
@@ -87,6 +88,56 @@ int main() {
     if (ms < 40) {
         std::printf("FAIL unbuffered send returned after %.1f ms, before the receiver\n", ms);
         rc = 1;
+    }
+    // try_recv never blocks, even beside a receiver blocked in recv on an
+    // unbuffered channel (golrun_next_event's timeout and golrun_wait rely on it)
+    {
+        gol::Chan<int> c0(0);
+        std::atomic<int> got{0};
+        std::thread blocked([&] {
+            int v;
+            if (c0.recv(v)) got++;
+        });
+        std::this_thread::sleep_for(std::chrono::milliseconds(20));  // past the spin: asleep in recv0
+        const auto t1 = std::chrono::steady_clock::now();
+        int v, tries = 0;
+        for (; tries < 1000; ++tries)
+            if (c0.try_recv(v) == 1) got++;
+        const double tms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+        std::thread s2([&] { c0.send(1); c0.send(2); });
+        while (got.load() < 2) {
+            if (c0.try_recv(v) == 1) got++;
+            std::this_thread::yield();
+        }
+        s2.join();
+        blocked.join();
+        if (tms > 500) {
+            std::printf("FAIL 1000 try_recv beside a blocked recv took %.1f ms\n", tms);
+            rc = 1;
+        }
+    }
+    // send_batch of k > 1 values wakes every sleeping receiver that can take one
+    {
+        gol::Chan<int> cb(8);
+        std::atomic<int> got{0};
+        std::vector<std::thread> rs;
+        for (int i = 0; i < 2; ++i)
+            rs.emplace_back([&] {
+                int v;
+                if (cb.recv(v)) got++;
+            });
+        std::this_thread::sleep_for(std::chrono::milliseconds(20));  // both asleep on the condition variable
+        int two[2] = {1, 2};
+        cb.send_batch(two, 2);
+        const auto t2 = std::chrono::steady_clock::now();
+        while (got.load() < 2 && std::chrono::steady_clock::now() - t2 < std::chrono::seconds(1))
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        if (got.load() < 2) {
+            std::printf("FAIL a batch of 2 woke %d of 2 sleeping receivers\n", got.load());
+            rc = 1;
+            cb.close();
+        }
+        for (auto &t : rs) t.join();
     }
     std::printf(rc ? "chan stress FAILED\n" : "chan stress ok\n");
     return rc;

@@ -138,3 +138,43 @@ def test_wrong_result_macro_is_a_compile_error(tmp_path):
     p = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-fsyntax-only",
                         "-DGOL_SPLIT_NOHOOK=1", src], capture_output=True, text=True, timeout=300)
     assert p.returncode != 0 and "GOL_SPLIT_NOHOOK" in p.stderr
+
+
+def test_resident_turn_bound(tmp_path):
+    """K1r's / K1p's super-step arithmetic is 32-bit.  A step of
+    more than golk::kResidentMaxTurns turns runs as several resident launches
+    of at most that many (golhip.hip step_locked), and at that bound
+    J = ceil(turns / D), j * D and turns - j * D fit an int for every depth
+    the kernels take (1..64): checked here with g++ on csrc/gol_limits.h."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = tmp_path / "bound.cpp"
+    src.write_text(r'''
+#include <climits>
+#include <cstdio>
+#include <initializer_list>
+#include "gol_limits.h"
+int main() {
+    using namespace golk;
+    for (long long left : {2ll, 1000ll, (long long)INT_MAX, (long long)INT_MAX + 1, 10000000000ll, LLONG_MAX / 2}) {
+        const long long run = resident_turns(left);
+        if (run < 1 || run > left || run > kResidentMaxTurns) return 1;
+        if (left <= kResidentMaxTurns && run != left) return 2;
+        for (int D = 1; D <= kResidentMaxDepth; ++D) {
+            const long long J = (run + D - 1) / D;  // the kernel's int J, int j * D
+            if (J > INT_MAX || (J - 1) * D > INT_MAX || (long long)run + D - 1 > INT_MAX) return 3;
+        }
+    }
+    // 10^10 turns (main.go:37-41's default) in launches of the bound: 10 launches, none wraps
+    long long left = 10000000000ll, n = 0;
+    while (left > 0) { left -= resident_turns(left); ++n; }
+    if (n != 10) return 4;
+    std::puts("ok");
+    return 0;
+}
+''')
+    exe = tmp_path / "bound"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-I", os.path.join(root, "game-of-life-distributed_amd", "csrc"),
+                    str(src), "-o", str(exe)], check=True, timeout=120)
+    assert subprocess.run([str(exe)], capture_output=True, text=True, timeout=60).stdout.strip() == "ok"

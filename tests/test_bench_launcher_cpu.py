@@ -95,3 +95,144 @@ def test_watchdog_ends_a_hung_stage_with_a_json_line():
     assert p.returncode == 3
     (line,) = _json_lines(p.stdout)
     assert line["stage"] == "golhip_comm_init" and line["value"] is None and "watchdog" in line["error"]
+
+
+# ---------------------------------------------------------------- configs[3] block
+FULLSIZE = json.load(open(os.path.join(ROOT, "tests", "golden", "fullsize.json")))
+
+
+class _FakeBoard:
+    """Stands in for golhip.Board: turns advance, the digest / alive count are
+    the fixture's at the checkpoint (rank 0's share; the others add 0), or a
+    wrong digest for the configs named in `bad`."""
+
+    def __init__(self, W, H, row0, rows, rank, bad):
+        self.W, self.rows, self.rank, self.bad = W, rows, rank, bad
+        self.key = {65536: "c2", 262144: "c3"}[W]
+        self.turn = 0
+        self.closed = False
+
+    def set_tb_depth(self, d): pass
+    def set_rows_per_wave(self, r): pass
+    def set_option(self, k, v): pass
+    def comm_init(self, uid, n, r): self.comm = (n, r)
+    def comm_info(self): return {"nranks": self.comm[0], "rank": self.comm[1], "ring_rows": self.rows}
+    def fill_random(self, seed): self.turn = 0
+    def step(self, n): self.turn += n
+    def sync(self): pass
+    def stream(self): return 0
+    def perf_reset(self): pass
+    def close(self): self.closed = True
+
+    def _cp(self):
+        return FULLSIZE[self.key]["checkpoints"].get(str(self.turn))
+
+    def board_hash(self):
+        cp = self._cp()
+        if self.rank or cp is None:
+            return 0
+        return int(cp["hash"], 16) ^ (1 if self.key in self.bad else 0)
+
+    def alive_count(self, global_sum=False):
+        cp = self._cp()
+        return (cp["alive"] if cp and self.rank == 0 else 0), self.turn
+
+    def perf(self):
+        wpl = 4 if self.W == 262144 else 2
+        return {"persist_turns": 0, "step_turns": 100, "step_launches": 10, "skew_launches": 10,
+                "split_launches": 0, "tb_depth": 9 if wpl == 4 else 20, "words_per_lane": wpl,
+                "persist_launches": 0, "persist_depth": 0, "rows_per_wave": 0, "halo_bytes": 0,
+                "halo_exchanges": 0}
+
+
+def _fake_env(world=1, bad=()):
+    boards = []
+
+    class FakeEnv:
+        def __init__(self, a, world_, rank, local):
+            self.a, self.world, self.rank, self.local, self.dist = a, world, 0, 0, None
+
+        def stage(self, name): pass
+
+        def board(self, W, H, row0, rows):
+            b = _FakeBoard(W, H, row0, rows, self.rank, bad)
+            boards.append(b)
+            return b
+
+        def unique_id(self): return b"x"
+        def barrier(self, board): pass
+        def gsum(self, x): return x % (1 << 64)
+        def gmax(self, x): return x
+        def bcast(self, x): return x
+
+        def gather(self, obj):  # every rank's row, as rank r would report it
+            return [dict(obj, rank=r, row0=r * obj["rows"]) for r in range(self.world)]
+
+        def region_timer(self, board):
+            class T:
+                def start(self): pass
+                def stop(self): return 1.0
+            return T()
+
+        def close(self): pass
+
+    return FakeEnv, boards
+
+
+def _run_main(monkeypatch, capsys, argv, env):
+    monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
+    code = 0
+    try:
+        bench.main(env_factory=env)
+    except SystemExit as e:
+        code = e.code
+    return code, _json_lines(capsys.readouterr().out)
+
+
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_default_line_carries_a_configs3_block(monkeypatch, capsys, world):
+    env, boards = _fake_env(world)
+    if world > 1:
+        monkeypatch.setenv("WORLD_SIZE", str(world))
+        monkeypatch.setenv("RANK", "0")
+    code, (line,) = _run_main(monkeypatch, capsys, ["--gpus", str(world), "--steps", "3", "--no-cpu-baseline",
+                                                    "--warmup-seconds", "0", "--configs3-warmup-seconds", "0"], env)
+    assert code == 0 and line["parity"] is True
+    assert line["config"]["board"] == [65536, 65536] and line["value"] > 0  # the primary value stays configs[2]
+    c3 = line["configs3"]
+    assert c3["config"]["board"] == [262144, 262144] and c3["config"]["turns_per_step"] == 100
+    assert c3["config"]["rows_per_rank"] == 262144 // world and c3["n_gpus"] == world and c3["steps"] == 3
+    assert c3["parity"] is True and c3["parity_check"]["fixture"] == "tests/golden/fullsize.json c3 turn 100"
+    assert c3["parity_check"]["alive"] == FULLSIZE["c3"]["checkpoints"]["100"]["alive"]
+    assert c3["value"] > 0 and c3["unit"] == "GCUPS" and c3["scaling"] == "strong"
+    assert c3["roofline"]["frac"] > 0 and c3["config"]["words_per_lane"] == 4
+    if world > 1:
+        assert [r["rank"] for r in c3["config"]["ranks"]] == list(range(world))
+        assert {r["rows"] for r in c3["config"]["ranks"]} == {262144 // world}
+    assert [b.W for b in boards] == [65536, 262144] and all(b.closed for b in boards)  # one board at a time
+
+
+def test_configs3_parity_failure_fails_the_line(monkeypatch, capsys):
+    env, _ = _fake_env(1, bad=("c3",))
+    code, (line,) = _run_main(monkeypatch, capsys, ["--steps", "1", "--no-cpu-baseline", "--warmup-seconds", "0",
+                                                    "--configs3-warmup-seconds", "0"], env)
+    assert code == 1 and line["parity"] is False and line["configs3"]["parity"] is False
+    assert line["parity_check"]["ok"] is True  # configs[2] itself was right
+
+
+def test_no_configs3_flag_and_other_workloads_skip_the_block(monkeypatch, capsys):
+    env, boards = _fake_env(1)
+    code, (line,) = _run_main(monkeypatch, capsys, ["--steps", "1", "--no-cpu-baseline", "--warmup-seconds", "0",
+                                                    "--no-configs3"], env)
+    assert code == 0 and "configs3" not in line and [b.W for b in boards] == [65536]
+
+
+def test_cpu_share_is_measured():
+    s = bench.cpu_share()
+    assert s["affinity"] == len(os.sched_getaffinity(0)) and 1 <= s["threads"] <= s["affinity"]
+    assert s["gomaxprocs_equiv"] == s["threads"]
+
+
+def test_count_gpus_honours_visible_devices(monkeypatch):
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert bench.count_gpus()[0] == 0

@@ -145,6 +145,43 @@ def test_config3_262144_100_turns(full, opts):  # default: skewed band stacks
     run_checkpoints(full, "c3", **opts)
 
 
+@pytest.mark.parametrize("nstrips", [8, 2])
+def test_config3_strips_in_process(full, nstrips):
+    """configs[3] as the row strips of its 8- and 2-GPU strong-scaling plan
+    (distributor.go:116-173's turn loop over a partitioned board; the README's
+    halo extension): 262144^2 in `nstrips` strips of 262144 / nstrips rows,
+    100 turns with deep halos moved by device copies, the strips' digests and
+    alive counts summed against the c3 fixture, the fixture's sample rows
+    compared bit for bit.  Every strip must have run the plan a ring share
+    of that size runs: K1w (skewed band stacks) on four words per lane, on
+    its extended rows."""
+    js, rows = full
+    rec = js["c3"]
+    N = rec["width"]
+    bounds = [N * i // nstrips for i in range(nstrips + 1)]
+    strips = [golhip.Board(N, N, row0=bounds[i], rows=bounds[i + 1] - bounds[i]) for i in range(nstrips)]
+    try:
+        for s in strips:
+            s.fill_random(rec["seed"])
+        golhip.group_step(strips, 100)
+        cp = rec["checkpoints"]["100"]
+        digest = sum(s.board_hash() for s in strips) % (1 << 64)
+        assert f"{digest:016x}" == cp["hash"]
+        assert sum(s.alive_count()[0] for s in strips) == cp["alive"]
+        assert rec["sample_turn"] == 100
+        for i, r in enumerate(rec["sample_rows"]):
+            k = max(j for j in range(nstrips) if bounds[j] <= r)
+            assert np.array_equal(strips[k].snapshot_rows(r - bounds[k], 1)[0], rows["c3_rows"][i]), ("row", r)
+        for s in strips:
+            p = s.perf()
+            assert p["words_per_lane"] == 4, p
+            assert p["step_launches"] > 0 and p["skew_launches"] == p["step_launches"], p
+            assert p["step_turns"] == 100 and p["halo_bytes"] > 0, p
+    finally:
+        for s in strips:
+            s.close()
+
+
 # ---------------------------------------------------------------- configs[4]
 def test_config4_5120_event_stream_batched(full):
     """configs[4]: the initial CellFlipped list (alive cells at load,
