@@ -36,10 +36,19 @@
               DPP(40,56) DPP(41,57) DPP(42,58) DPP(43,59) DPP(44,60) DPP(45,61) DPP(46,62) DPP(47,63)
 #define V_ALB ALB(40,48,49) ALB(41,49,50) ALB(42,50,51) ALB(43,51,52) ALB(44,52,53) ALB(45,53,54) ALB(46,54,55) ALB(47,55,56) \
               ALB(40,56,57) ALB(41,57,58) ALB(42,58,59) ALB(43,59,60) ALB(44,60,61) ALB(45,61,62) ALB(46,62,63) ALB(47,63,48)
-// the step kernel's ratio, 9 bitop3 : 1 dpp : 1 alignbit (16 = 12 + 2 + 2), independent
+// 12 bitop3 : 2 dpp : 2 alignbit = 6 : 1 : 1 (16 instructions; named "mix9:1:1" before round 5, which it is not)
 #define V_MIX B3(40,48,49,50) B3(41,49,50,51) B3(42,50,51,52) DPP(43,60) B3(44,52,53,54) B3(45,53,54,55) ALB(46,61,62) B3(47,55,56,57) \
               B3(40,56,57,58) B3(41,57,58,59) DPP(42,63) B3(43,59,60,61) B3(44,60,61,62) ALB(45,61,48) B3(46,62,63,48) B3(47,63,48,49)
 
+// the step kernels' ratio per word-turn at two words per lane, 9 bitop3 : 1 dpp : 1 alignbit
+// (22 = 18 + 2 + 2), independent, the shifts spread over the block
+#define V_MIX911 B3(40,48,49,50) B3(41,49,50,51) B3(42,50,51,52) B3(43,51,52,53) DPP(44,60) B3(45,53,54,55) B3(46,54,55,56) \
+                 B3(47,55,56,57) B3(40,56,57,58) B3(41,57,58,59) ALB(42,61,62) B3(43,59,60,61) B3(44,60,61,62) B3(45,61,62,63) \
+                 B3(46,62,63,48) DPP(47,63) B3(40,48,49,50) B3(41,49,50,51) B3(42,50,51,52) ALB(43,62,48) B3(44,52,53,54) B3(45,53,54,55)
+// 10 : 1 : 1 per word at four words per lane (quads: 1/2 DPP + 1/2 alignbit per word): 20 + 1 + 1 = 22
+#define V_MIX10 B3(40,48,49,50) B3(41,49,50,51) B3(42,50,51,52) B3(43,51,52,53) B3(44,52,53,54) DPP(45,60) B3(46,54,55,56) \
+                B3(47,55,56,57) B3(40,56,57,58) B3(41,57,58,59) B3(42,58,59,60) B3(43,59,60,61) B3(44,60,61,62) B3(45,61,62,63) \
+                B3(46,62,63,48) B3(47,63,48,49) ALB(40,61,62) B3(41,49,50,51) B3(42,50,51,52) B3(43,51,52,53) B3(44,52,53,54) B3(46,53,54,55)
 // 15 bitop3 + 1 dpp / 1 alignbit; 12 + 4 spread; 12 + 4 grouped
 #define V_D1 B3(40,48,49,50) B3(41,49,50,51) B3(42,50,51,52) B3(43,51,52,53) B3(44,52,53,54) B3(45,53,54,55) B3(46,54,55,56) DPP(47,60) \
              B3(40,56,57,58) B3(41,57,58,59) B3(42,58,59,60) B3(43,59,60,61) B3(44,60,61,62) B3(45,61,62,63) B3(46,62,63,48) B3(47,63,48,49)
@@ -79,6 +88,8 @@ KERNEL(k_chain4, V_CHAIN4)
 KERNEL(k_dpp, V_DPP)
 KERNEL(k_alb, V_ALB)
 KERNEL(k_mix, V_MIX)
+KERNEL(k_mix911, V_MIX911)
+KERNEL(k_mix10, V_MIX10)
 KERNEL(k_d1, V_D1)
 KERNEL(k_a1, V_A1)
 KERNEL(k_d4s, V_D4S)
@@ -130,7 +141,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&sink, 16 * cus));
     long long* hs = (long long*)malloc(16 * cus);
     struct { const char* n; kfn f; int len; } ks[] = {{"indep", k_indep, k_indep_n}, {"bank3", k_bank3, k_bank3_n}, {"bank2", k_bank2, k_bank2_n},
-        {"chain1", k_chain1, k_chain1_n}, {"chain2", k_chain2, k_chain2_n}, {"chain4", k_chain4, k_chain4_n}, {"dpp", k_dpp, k_dpp_n}, {"alignbit", k_alb, k_alb_n}, {"mix9:1:1", k_mix, k_mix_n},
+        {"chain1", k_chain1, k_chain1_n}, {"chain2", k_chain2, k_chain2_n}, {"chain4", k_chain4, k_chain4_n}, {"dpp", k_dpp, k_dpp_n}, {"alignbit", k_alb, k_alb_n}, {"mix6:1:1", k_mix, k_mix_n}, {"mix9:1:1", k_mix911, k_mix911_n}, {"mix10:1:1", k_mix10, k_mix10_n},
         {"b3x15+dpp", k_d1, k_d1_n}, {"b3x15+alb", k_a1, k_a1_n}, {"b3x12+dpp4spread", k_d4s, k_d4s_n}, {"b3x12+alb4spread", k_a4s, k_a4s_n}, {"b3x12+dpp4grouped", k_d4g, k_d4g_n},
         {"b3x12+alb4grouped", k_a4g, k_a4g_n}, {"xor_vop2", k_xor, k_xor_n}, {"real_HHHVVH", k_real_HHHVVH, k_real_HHHVVH_n}, {"real_spread", k_real_spread, k_real_spread_n}, {"HH_pairs", k_HH_pairs, k_HH_pairs_n}, {"HV_alt", k_HV_alt, k_HV_alt_n}, {"HVV", k_HVV, k_HVV_n}, {"HVVV", k_HVVV, k_HVVV_n}, {"bperm_alb", k_bperm_alb, k_bperm_alb_n}, {"bperm2_alb2", k_bperm2_alb2, k_bperm2_alb2_n}, {"dpp_alb", k_dpp_alb, k_dpp_alb_n}, {"dpp2_alb2", k_dpp2_alb2, k_dpp2_alb2_n}, {"xor_e64", k_xor_e64, k_xor_e64_n}, {"xor3", k_xor3, k_xor3_n}};
     hipEvent_t e0, e1;
@@ -152,9 +163,13 @@ int main(int argc, char** argv) {
             double cyc = 0, wall = 0;
             for (int b = 0; b < cus; ++b) cyc += hs[2 * b], wall += hs[2 * b + 1];
             const double ghz = cyc / (wall / 100e6) / 1e9;  // shader clock over the 100 MHz counter
-            const double per_cycle = double(wps) * iters * 16 * k.len / (cyc / cus);  // per SIMD, per measured cycle
-            printf("{\"variant\": \"%s\", \"waves_per_simd\": %d, \"ms\": %.3f, \"winst_per_simd_cycle_2p4\": %.4f, "
-                   "\"clock_ghz\": %.3f, \"winst_per_simd_cycle\": %.4f}\n", k.n, wps, ms, per_simd_cycle, ghz, per_cycle);
+            // per SIMD and per cycle of the clock the CUs ran at: the measured
+            // clock x the event-timed wall time (round 5; before, the in-kernel
+            // cycle sum of lane 0 alone, which under-counted: values > 0.5)
+            const double per_cycle = winst / (ms * 1e-3) / (cus * 4.0 * ghz * 1e9);
+            printf("{\"variant\": \"%s\", \"len\": %d, \"waves_per_simd\": %d, \"ms\": %.3f, "
+                   "\"winst_per_simd_cycle_2p4\": %.4f, \"clock_ghz\": %.3f, \"winst_per_simd_cycle\": %.4f}\n",
+                   k.n, k.len, wps, ms, per_simd_cycle, ghz, per_cycle);
         }
     }
     return 0;
