@@ -283,11 +283,9 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str, 
             perf["persist_turns"]
         depth = perf["persist_depth"]
     else:
-        # split tiling: a step launch is kernel A + kernel B; named after the
-        # family that ran most of the step launches (262144^2 x 100 turns =
-        # 11 split launches of 8 turns + 2 paired-band launches of 6)
+        # named after the family that ran most of the step launches
         kname = ("gol_skew_kernel" if 2 * perf.get("skew_launches", 0) > perf["step_launches"] else
-                 "gol_split" if 2 * perf.get("split_launches", 0) > perf["step_launches"] else "gol_tb_pair_kernel")
+                 "gol_tb_pair_kernel")
         launches, kms, kturns = perf["step_launches"], region_ms, perf["step_turns"]
         depth = perf["tb_depth"]
     launches = max(1, launches)
@@ -306,12 +304,10 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str, 
         "unit": "Gslot/s (wave64 VALU issue slots)",
         "frac": round(achieved / VALU_PEAK_GSLOTS, 4) if achieved else None,
         "traffic": None,
-        "kernel": (f"gol_split_pair_kernel<{depth}, {wpl}> + gol_split_tri_kernel<{depth}, {wpl}>"
-                   if kname == "gol_split" else f"{kname}<{depth}, {wpl}>"),
+        "kernel": f"{kname}<{depth}, {wpl}>",
         "launch_time": "HIP events on the engine stream around the timed region / launches (boundaries included)",
         "avg_launch_ms": round(avg_s * 1e3, 5),
         "launches": launches,
-        "split_launches": perf.get("split_launches", 0),
         "skew_launches": perf.get("skew_launches", 0),
         "turns_per_launch": tpl,
         "slots_per_word_turn": spw,

@@ -58,25 +58,6 @@ int tb_wave_slots_per_cu(int depth, int wpl, bool paired);  // resident waves pe
 // Rows per wavefront minimising (rounds of waves) x (rows streamed per wave).
 int auto_rows_per_wave(int Ww, int rows, int depth, int wave_slots, bool fill_skip, int wpl, bool paired = false);
 
-// Split tiling (torus, per launch; gol_kernels.hip K1s): kernel A streams
-// regions of input rows from both ends and exports the edge rows of every
-// generation, kernel B computes the triangles between the bands.  Region q is
-// input rows [q H / nreg, (q + 1) H / nreg), each at least 2 P0 rows.
-struct SplitArgs {
-    StepArgs base;   // torus step: src, dst, W, Ww, rows_out = H, dst_base, in, alive
-    int nreg;        // regions
-    int tiles_x;
-    int P0;          // split_prefix_rows(depth)
-    uint32_t *exp;   // split_exp_words() words
-    int *meet;       // 2 * nreg * tiles_x: input rows each wave of a region streamed (U, L)
-};
-bool split_supported(int depth, int wpl);
-int split_prefix_rows(int depth);
-inline int64_t split_exp_words(int nreg, int tiles_x, int depth, int wpl) {
-    return (int64_t)nreg * tiles_x * 4 * (depth - 1) * 3 * 64 * wpl;
-}
-hipError_t launch_split(const SplitArgs &p, int depth, int wpl, hipStream_t s);
-
 // Skewed band stacks (K1w, gol_kernels.hip; torus and row strips, per
 // launch).  Output rows [0, base.rows_out) of the StepArgs frame come from
 // input rows [-D, rows_out + D) through base.in.  The input rows
@@ -152,7 +133,6 @@ struct LdsBandArgs {
     int xcd;               // 1: consecutive bands on one XCD (nb % 8 == 0)
     int nt;                // threads per workgroup: 512 or 1024
     int stride;            // LDS words per row: lds_band_stride (>= Ww)
-    int split;             // 1: full super-steps compute their edge rows first, publish, then the interior
     int fault;             // tests: band 0 never publishes, so its neighbours' waits time out
     int pre;               // > 0: full super-steps run their first `pre` turns on the interior rows
                            //      while the halos travel (lds_pre)
@@ -165,6 +145,46 @@ inline int64_t lds_band_lds_bytes(int hmax, int D, int stride) { return 2ll * (h
 int lds_band_stride(int Ww, int wpl, int nt);
 int lds_band_blocks_per_cu(int wpl, int nt, int stride, int64_t lds_bytes);
 hipError_t launch_lds_band(const LdsBandArgs &p, int wpl, hipStream_t s);
+
+// Resident LDS turn pipeline (K1t, gol_kernels.hip; small tori whose rows are
+// one wavefront wide: Ww == 64 * wpl).  Workgroup b of nb owns a band of
+// h_b rows, skewed: generation t of the band is the rows [r_b + t, r_{b+1} + t)
+// (mod rows), so generation t needs only generation t - 1's rows of the band
+// plus the first two rows of the band below (no trapezoid, no super-steps).
+// Wave w of the kPipeWaves computes the turns w + 1, w + 1 + kPipeWaves, ...:
+// it streams its band's rows top to bottom, reading the previous turn's rows
+// from the previous wave's LDS ring and writing its own into its ring (the
+// last wave's ring feeds the first: the turns circulate).  Each turn's first
+// two rows also go to `edge` for the band above (write-through {word, tag}
+// granules per (band, turn mod kPipeQ)); `econs` returns which turns were read.
+// The last turn's rows go to dst at [r_b + turns, r_{b+1} + turns).
+constexpr int kPipeWaves = 8;   // waves (stages) per workgroup
+constexpr int kPipeQ = 32;      // edge slots per band: turns a band may run ahead of the band above
+constexpr int kPipeK = 8;       // slots of each ring but the last (the last holds the band: kw >= hmax + 4)
+struct PipeArgs {
+    const uint32_t *src;   // generation 0: rows x Ww words
+    uint32_t *dst;         // the last generation (the other buffer)
+    uint32_t *edge;        // pipe_edge_words(nb, Ww): {word, tag} granules, tag = tag_base + turn
+    unsigned *econs;       // nb, zeroed: turns of band b's edges (0, 1, ...) band b - 1 has read
+    unsigned *error;       // zeroed; set on a spin timeout (every wave then drains)
+    unsigned long long *alive;  // nullable: += popcount of the last generation
+    unsigned long long *trace;  // nullable: [0..3] += wave ticks waiting for ring rows, ring room, imports,
+                                // edge room; [4] += wave ticks in the kernel; [8..10] += ticks in the
+                                // steady-state row loop, its rows, ring-row waits among them
+    long long timeout_ticks;    // s_memrealtime ticks (100 MHz) a wait may take
+    int Ww, rows, nb, turns;
+    int hmax;              // ceil(rows / nb)
+    int kw;                // slots of the last wave's ring: a power of two >= hmax + 4
+    int xcd;               // 1: consecutive bands on one XCD (nb % 8 == 0)
+    unsigned tag_base;     // edge tags of this launch are tag_base + turn (> every tag in the buffer)
+};
+__host__ __device__ inline int64_t pipe_edge_words(int nb, int Ww) { return 4ll * nb * kPipeQ * Ww; }
+__host__ __device__ inline int pipe_slots(int kw) { return (kPipeWaves - 1) * kPipeK + kw; }
+// rows, one tag per row slot, CONS[kPipeWaves], 64 dummy words (the lanes
+// other than lane 0 of a signal store write there: no same-address stores)
+inline int64_t pipe_lds_bytes(int Ww, int kw) { return ((int64_t)pipe_slots(kw) * (Ww + 1) + kPipeWaves + 64) * 4; }
+int pipe_blocks_per_cu(int wpl, int64_t lds_bytes);
+hipError_t launch_pipe(const PipeArgs &p, int wpl, hipStream_t s);
 
 hipError_t launch_pack(const uint8_t *bytes, uint32_t *words, int W, int Ww, int rows, hipStream_t s);
 // il: the words are in the interleaved pair layout of the wpl = 2 step kernels

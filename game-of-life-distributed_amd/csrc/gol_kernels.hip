@@ -13,6 +13,7 @@
 // cell (y, x) = bit x%32 of word x/32.  Everything here is integer work bound
 // by HBM or VALU; none of it is matrix-shaped, so there is no MFMA.
 #include "gol_kernels.h"
+#include "gol_bits.h"
 
 #include <algorithm>
 #include <climits>
@@ -35,66 +36,6 @@ __device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<int
 template <int N, typename F>
 __device__ __forceinline__ void static_for(F &&f) {
     static_for_impl(f, std::make_integer_sequence<int, N>());
-}
-
-// ---------------------------------------------------------------------------
-// bit-sliced helpers
-// ---------------------------------------------------------------------------
-template <typename F>
-constexpr unsigned tt3(F f) {
-    unsigned r = 0;
-    for (int i = 0; i < 8; ++i)
-        if (f((i >> 2) & 1, (i >> 1) & 1, i & 1)) r |= 1u << i;
-    return r;
-}
-// v_bitop3_b32 truth tables, operand order (a, b, c) -> index a*4 + b*2 + c.
-constexpr unsigned kXor3 = tt3([](int a, int b, int c) { return (a ^ b ^ c) != 0; });       // 0x96
-constexpr unsigned kMaj = tt3([](int a, int b, int c) { return a + b + c >= 2; });          // 0xE8
-// Column sum of three 2-bit row sums (h0 + 2 h1 each, centre included):
-//   u = sum of the h0 bits = u0 + 2 u1,  v = sum of the h1 bits = v0 + 2 v1,
-//   sum9 = u0 + 2 T with T = u1 + v0 + 2 v1.
-// next = (sum9 == 3) | (centre & sum9 == 4) in three LUTs, found by exhaustive
-// search over 3-gate circuits; it leans on one unreachable input (centre
-// alive with sum9 == 0) and is checked against all 512 neighbourhoods in
-// tests/test_rule_circuit.py:
-//   g1   = [T == 0 or T == 2]
-//   g2   = !v1 & (!centre | u0) | !u0 & !centre
-//   next = u0 ? (!g1 & g2) : (g1 & !g2)
-constexpr unsigned kG1 = tt3([](int u1, int v0, int v1) { int T = u1 + v0 + 2 * v1; return T == 0 || T == 2; });
-constexpr unsigned kG2 = tt3([](int u0, int v1, int c) { return (!v1 && (!c || u0)) || (!u0 && !c); });
-constexpr unsigned kNext = tt3([](int u0, int g1, int g2) { return u0 ? (!g1 && g2) : (g1 && !g2); });
-static_assert(kG1 == 0x43 && kG2 == 0x35 && kNext == 0x24, "rule LUTs");
-static_assert(kXor3 == 0x96 && kMaj == 0xE8, "bitop3 table order");
-
-template <unsigned IMM>
-__device__ __forceinline__ uint32_t bop(uint32_t a, uint32_t b, uint32_t c) {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, IMM);
-}
-// Whole-wavefront lane shifts (DPP wave_shr:1 / wave_shl:1): lane i receives
-// lane i-1 / i+1; bound_ctrl zero-fills the edge lane (no `old` operand, so
-// no extra v_mov).  Edge lanes are the tile halo.
-__device__ __forceinline__ uint32_t from_left_lane(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);
-}
-__device__ __forceinline__ uint32_t from_right_lane(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xF, 0xF, true);
-}
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
-    uint64_t z = x + 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
 }
 
 // ---------------------------------------------------------------------------
@@ -269,19 +210,6 @@ __device__ __forceinline__ void row_sums(const Lanes<WPL> &x, uint32_t (&s0)[WPL
         s0[k] = bop<kXor3>(west[k], x.w[k], east[k]);
         s1[k] = bop<kMaj>(west[k], x.w[k], east[k]);
     }
-}
-
-// The B3/S23 rule from the row sums of the rows above (a), at (b) and below
-// (c) and the centre word: column sums + the 3-LUT rule (kG1, kG2, kNext).
-__device__ __forceinline__ uint32_t rule_word(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1, uint32_t c0,
-                                              uint32_t c1, uint32_t centre) {
-    const uint32_t u0 = bop<kXor3>(a0, b0, c0);
-    const uint32_t u1 = bop<kMaj>(a0, b0, c0);
-    const uint32_t v0 = bop<kXor3>(a1, b1, c1);
-    const uint32_t v1 = bop<kMaj>(a1, b1, c1);
-    const uint32_t g1 = bop<kG1>(u1, v0, v1);
-    const uint32_t g2 = bop<kG2>(u0, v1, centre);
-    return bop<kNext>(u0, g1, g2);
 }
 
 // One stage (turn t) for the row entering with role R (R = input index % 3).
@@ -785,47 +713,19 @@ __global__ __launch_bounds__(512) void gol_tb_pair_kernel(StepArgs a) {
     }
 }
 
-// ---------------------------------------------------------------------------
-// K1s: split tiling (torus, per launch).  The overlapped bands of K1 compute
-// the D-row trapezoid around every band boundary twice (once per side):
-// ~1.25 D^2 extra stage-rows per band, 50 % of the work at 16384^2 (S = 40).
-// K1s splits the launch in two kernels that compute every stage-row once:
-//   A (gol_split_pair_kernel): the two waves of a SIMD stream one region of
-//     input rows [R, E) from both ends (as K1's paired bands, claiming input
-//     rows three at a time until they meet at m), with no halo rows: a wave
-//     whose input rows are [a, b) produces generation t for rows
-//     [a + t, b - t) only (the shrinking trapezoid) and stores generation D
-//     rows [a + D, b - D).  Each wave exports, per generation t = 1..D-1, the
-//     two rows at each end of its trapezoid: the first two it produces
-//     (input index 2t, 2t + 1, during the pipeline fill) and the last two
-//     (the stage inputs of its last two input rows, still in the ring).
-//   B (gol_split_tri_kernel): one wave per boundary (the meeting point m of
-//     each region and the region ends) computes the triangle in between,
-//     generation s rows [b - s, b + s) for s = 1..D, from generation s-1 rows
-//     [b - s - 1, b + s + 1): the outer two on each side are the exports, the
-//     inner ones its own previous stage, held in registers.
-// Work per band: S D + ~0.25 D^2 stage-rows instead of S D + 1.25 D^2.
-// ---------------------------------------------------------------------------
-// Export rows: per (region, tile) 4 slots x (D - 1) generations x 3 tile rows
-// (64 lanes x WPL words, lane-contiguous): j = 0 the generation-t row next
-// to the triangle (the "inner" row, raw: B needs it as a centre); for the
-// end slots 1, 2, j = 1, 2 are the row sums (s0, s1) of the row beyond it (the
-// "outer" row: B only needs its sums), for the start slots 0, 3, j = 1 is the
-// outer row raw (stored from inside the fill's groups, where its sums are
-// not at hand; B sums it).  Slot 0: U's first rows (inner R + t, outer R + t + 1); 1: U's last
-// rows (inner m - 1 - t, outer m - 2 - t); 2: L's last rows (inner m + t,
-// outer m + 1 + t); 3: L's first rows (inner E - 1 - t, outer E - 2 - t).  The
-// end exports are the ring's live state (the last row's centre and both
-// rows' sums), so they cost no extra registers.
-template <int D, int WPL>
-__device__ __forceinline__ size_t split_exp_off(const SplitArgs &p, int region, int tile, int slot, int t, int j) {
-    const size_t row = ((((size_t)region * p.tiles_x + tile) * 4 + slot) * (D - 1) + (t - 1)) * 3 + j;
-    return row * (64 * WPL);
+// Popcount of a workgroup's waves into *alive with one device atomic (the
+// last of `active` waves to arrive adds the sum).
+__device__ __forceinline__ void wg_count(unsigned long long *alive, unsigned long long *s_cnt, uint32_t cnt, int active) {
+    const uint32_t tot = wave_sum_u32(cnt);
+    if ((threadIdx.x & 63) == 0) {
+        const unsigned long long mine = (1ull << 40) | tot;
+        const unsigned long long now = atomicAdd(s_cnt, mine) + mine;
+        const unsigned long long sum = now & ((1ull << 40) - 1);
+        if ((int)(now >> 40) == active && sum) atomicAdd(alive, sum);
+    }
 }
-template <int D, int WPL>
-__device__ __forceinline__ uint32_t *split_exp_row(const SplitArgs &p, int region, int tile, int slot, int t, int j) {
-    return p.exp + split_exp_off<D, WPL>(p, region, tile, slot, t, j);
-}
+
+// Row helpers of the skewed band stacks (K1w below): one tile row as lanes.
 template <int WPL>
 __device__ __forceinline__ void put_lanes(uint32_t *row, const uint32_t (&v)[WPL]) {
     const int lane = threadIdx.x & 63;
@@ -873,17 +773,7 @@ __device__ __forceinline__ Lanes<WPL> load_row(const uint32_t *p) {
     }
     return v;
 }
-template <int WPL>
-__device__ __forceinline__ void store_row(uint32_t *p, const Lanes<WPL> &v) {
-    if constexpr (WPL == 1)
-        *p = v.w[0];
-    else if constexpr (WPL == 2)
-        *reinterpret_cast<uint2 *>(p) = make_uint2(v.w[0], v.w[1]);
-    else
-        *reinterpret_cast<uint4 *>(p) = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
-}
-
-// push_group for the fill of a split band: before stage t of a row with input
+// push_group for the fill of a skewed band: before stage t of a row with input
 // index ii in {2t, 2t + 1} (its first two valid rows), hook(t, ii, x) exports it.
 template <int D, int A, int WPL, typename Hook>
 __device__ __forceinline__ void push_group_exp(Lanes<WPL> &x0, Lanes<WPL> &x1, Lanes<WPL> &x2,
@@ -909,346 +799,6 @@ __device__ __forceinline__ void push_group_exp(Lanes<WPL> &x0, Lanes<WPL> &x1, L
         }
     }
 }
-// Input rows a wave streams before it claims any (the fill, which exports
-// the first rows of generations 1..D-1): the first multiple of 3 >= 2D.
-__host__ __device__ constexpr int split_prefix(int depth) { return 3 * ((2 * depth + 2) / 3); }
-
-// One wave of a split region: dir = 1 (U) streams input rows R, R+1, ...,
-// dir = -1 (L) streams E-1, E-2, ...; both claim rows from *claim after their
-// prefix.  Returns the popcount of its stored rows.
-template <int D, int WPL>
-__device__ __forceinline__ uint32_t stream_split(const SplitArgs &p, int region, int tile, int dir, int *claim) {
-    const StepArgs &a = p.base;
-    const int lane = threadIdx.x & 63;
-    const int Ww = a.Ww, H = a.rows_out;
-    const int R = (int)((int64_t)region * H / p.nreg), E = (int)((int64_t)(region + 1) * H / p.nreg);
-    const int len = E - R;
-    const int t0 = tile * kTileValid * WPL;
-    int col = (t0 + WPL * (lane - 1)) % Ww;
-    if (col < 0) col += Ww;
-    const bool keep = lane >= 1 && lane <= kTileValid && (t0 + WPL * (lane - 1)) < Ww;
-    int r = dir > 0 ? R : E - 1;  // next input row (absolute, wraps: prefetch past the board)
-    const uint32_t *__restrict__ src = a.src + (size_t)a.in.base * Ww + col;
-    auto load_next = [&]() -> Lanes<WPL> {
-        const Lanes<WPL> v = load_row<WPL>(src + (size_t)r * Ww);
-        if (dir > 0)
-            r = (r + 1 == H) ? 0 : r + 1;
-        else
-            r = (r == 0) ? H - 1 : r - 1;
-        return v;
-    };
-    // output index oi = input index - 2D: generation-D row R + D + oi (U) or
-    // E - 1 - D - oi (L); stored when oi >= 0 (every consumed input is real)
-    const __amdgpu_buffer_rsrc_t brs =
-        __builtin_amdgcn_make_buffer_rsrc(a.dst + (size_t)(a.dst_base + R) * Ww, (short)0, WPL <= 2 ? len * Ww * 4 : 0,
-                                          0x00020000);
-    uint32_t cnt = 0;
-    auto emit = [&](const Lanes<WPL> &y, int oi) {
-        const bool ok = keep && oi >= 0;
-        const int rel = dir > 0 ? D + oi : len - 1 - D - oi;
-        if constexpr (WPL <= 2) {
-            const int off = ok ? (rel * Ww + col) * 4 : INT_MAX;  // out of range: dropped
-            if constexpr (WPL == 1)
-                __builtin_amdgcn_raw_buffer_store_b32(y.w[0], brs, off, 0, 0);
-            else
-                __builtin_amdgcn_raw_buffer_store_b64((__attribute__((ext_vector_type(2))) unsigned){y.w[0], y.w[1]},
-                                                      brs, off, 0, 0);
-        } else if (ok) {
-            store_row<WPL>(a.dst + (size_t)(a.dst_base + R + rel) * Ww + col, y);
-        }
-        uint32_t pc = 0;
-#pragma unroll
-        for (int k = 0; k < WPL; ++k) pc += __builtin_popcount(y.w[k]);
-        cnt += ok ? pc : 0u;
-    };
-    const int start_slot = dir > 0 ? 0 : 3, end_slot = dir > 0 ? 1 : 2;
-    // Start exports from inside the fill's groups as buffer stores whose
-    // offset is out of range unless the row is one to export (no branch: a
-    // branch per stage-row splits the group's code and costs far more).
-    const __amdgpu_buffer_rsrc_t ers = __builtin_amdgcn_make_buffer_rsrc(
-        p.exp + split_exp_off<D, WPL>(p, region, tile, start_slot, 1, 0), (short)0, (D - 1) * 3 * 64 * WPL * 4,
-        0x00020000);
-    const int lane_off = lane * WPL * 4;
-    auto hook = [&](int t, int ii, const Lanes<WPL> &x) {
-        const int d = ii - 2 * t;
-        const int rowb = (t >= 1 && (d == 0 || d == 1)) ? ((t - 1) * 3 + d) * 64 * WPL * 4 : 0x40000000;
-        const int off = lane_off + rowb;
-        if constexpr (WPL == 1)
-            __builtin_amdgcn_raw_buffer_store_b32(x.w[0], ers, off, 0, 0);
-        else if constexpr (WPL == 2)
-            __builtin_amdgcn_raw_buffer_store_b64((__attribute__((ext_vector_type(2))) unsigned){x.w[0], x.w[1]}, ers,
-                                                  off, 0, 0);
-        else
-            __builtin_amdgcn_raw_buffer_store_b128(
-                (__attribute__((ext_vector_type(4))) unsigned){x.w[0], x.w[1], x.w[2], x.w[3]}, ers, off, 0, 0);
-    };
-
-    uint32_t h0[3][D][WPL], h1[3][D][WPL], cc[3][D][WPL];
-#pragma unroll
-    for (int s = 0; s < 3; ++s)
-#pragma unroll
-        for (int t = 0; t < D; ++t)
-#pragma unroll
-            for (int k = 0; k < WPL; ++k) h0[s][t][k] = h1[s][t][k] = cc[s][t][k] = 0u;
-
-    Lanes<WPL> x0 = vmov(load_next()), x1 = vmov(load_next()), x2 = vmov(load_next());
-    int ii = 0;  // input index of x0
-    // Fill: phase A runs stages [0, A) while no row of the group reaches stage A
-    // (stage t is valid from input index 2t); the last phase (A = D) runs until
-    // every first row is exported (input index 2D - 1).
-    auto fill = [&](auto a_tag) {
-        constexpr int A = decltype(a_tag)::value;
-        for (; A == D ? ii <= 2 * D - 1 : (ii + 2) / 2 <= A - 1; ii += 3) {
-            const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
-            __builtin_amdgcn_sched_barrier(0);
-            Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
-            push_group_exp<D, A, WPL>(y0, y1, y2, h0, h1, cc, ii, hook);
-            if constexpr (A == D) {
-                emit(y0, ii - 2 * D);
-                emit(y1, ii + 1 - 2 * D);
-                emit(y2, ii + 2 - 2 * D);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            x0 = vmov(n0);
-            x1 = vmov(n1);
-            x2 = vmov(n2);
-        }
-    };
-    if constexpr (D >= 4) {
-        fill(std::integral_constant<int, D / 4>());
-        fill(std::integral_constant<int, D / 2>());
-        fill(std::integral_constant<int, 3 * D / 4>());
-    }
-    fill(std::integral_constant<int, D>());
-
-    // The group after the fill is the wave's own (P0 + 3 rows each); each
-    // body claims the next group, and learns at its end (the LDS round trip
-    // hidden under the group) whether there is one.  A grant of 1 or 2 rows
-    // still streams a whole group: its last rows overlap the other wave's
-    // first ones (real rows, computed twice); B takes the overlap delta from
-    // the two waves' row counts.  On the last body the ring holds the band's
-    // last two rows: stage t's input of the last (raw, the triangle's inner
-    // row) and the row sums of the one before (outer) are exported there, in
-    // the loop (used after the loop, the ring state spills inside it).
-    Lanes<WPL> q0, q1, q2;
-#pragma unroll
-    for (int k = 0; k < WPL; ++k) q0.w[k] = q1.w[k] = q2.w[k] = 0u;
-    int qoi = -8;  // the first body stores nothing real
-    for (int i = 0; i < GOL_LOOP_PAD; ++i) asm volatile("s_nop 0");
-    for (;;) {
-        const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
-        emit(q0, qoi);
-        emit(q1, qoi + 1);
-        emit(q2, qoi + 2);
-        int o = 0;
-        if (lane == 0) o = __hip_atomic_fetch_add(claim, -3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __builtin_amdgcn_sched_barrier(0);
-        Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
-        push_group<D, D, WPL>(y0, y1, y2, h0, h1, cc);
-        q0 = y0;
-        q1 = y1;
-        q2 = y2;
-        qoi = ii - 2 * D;
-        ii += 3;
-        __builtin_amdgcn_sched_barrier(0);
-        x0 = vmov(n0);
-        x1 = vmov(n1);
-        x2 = vmov(n2);
-        asm volatile("" : "+v"(o));  // the LDS wait here, after the group
-        if (__builtin_amdgcn_readfirstlane(o) <= 0) {
-            size_t off = split_exp_off<D, WPL>(p, region, tile, end_slot, 1, 0);
-            asm volatile("" : "+s"(off));
-            uint32_t *row = p.exp + off;
-#pragma unroll
-            for (int t = 1; t < D; ++t) {
-                put_lanes<WPL>(row, cc[2][t]);
-                put_lanes<WPL>(row + 64 * WPL, h0[1][t]);
-                put_lanes<WPL>(row + 2 * 64 * WPL, h1[1][t]);
-                row += 3 * 64 * WPL;
-            }
-            break;
-        }
-    }
-    emit(q0, qoi);
-    emit(q1, qoi + 1);
-    emit(q2, qoi + 2);
-    if (lane == 0) p.meet[2 * (region * p.tiles_x + tile) + (dir > 0 ? 0 : 1)] = ii;
-    return cnt;
-}
-
-// Popcount of a workgroup's waves into *alive with one device atomic (the
-// last of `active` waves to arrive adds the sum).
-__device__ __forceinline__ void wg_count(unsigned long long *alive, unsigned long long *s_cnt, uint32_t cnt, int active) {
-    const uint32_t tot = wave_sum_u32(cnt);
-    if ((threadIdx.x & 63) == 0) {
-        const unsigned long long mine = (1ull << 40) | tot;
-        const unsigned long long now = atomicAdd(s_cnt, mine) + mine;
-        const unsigned long long sum = now & ((1ull << 40) - 1);
-        if ((int)(now >> 40) == active && sum) atomicAdd(alive, sum);
-    }
-}
-
-// K1s A: a workgroup of 8 waves = 4 (region, tile) units, waves w and w + 4
-// (the two of a SIMD) stream unit w & 3 from the top and from the bottom.
-template <int D, int WPL>
-__global__ __launch_bounds__(512) void gol_split_pair_kernel(SplitArgs p) {
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int units = p.nreg * p.tiles_x;
-    const int qu = blockIdx.x * 4 + (w & 3);
-    const int region = qu / p.tiles_x, tile = qu - region * p.tiles_x;
-    const int H = p.base.rows_out;
-    __shared__ int s_claim[4];
-    __shared__ unsigned long long s_cnt;
-    if (w < 4 && lane == 0 && qu < units) {
-        const int len = (int)((int64_t)(region + 1) * H / p.nreg) - (int)((int64_t)region * H / p.nreg);
-        s_claim[w] = len - 2 * (p.P0 + 3);
-    }
-    if (threadIdx.x == 0) s_cnt = 0;
-    __syncthreads();
-    if (qu >= units) return;  // wave-uniform, after the only barrier
-    const uint32_t cnt = stream_split<D, WPL>(p, region, tile, w < 4 ? 1 : -1, &s_claim[w & 3]);
-    if (p.base.alive) wg_count(p.base.alive, &s_cnt, cnt, 2 * min(4, units - blockIdx.x * 4));
-}
-
-// K1s B: one wave per (boundary, tile); boundary e = 2 q is region q's meeting
-// point, e = 2 q + 1 its end (region q + 1's start).  Positions p are rows
-// b + p, b the lower band's first row; the upper band ends at b + delta
-// (delta = 0..2 rows streamed by both waves of a region, 0 at region ends).
-// cur[p + D + 1] holds generation s - 1 of row b + p while stage s computes
-// rows [delta - s, s).
-template <int D, int WPL>
-__global__ __launch_bounds__(256) void gol_split_tri_kernel(SplitArgs p) {
-    const StepArgs &a = p.base;
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-    const int nb = 2 * p.nreg * p.tiles_x;
-    __shared__ unsigned long long s_cnt;
-    if (threadIdx.x == 0) s_cnt = 0;
-    __syncthreads();
-    if (wave >= nb) return;
-    const int Ww = a.Ww, H = a.rows_out;
-    const int e = wave / p.tiles_x, tile = wave - e * p.tiles_x;
-    const int q = e >> 1, kind = e & 1;
-    const int R = (int)((int64_t)q * H / p.nreg), E = (int)((int64_t)(q + 1) * H / p.nreg);
-    const int unit = q * p.tiles_x + tile;
-    const int b = kind == 0 ? E - p.meet[2 * unit + 1] : (E == H ? 0 : E);
-    const int delta = kind == 0 ? (R + p.meet[2 * unit]) - (E - p.meet[2 * unit + 1]) : 0;
-    const int up_reg = q, up_slot = kind == 0 ? 1 : 3;
-    const int lo_reg = kind == 0 ? q : (q + 1 == p.nreg ? 0 : q + 1), lo_slot = kind == 0 ? 2 : 0;
-    const int t0 = tile * kTileValid * WPL;
-    int col = (t0 + WPL * (lane - 1)) % Ww;
-    if (col < 0) col += Ww;
-    const bool keep = lane >= 1 && lane <= kTileValid && (t0 + WPL * (lane - 1)) < Ww;
-    auto row_of = [&](int pp) {
-        int rr = b + pp;
-        rr = rr < 0 ? rr + H : (rr >= H ? rr - H : rr);
-        return rr;
-    };
-    const uint32_t *__restrict__ src = a.src + (size_t)a.in.base * Ww + col;
-
-    Lanes<WPL> cur[2 * D + 2];
-#pragma unroll
-    for (int i = 0; i < 2 * D + 2; ++i)
-#pragma unroll
-        for (int k = 0; k < WPL; ++k) cur[i].w[k] = 0u;
-    // Generation s - 1 outer rows for stage s: upper inner (position -s, raw)
-    // and outer sums (-s - 1), lower inner (s - 1, raw) and outer sums (s).
-    // Stage 1 takes generation 0 from the board; each stage loads the next
-    // one's exports (a deeper register ring measured slower: fewer waves).
-    Lanes<WPL> ui, li;
-    uint32_t us0[WPL], us1[WPL], ls0[WPL], ls1[WPL];
-    {
-        const Lanes<WPL> uo = load_row<WPL>(src + (size_t)row_of(delta - 2) * Ww);
-        const Lanes<WPL> lo = load_row<WPL>(src + (size_t)row_of(1) * Ww);
-        ui = load_row<WPL>(src + (size_t)row_of(delta - 1) * Ww);
-        li = load_row<WPL>(src + (size_t)row_of(0) * Ww);
-        row_sums<WPL>(uo, us0, us1);
-        row_sums<WPL>(lo, ls0, ls1);
-    }
-    for (int s = 1; s <= D; ++s) {
-        Lanes<WPL> nui = ui, nli = li, nus0 = ui, nus1 = ui, nls0 = li, nls1 = li;
-        if (s < D) {
-            nui = get_lanes<WPL>(split_exp_row<D, WPL>(p, up_reg, tile, up_slot, s, 0));
-            nus0 = get_lanes<WPL>(split_exp_row<D, WPL>(p, up_reg, tile, up_slot, s, 1));
-            nli = get_lanes<WPL>(split_exp_row<D, WPL>(p, lo_reg, tile, lo_slot, s, 0));
-            nls0 = get_lanes<WPL>(split_exp_row<D, WPL>(p, lo_reg, tile, lo_slot, s, 1));
-            if (kind == 0) {
-                nus1 = get_lanes<WPL>(split_exp_row<D, WPL>(p, up_reg, tile, up_slot, s, 2));
-                nls1 = get_lanes<WPL>(split_exp_row<D, WPL>(p, lo_reg, tile, lo_slot, s, 2));
-            }
-        }
-        uint32_t ha0[WPL], ha1[WPL], hb0[WPL], hb1[WPL];
-#pragma unroll
-        for (int k = 0; k < WPL; ++k) {
-            ha0[k] = us0[k];
-            ha1[k] = us1[k];
-        }
-        row_sums<WPL>(ui, hb0, hb1);
-#pragma unroll
-        for (int S = 1; S <= D; ++S) {
-            if (s == S) {
-#pragma unroll
-                for (int Dl = 0; Dl <= 2; ++Dl)
-                    if (delta == Dl) cur[Dl - S + D + 1] = ui;
-                cur[S - 1 + D + 1] = li;
-            }
-        }
-#pragma unroll
-        for (int P = -D; P < D; ++P) {
-            if (P >= delta - s && P < s) {
-                uint32_t hc0[WPL], hc1[WPL];
-                if (P + 1 == s) {  // the lower outer row: its sums come with the exports
-#pragma unroll
-                    for (int k = 0; k < WPL; ++k) {
-                        hc0[k] = ls0[k];
-                        hc1[k] = ls1[k];
-                    }
-                } else {
-                    row_sums<WPL>(cur[P + 1 + D + 1], hc0, hc1);
-                }
-                Lanes<WPL> nx;
-#pragma unroll
-                for (int k = 0; k < WPL; ++k)
-                    nx.w[k] = rule_word(ha0[k], ha1[k], hb0[k], hb1[k], hc0[k], hc1[k], cur[P + D + 1].w[k]);
-                cur[P + D + 1] = nx;
-#pragma unroll
-                for (int k = 0; k < WPL; ++k) {
-                    ha0[k] = hb0[k];
-                    ha1[k] = hb1[k];
-                    hb0[k] = hc0[k];
-                    hb1[k] = hc1[k];
-                }
-            }
-        }
-        if (s < D) {  // generation s for stage s + 1
-            ui = nui;
-            li = nli;
-            if (kind == 1) {
-                row_sums<WPL>(nus0, us0, us1);
-                row_sums<WPL>(nls0, ls0, ls1);
-            } else {
-#pragma unroll
-                for (int k = 0; k < WPL; ++k) {
-                    us0[k] = nus0.w[k];
-                    us1[k] = nus1.w[k];
-                    ls0[k] = nls0.w[k];
-                    ls1[k] = nls1.w[k];
-                }
-            }
-        }
-    }
-    uint32_t cnt = 0;
-#pragma unroll
-    for (int P = -D; P < D; ++P) {
-        const bool ok = keep && P >= delta - D;
-        if (ok) store_row<WPL>(a.dst + (size_t)(a.dst_base + row_of(P)) * Ww + col, cur[P + D + 1]);
-#pragma unroll
-        for (int k = 0; k < WPL; ++k) cnt += ok ? __builtin_popcount(cur[P + D + 1].w[k]) : 0u;
-    }
-    if (a.alive) wg_count(a.alive, &s_cnt, cnt, min(4, nb - (int)blockIdx.x * 4));
-}
-
 // ---------------------------------------------------------------------------
 // K1w: skewed band stacks (round 3; torus and row strips, per launch).
 //
@@ -1791,14 +1341,8 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
 // Per row and word: three LDS loads (own word or pair, one neighbour word
 // each side), the row sums (2 LUTs, and a funnel shift per pair side), the
 // column sums and the rule (7 LUTs), one LDS store; each buffer has 3 spare
-// rows for the row loop's prefetch.  Option lds_split runs a full super-step
-// boundary first (edge rows, publish, interior).  Every wait
-// is bounded (error word, all drain).
+// rows for the row loop's prefetch.  Every wait is bounded (error word, all drain).
 // ---------------------------------------------------------------------------
-template <int WPL>
-struct LdsRow {
-    uint32_t s0[WPL], s1[WPL], c[WPL];
-};
 // A row's words as loaded: the lane's own word (pair) and one neighbour word on each side.
 template <int WPL>
 struct LdsRaw {
@@ -1846,8 +1390,6 @@ __device__ __forceinline__ void lds_sums(const LdsRaw<WPL> &x, LdsRow<WPL> &s) {
     }
 }
 
-typedef unsigned v4u32 __attribute__((ext_vector_type(4)));
-constexpr int kCpolSc1 = 16;  // buffer load/store aux bit: sc1 (write-through store, L1-bypassing load)
 
 // S > 0: LDS rows S words apart (>= Ww, a compile-time stride: the row
 // loop's loads and stores of consecutive rows take immediate offsets); 0: Ww.
@@ -2035,7 +1577,7 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
         // rows read turn t - 1's interior rows D + t - 1, D + t (bottom: D + h - t
         // - 1, D + h - t), which the interior turns t + 1, t + 3, .. (same buffer)
         // never reach.  Turn t's buffer is A for even t, B for odd.
-        const int pre = (j > 0 && Dj == D && !p.split) ? min(p.pre, D) : 0;
+        const int pre = (j > 0 && Dj == D) ? min(p.pre, D) : 0;
         if (pre > 0) {
             for (int t = 1; t <= pre; ++t) {
                 do_turn((t & 1) ? A : B, (t & 1) ? B : A, D + t, D + h - t, 0, 0);
@@ -2067,51 +1609,25 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
             pending = false;
         }
         if (j > 0 && !wait_halos()) return;
-        if (p.split && Dj == D) {
-            // Boundary first: turn t computes the top rows [t, 3D - t) and the bottom
-            // rows [h - D + t, h + 2D - t) (the only rows the edges depend on), the
-            // edges leave, and the interior [3D - t, h - D + t) follows while they
-            // travel.  Turn t of the interior reads turn t - 1's rows 3D - t - 1 ..
-            // 3D - t and h - D + t - 1 .. h - D + t from the edge phase: still in the
-            // turn-(t - 1) buffer, since the edge phase's turn t + 1 stopped at row
-            // 3D - t - 2 (started at h - D + t + 1).  Turn t's buffer is A for even
-            // t, B for odd.
-            for (int t = 1; t <= D; ++t)
-                do_turn((t & 1) ? A : B, (t & 1) ? B : A, t, 3 * D - t, h - D + t, h + 2 * D - t);
-            uint32_t *F = (D & 1) ? B : A;
-            lap(0);
-            if (more) publish(F);
-            lap(1);
-            for (int t = 1; t <= D; ++t) {
-                do_turn((t & 1) ? A : B, (t & 1) ? B : A, 3 * D - t, h - D + t, 0, 0);
-                if (t == 1 && more) signal((unsigned)(j + 1));
-            }
-            if (F != A) {
-                B = A;
-                A = F;
-            }
-            lap(0);
-        } else {
-            // the last, shorter super-step needs only Dj halo rows of the D
-            const int skip = D - Dj;
-            for (int t = 1; t <= Dj; ++t) {
-                do_turn(A, B, skip + t, R - skip - t, 0, 0);
-                uint32_t *T = A;
-                A = B;
-                B = T;
-            }
-            lap(0);
-            if (more) {
-                publish(A);
-                // the next super-step signals after its first interior turn when it
-                // runs interior first (full, lds_pre), else now
-                if (p.pre > 0 && !p.split && min(D, p.turns - (j + 1) * D) == D)
-                    pending = true;
-                else
-                    signal((unsigned)(j + 1));
-            }
-            lap(1);
+        // whole turns (a shorter last super-step needs only Dj halo rows of the D)
+        const int skip = D - Dj;
+        for (int t = 1; t <= Dj; ++t) {
+            do_turn(A, B, skip + t, R - skip - t, 0, 0);
+            uint32_t *T = A;
+            A = B;
+            B = T;
         }
+        lap(0);
+        if (more) {
+            publish(A);
+            // the next super-step signals after its first interior turn when it
+            // runs interior first (full, lds_pre), else now
+            if (p.pre > 0 && min(D, p.turns - (j + 1) * D) == D)
+                pending = true;
+            else
+                signal((unsigned)(j + 1));
+        }
+        lap(1);
     }
     if (p.trace && threadIdx.x == 0) {
         for (int k = 0; k < 4; ++k) atomicAdd(&p.trace[k], (unsigned long long)tr[k]);
@@ -2246,29 +1762,6 @@ hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s, bool fill
         hipLaunchKernelGGL(kern, grid, block, 0, s, a);
         return hipGetLastError();
     });
-}
-
-bool split_supported(int depth, int wpl) {
-    return (wpl == 2 && (depth == 8 || depth == 12 || depth == 16 || depth == 20)) || (wpl == 4 && (depth == 8 || depth == 9)) ||
-           (wpl == 1 && (depth == 16 || depth == 32));
-}
-int split_prefix_rows(int depth) { return split_prefix(depth); }
-
-hipError_t launch_split(const SplitArgs &p, int depth, int wpl, hipStream_t s) {
-    const int units = p.nreg * p.tiles_x;
-    const dim3 ga((units + 3) / 4), gb((2 * units + 3) / 4);
-#define GOL_SCASE(D, WP)                                                    \
-    if (depth == D && wpl == WP) {                                          \
-        hipLaunchKernelGGL((gol_split_pair_kernel<D, WP>), ga, dim3(512), 0, s, p); \
-        hipError_t e = hipGetLastError();                                   \
-        if (e != hipSuccess) return e;                                      \
-        hipLaunchKernelGGL((gol_split_tri_kernel<D, WP>), gb, dim3(256), 0, s, p); \
-        return hipGetLastError();                                           \
-    }
-    GOL_SCASE(8, 2) GOL_SCASE(12, 2) GOL_SCASE(16, 2) GOL_SCASE(20, 2) GOL_SCASE(8, 4) GOL_SCASE(9, 4) GOL_SCASE(16, 1)
-    GOL_SCASE(32, 1)
-#undef GOL_SCASE
-    return hipErrorInvalidValue;
 }
 
 template <typename F>

@@ -112,12 +112,6 @@ struct golhip {
     int cu_count = 0;           // CUs the launches are planned for (option "cu_count": fewer)
     int dev_cu = 0;             // the device's CUs
     bool fill_skip = true;      // option "fill_skip"
-    int split = 1;              // option "split": split tiling (K1s) for per-launch torus steps
-                                // (65536^2 +1.3 %, 262144^2 +4.4 %, profiles/r2t/split_ab.jsonl)
-    uint32_t *split_exp = nullptr;  // K1s export rows
-    int64_t split_exp_cap = 0;      // words
-    int *split_meet = nullptr;      // K1s per-region wave row counts
-    int64_t split_meet_cap = 0;
     int last_variant = 1;           // kernel family of the last step launch (golhip_perf kernel_variant)
     int skew = 1;                   // option "skew": skewed band stacks (K1w) for per-launch steps
     int skew_young = 0;             // option "skew_young": band height of waves 4..7, % of waves 0..3's (0: by kernel)
@@ -125,7 +119,6 @@ struct golhip {
     int skew_prio = 0;              // option "skew_prio": s_setprio 1 for waves 4..7
     int skew_tx = 0;                // option "skew_tx": tiles per K1w workgroup (0: plan, 1 or 2)
     int skew_half = 0;              // option "skew_half": half-wave tiles (0: when fewer wave-rows, 1: whenever possible, -1: never)
-    int skew_nst = 0;               // option "skew_nst" (measurement): stacks per tile column (0: plan)
     int lds_bpc[4] = {};               // K1r workgroups per CU by (wpl, 512 / 1024 threads) at lds_bpc_bytes of LDS
     int64_t lds_bpc_bytes[4] = {};
     int lds_bpc_stride[4] = {};
@@ -140,11 +133,20 @@ struct golhip {
     int lds_waves = 8;              // option "lds_waves": K1r waves per workgroup (8 or 16)
     int lds_wg_cu = 1;              // option "lds_wg_cu": K1r bands (workgroups) per CU (1 or 2)
     int lds_stride = 1;             // option "lds_stride": K1r LDS rows at a compile-time stride where instantiated
-    int lds_split = 0;              // option "lds_split": K1r super-steps compute and publish their edge rows first
     int resident_fault = 0;         // option "resident_fault" (tests): K1r band 0 / K1p workgroup 0 never report
                                     // (their neighbours' bounded waits time out: the restore-and-re-run path)
     int lds_pre = 2;                // option "lds_pre": K1r interior-first turns while the halos travel
                                     // (profiles/r4pre: 8192^2 31.4 -> 33.9 TCUPS at 2; 1: 33.2, 3: 33.1, 4: 32.3)
+    int lds_pipe = 0;               // option "lds_pipe": resident LDS turn pipeline K1t where it fits (1; 0 off:
+                                    // slower than K1r at every width it runs)
+    uint32_t *pipe_edge = nullptr;  // K1t edge rows (golk::pipe_edge_words)
+    int64_t pipe_edge_cap = 0;
+    unsigned *pipe_sync = nullptr;  // K1t [0] error, then econs[nb]
+    uint32_t pipe_tag_base = 0;     // K1t edge tags: next launch's base (0: edge buffer not zeroed yet)
+    int64_t pipe_sync_cap = 0;
+    int pipe_bpc[3] = {};           // K1t workgroups per CU by wpl at pipe_bpc_bytes of LDS
+    int64_t pipe_bpc_bytes[3] = {};
+    int64_t pipe_launches = 0;
     uint32_t *lds_edge = nullptr;   // K1r edge rows (golk::lds_band_edge_words)
     int64_t lds_edge_cap = 0;
     int64_t lds_launches = 0;
@@ -152,7 +154,6 @@ struct golhip {
     int wpl_opt = 0;            // option "wpl": words per lane (0 = auto, 1, 2, 4)
     int persist_depth = 0;      // option "persist_depth" (0: tb_depth)
     int persist_waves = 0;      // option "persist_waves": waves per workgroup (0: default)
-    int age_split = -1;         // option "age_split": % of a workgroup's rows for its oldest waves (0: equal, -1: auto)
     int paired_bands = 1;       // option "paired_bands": SIMD mates share two bands from both ends (persistent)
     int dummy_rows = 0;         // option "dummy_rows": halo rows taking the kernels' dummy stores (0: all)
     int persist_wg_tx = 0;      // option "persist_wg_tx": tiles across a persistent workgroup (0: plan)
@@ -210,15 +211,6 @@ struct golhip {
     int nranks = 1, rank = 0;
     int ring_rows = 0;          // smallest strip of the ring (every rank plans from it)
     int halo_skip = 0;          // option "halo_skip" (measurement only: no exchange, wrong halos)
-    // option "overlap": the last launch of an exchange round runs its boundary
-    // rows on a side stream, then posts the next round's exchange there, while
-    // the interior rows run on the engine stream (launch_overlap)
-    int overlap = 0;
-    hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_x = nullptr;
-    int halo_ready = 0;         // halo rows already exchanged for the board at turn halo_turn
-    int64_t halo_turn = -1;
-    int64_t overlap_launches = 0;
     int64_t halo_exchanges = 0;
     double halo_ms = 0;         // exchange time on the engine stream (GOLHIP_FLAG_TIMING)
 
@@ -230,7 +222,7 @@ struct golhip {
     };
     std::vector<Timed> ev_pending;
     double step_ms = 0, persist_ms = 0;
-    int64_t step_launches = 0, step_turns = 0, halo_bytes = 0, split_launches = 0;
+    int64_t step_launches = 0, step_turns = 0, halo_bytes = 0;
     int64_t persist_turns = 0;
 
     std::mutex mu;
@@ -390,6 +382,8 @@ constexpr int64_t kPersistAutoMaxBytes = 64ll << 20;
 int wpl_per_launch(golhip_t h);
 bool skew_fills(golhip_t h);
 bool lds_fits(golhip_t h, int wpl, golk::LdsBandArgs *out = nullptr);
+int pipe_wpl(golhip_t h);
+bool pipe_fits(golhip_t h, int wpl, golk::PipeArgs *out = nullptr);
 bool persist_on(golhip_t h) {
     // a multi-rank ring never runs the resident kernel (try_persist_halo):
     // plan words per lane and halos for the per-launch kernels that do run
@@ -410,6 +404,7 @@ int wpl_for(golhip_t h) {
     if (h->wpl_opt == 1 || h->wpl_opt == 2) return h->wpl_opt;
     if (h->wpl_opt == 4) return h->W % 128 == 0 ? 4 : 2;
     if ((!h->torus() && !h->comm) || !persist_on(h)) return wpl_per_launch(h);
+    if (pipe_fits(h, pipe_wpl(h))) return pipe_wpl(h);  // K1t: a whole row per wave
     if (lds_fits(h, 2)) return 2;  // K1r: pairs (11 slots a word-turn against 15)
     auto best = [&](int wpl) {
         const int d = default_depth(h, wpl);
@@ -453,7 +448,6 @@ int wpl_per_launch(golhip_t h) {
 // Converts the current board in place when the wanted layout changes.
 int set_layout(golhip_t h, int il) {
     if (h->il == il) return GOLHIP_OK;
-    h->halo_ready = 0;
     if (h->loaded) HIP_OR_FAIL(golk::launch_convert_layout(h->cur_rows(), h->local_words(), h->il, il, h->stream));
     h->il = il;
     return GOLHIP_OK;
@@ -462,7 +456,6 @@ int want_il(golhip_t h) { return wpl_for(h) >= 2 ? wpl_for(h) : 0; }
 // After canonical words were written into the current buffer.
 int loaded_canonical(golhip_t h) {
     h->il = 0;
-    h->halo_ready = 0;
     h->loaded = true;
     return set_layout(h, want_il(h));
 }
@@ -613,54 +606,6 @@ void shift_rows(golk::StepArgs &a, int lo, int hi) {
     a.count_hi = -lo + rows;
 }
 
-// Split tiling (K1s, option "split"): whole-torus launches whose depth and
-// words per lane have an instance.  Regions of input rows, two waves each,
-// sized to fill the CUs' wave slots once (two per SIMD); each region needs
-// 2 (P0 + 3) rows (both waves' own prefix) plus a little to share.
-bool split_plan(golhip_t h, int depth, int wpl, golk::SplitArgs *sp) {
-    if (!h->split || h->W % 32 != 0 || !h->torus() || !golk::split_supported(depth, wpl)) return false;
-    const int tiles = golk::tb_tiles(h->Ww, wpl);
-    const int P0 = golk::split_prefix_rows(depth);
-    const int minlen = 2 * (P0 + 3) + 3;
-    const int pairs = std::max(1, h->cu_count * 4);  // two waves per SIMD
-    int nreg = std::max(1, pairs / tiles);
-    nreg = std::min(nreg, h->rows / minlen);
-    if (nreg < 1) return false;
-    // a region's buffer-store range (WPL <= 2: one resource over its rows) must
-    // stay < 2 GiB: more regions (they only need minlen rows each), else K1
-    const int64_t row_bytes = (int64_t)h->Ww * 4;
-    while (wpl <= 2 && ((int64_t)h->rows + nreg - 1) / nreg * row_bytes >= (1ll << 31)) {
-        if (nreg >= h->rows / minlen) return false;
-        ++nreg;
-    }
-    sp->nreg = nreg;
-    sp->tiles_x = tiles;
-    sp->P0 = P0;
-    return true;
-}
-
-int split_buffers(golhip_t h, golk::SplitArgs &sp, int depth, int wpl) {
-    const int64_t words = golk::split_exp_words(sp.nreg, sp.tiles_x, depth, wpl);
-    if (words > h->split_exp_cap) {
-        HIP_OR_FAIL(hipFree(h->split_exp));
-        h->split_exp = nullptr;
-        h->split_exp_cap = 0;
-        HIP_OR_FAIL(hipMalloc(&h->split_exp, (size_t)words * 4));
-        h->split_exp_cap = words;
-    }
-    const int64_t nm = 2ll * sp.nreg * sp.tiles_x;
-    if (nm > h->split_meet_cap) {
-        HIP_OR_FAIL(hipFree(h->split_meet));
-        h->split_meet = nullptr;
-        h->split_meet_cap = 0;
-        HIP_OR_FAIL(hipMalloc(&h->split_meet, (size_t)nm * sizeof(int)));
-        h->split_meet_cap = nm;
-    }
-    sp.exp = h->split_exp;
-    sp.meet = h->split_meet;
-    return GOLHIP_OK;
-}
-
 // Skewed band stacks (K1w, option "skew"): any per-launch step (whole torus
 // or a strip's extended rows) whose depth and words per lane have an
 // instance.  One workgroup of 8 waves per stack, sized to fill every CU once:
@@ -703,7 +648,7 @@ bool skew_dims(golhip_t h, int depth, int wpl, int L, golk::SkewArgs *sk) {
             // stacks of Lh / nst + hcap rows whose bands average at least smin + hcap
             // rows (the bottom band gives up hcap of them)
             const int nst = std::min(h->cu_count * bpc / tcols,
-                                     h->skew_nst > 0 ? h->skew_nst : Lh / (sy * (smin + hcap) - hcap));
+                                     Lh / (sy * (smin + hcap) - hcap));
             if (nst < 1) continue;
             // "skew" 1 (default): only when the stacks fill at least 3/4 of the CUs'
             // workgroup slots (smaller tori run the resident kernel, persist_on);
@@ -773,9 +718,8 @@ bool skew_plan(golhip_t h, int depth, int wpl, const golk::StepArgs &a, golk::Sk
 // Launch the step kernel for output rows [lo, hi) of this handle (halos, if
 // used, already in place); `alive` (nullable) accumulates their popcount.
 // No bookkeeping: see finish_launch.
-int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int lo, int hi,
-                hipStream_t on = nullptr) {
-    const hipStream_t st = on ? on : h->stream;
+int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int lo, int hi) {
+    const hipStream_t st = h->stream;
     golk::StepArgs a = step_args(h, alive, halo);
     if (lo != 0 || hi != h->rows) shift_rows(a, lo, hi);
     const int wpl = wpl_for(h);
@@ -798,23 +742,17 @@ int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int
         HIP_OR_FAIL(hipEventRecord(e0, st));
     }
     hipError_t e;
-    golk::SplitArgs sp{};
     golk::SkewArgs sk{};
     const bool skew = skew_plan(h, depth, wpl, a, &sk);
-    const bool split = !skew && !halo && a.rows_out == h->rows && split_plan(h, depth, wpl, &sp);
     if (skew) {
         sk.base = a;
         e = golk::launch_skew(sk, depth, wpl, st);
-    } else if (split) {
-        sp.base = a;
-        if (int rc = split_buffers(h, sp, depth, wpl)) return rc;
-        e = golk::launch_split(sp, depth, wpl, st);
     } else if (h->W % 32 == 0) {
         e = golk::launch_step_tb(a, depth, st, h->fill_skip, wpl, tb_paired(h));
     } else {
         e = golk::launch_step_generic(a, st);
     }
-    h->last_variant = h->W % 32 != 0 ? 0 : skew ? 3 : split ? 2 : 1;
+    h->last_variant = h->W % 32 != 0 ? 0 : skew ? 3 : 1;
     if (e != hipSuccess) return fail(GOLHIP_EHIP, "step launch: %s", hipGetErrorString(e));
     if (e1) {
         HIP_OR_FAIL(hipEventRecord(e1, st));
@@ -825,7 +763,6 @@ int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int
         }
     }
     h->step_launches++;
-    h->split_launches += split;
     h->skew_launches += skew;
     h->skew_half_launches += skew && sk.half;
     return GOLHIP_OK;
@@ -833,7 +770,6 @@ int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int
 
 void finish_launch(golhip_t h, int depth, bool count) {
     h->cur ^= 1;
-    h->halo_ready = 0;
     h->turns += depth;
     h->step_turns += depth;
     if (count) h->alive_turn = h->turns;
@@ -892,39 +828,6 @@ int launch_ext(golhip_t h, int depth, bool count, int ext) {
     return GOLHIP_OK;
 }
 
-// The last launch of an exchange round (ext 0) with the next round's
-// exchange of X rows overlapped (option "overlap"): the boundary rows
-// [0, X) and [rows - X, rows), which the exchange sends, run first on the
-// side stream and the exchange follows them there, while the interior rows
-// [X, rows - X) run on the engine stream; the engine waits for the exchange
-// before anything else.  All three launches read the current buffer and
-// write disjoint rows of the other; the exchange writes only halo rows.
-int ensure_side(golhip_t h) {
-    if (h->side) return GOLHIP_OK;
-    HIP_OR_FAIL(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
-    HIP_OR_FAIL(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-    HIP_OR_FAIL(hipEventCreateWithFlags(&h->ev_x, hipEventDisableTiming));
-    return GOLHIP_OK;
-}
-
-int launch_overlap(golhip_t h, int depth, int X) {
-    if (int rc = ensure_side(h)) return rc;
-    HIP_OR_FAIL(hipEventRecord(h->ev_fork, h->stream));
-    HIP_OR_FAIL(hipStreamWaitEvent(h->side, h->ev_fork, 0));
-    if (int rc = launch_rows(h, depth, nullptr, true, 0, X, h->side)) return rc;
-    if (int rc = launch_rows(h, depth, nullptr, true, h->rows - X, h->rows, h->side)) return rc;
-    if (int rc = launch_rows(h, depth, nullptr, true, X, h->rows - X)) return rc;
-    h->step_launches -= 2;  // one step launch in three parts
-    finish_launch(h, depth, false);
-    if (int rc = exchange_rccl(h, X, h->side)) return rc;
-    HIP_OR_FAIL(hipEventRecord(h->ev_x, h->side));
-    HIP_OR_FAIL(hipStreamWaitEvent(h->stream, h->ev_x, 0));
-    h->halo_ready = X;
-    h->halo_turn = h->turns;
-    h->overlap_launches++;
-    return GOLHIP_OK;
-}
-
 // After any stream sync: a persistent launch that timed out leaves the board
 // undefined, so it is reported (loudly) and the persistent path is disabled.
 int check_persist(golhip_t h) {
@@ -945,6 +848,16 @@ bool measurement_env() {
     const char *v = getenv("GOLHIP_MEASUREMENT");
     return v && !strcmp(v, "1");
 }
+// Test hooks (exact results, but they force failure paths: a band that never
+// publishes, a reported co-residency failure) need GOLHIP_TEST_HOOKS=1.
+bool test_hooks_env() {
+    const char *v = getenv("GOLHIP_TEST_HOOKS");
+    return v && !strcmp(v, "1");
+}
+// The consent-gated options, as golhip_build_info() reports them (the CPU
+// suite checks the list against the product contract).
+constexpr const char *kConsentInfo =
+    " CONSENT_MEASUREMENT=halo_skip,flip_debug:1-3 CONSENT_TEST_HOOKS=resident_fault,flip_debug:4";
 
 // After the stream has synchronised: the K1w spin-bound flag of the launches
 // it ran (reported by the call that ran them, then cleared).
@@ -974,7 +887,7 @@ bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int w
     golk::PersistArgs p{};
     // Unpaired fallback: with two waves per SIMD the older one is served
     // first, so the older half of the waves gets 65 % of the rows.
-    const int age_split = h->age_split >= 0 ? h->age_split : (nw == 8 ? 65 : 0);
+    const int age_split = nw == 8 ? 65 : 0;
     const bool split = age_split > 0 && age_split < 100;
     if (!golk::plan_persist(h->Ww, base.rows_out, depth, h->cu_count, wpl, nw, &p, h->persist_wg_tx)) return false;
     if (2ll * p.S * h->Ww * 4 >= (1ll << 31)) return false;  // a band's buffer-store range
@@ -1037,7 +950,6 @@ bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int w
         return false;
     }
     h->persist_pending = true;
-    h->halo_ready = 0;
     if (J & 1) h->cur ^= 1;
     const int64_t turns = J * depth - (half_last ? depth / 2 : 0);
     h->turns += turns;
@@ -1123,11 +1035,137 @@ bool lds_fits(golhip_t h, int wpl, golk::LdsBandArgs *out) {
         out->xcd = h->lds_xcd;
         out->nt = nt;
         out->stride = stride;
-        out->split = h->lds_split;
         out->fault = h->resident_fault;
         out->pre = h->lds_pre;
     }
     return true;
+}
+
+// K1t (gol_lds_pipe_kernel): words per lane of a torus whose rows are one
+// wavefront wide (Ww == 64 wpl), else 0.
+int pipe_wpl(golhip_t h) {
+    if (h->W % 32 != 0) return 0;
+    for (int wpl : {1, 2, 4})
+        if (h->Ww == 64 * wpl && (wpl == 1 || h->W % (32 * wpl) == 0)) return wpl;
+    return 0;
+}
+
+// The K1t plan of this torus at `wpl` words per lane (no side effects): one
+// band per CU of at least two rows, the rings of a band in one workgroup's
+// LDS, every workgroup resident (the bands wait on each other around the
+// torus).  False if K1t does not apply.
+bool pipe_fits(golhip_t h, int wpl, golk::PipeArgs *out) {
+    if (h->lds_pipe == 0 || !h->torus() || h->nranks > 1 || wpl < 1 || wpl != pipe_wpl(h)) return false;
+    const int nb = std::min(std::min(h->cu_count, h->dev_cu), h->rows / 2);
+    if (nb < 1) return false;
+    const int hmax = (h->rows + nb - 1) / nb;
+    int kw = 1;
+    while (kw < hmax + 4) kw <<= 1;
+    const int64_t bytes = golk::pipe_lds_bytes(h->Ww, kw);
+    if (bytes > 160 * 1024 - 256) return false;
+    const int slot = wpl == 4 ? 2 : wpl - 1;
+    int &bpc = h->pipe_bpc[slot];
+    if (bpc == 0 || h->pipe_bpc_bytes[slot] != bytes) {
+        bpc = std::max(0, golk::pipe_blocks_per_cu(wpl, bytes));
+        h->pipe_bpc_bytes[slot] = bytes;
+    }
+    if (bpc < 1 || (int64_t)nb > (int64_t)bpc * h->cu_count) return false;
+    if (out) {
+        out->Ww = h->Ww;
+        out->rows = h->rows;
+        out->nb = nb;
+        out->hmax = hmax;
+        out->kw = kw;
+        out->xcd = h->lds_xcd;
+    }
+    return true;
+}
+
+// Torus: the turns as K1t launches (one unless past golk::kResidentMaxTurns),
+// under the step guard like K1r / K1p; returns the turns run (0: K1t does
+// not apply).
+int64_t try_pipe(golhip_t h, int64_t left, bool count_last, int *rc) {
+    *rc = GOLHIP_OK;
+    if (left < 1) return 0;
+    const int wpl = h->il == 0 ? 1 : h->il;
+    golk::PipeArgs p{};
+    if (!pipe_fits(h, wpl, &p)) return 0;
+    const int64_t run = golk::resident_turns(left);
+    const int64_t ew = golk::pipe_edge_words(p.nb, p.Ww);
+    const int64_t sw = 1 + p.nb;  // error, econs[nb]
+    if (ew > h->pipe_edge_cap || sw > h->pipe_sync_cap) {
+        if (hipFree(h->pipe_edge) != hipSuccess || hipFree(h->pipe_sync) != hipSuccess) {
+            *rc = fail(GOLHIP_EHIP, "hipFree (K1t buffers)");
+            return 0;
+        }
+        h->pipe_edge = nullptr;
+        h->pipe_sync = nullptr;
+        h->pipe_edge_cap = h->pipe_sync_cap = 0;
+        if (hipMalloc(&h->pipe_edge, (size_t)ew * 4) != hipSuccess ||
+            hipMalloc(&h->pipe_sync, (size_t)sw * 4) != hipSuccess) {
+            (void)hipFree(h->pipe_edge);
+            h->pipe_edge = nullptr;
+            h->pipe_sync = nullptr;
+            return 0;
+        }
+        h->pipe_edge_cap = ew;
+        h->pipe_sync_cap = sw;
+        h->pipe_tag_base = 0;  // a fresh buffer: zero it before use
+    }
+    if (!h->h_err) {
+        if (hipHostMalloc(&h->h_err, sizeof(unsigned), hipHostMallocDefault) != hipSuccess) {
+            h->h_err = nullptr;
+            *rc = fail(GOLHIP_ENOMEM, "resident error word");
+            return 0;
+        }
+        *h->h_err = 0;
+    }
+    if (!take_guard(h, rc)) return 0;
+    const bool count = count_last && run == left;
+    hipError_t e = count ? hipMemsetAsync(h->d_scalars, 0, sizeof(unsigned long long), h->stream) : hipSuccess;
+    if (e == hipSuccess) e = hipMemsetAsync(h->pipe_sync, 0, (size_t)sw * 4, h->stream);
+    p.src = h->cur_rows();
+    p.dst = h->prev_rows();
+    p.edge = h->pipe_edge;
+    p.error = h->pipe_sync;
+    p.econs = h->pipe_sync + 1;
+    // edge tags: this launch's are above every tag already in the buffer
+    // (turn numbers restart at 1 each launch); on a wrap the buffer is zeroed
+    if ((uint64_t)h->pipe_tag_base + (uint64_t)run + 1 >= 0xFFFFFFFFull || h->pipe_tag_base == 0) {
+        if (e == hipSuccess) e = hipMemsetAsync(h->pipe_edge, 0, (size_t)h->pipe_edge_cap * 4, h->stream);
+        h->pipe_tag_base = 1;
+    }
+    p.tag_base = h->pipe_tag_base;
+    h->pipe_tag_base += (uint32_t)run + 1;
+    p.alive = count ? h->d_scalars : nullptr;
+    p.trace = h->d_trace;
+    p.timeout_ticks = h->persist_timeout_ticks;
+    p.turns = (int)run;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (e == hipSuccess && (h->flags & GOLHIP_FLAG_TIMING)) {
+        e0 = take_event(h);
+        e1 = take_event(h);
+        if (e0 && e1) e = hipEventRecord(e0, h->stream);
+    }
+    if (e == hipSuccess) e = golk::launch_pipe(p, wpl, h->stream);
+    if (e == hipSuccess && e1) {
+        e = hipEventRecord(e1, h->stream);
+        h->ev_pending.push_back({e0, e1, 1});
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(h->h_err, h->pipe_sync, sizeof(unsigned), hipMemcpyDeviceToHost, h->stream);
+    if (e != hipSuccess) {
+        *rc = fail(GOLHIP_EHIP, "resident LDS turn-pipeline launch: %s", hipGetErrorString(e));
+        return 0;
+    }
+    h->persist_pending = true;
+    h->cur ^= 1;
+    h->last_variant = 5;
+    h->turns += run;
+    h->persist_turns += run;
+    h->persist_launches++;
+    h->pipe_launches++;
+    if (count) h->alive_turn = h->turns;
+    return run;
 }
 
 // Torus: all `left` turns as one K1r launch (under the step guard, like
@@ -1191,7 +1229,6 @@ int64_t try_lds(golhip_t h, int64_t left, bool count_last, int *rc) {
         return 0;
     }
     h->persist_pending = true;
-    h->halo_ready = 0;
     h->cur ^= 1;
     h->last_variant = 4;
     h->turns += run;
@@ -1207,6 +1244,8 @@ int64_t try_lds(golhip_t h, int64_t left, bool count_last, int *rc) {
 int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     *rc = GOLHIP_OK;
     if (!persist_on(h) || h->W % 32 != 0 || !h->torus()) return 0;
+    if (int64_t n = try_pipe(h, left, count_last, rc)) return n;
+    if (*rc) return 0;
     if (int64_t n = try_lds(h, left, count_last, rc)) return n;
     if (*rc) return 0;
     const int wpl = wpl_for(h);
@@ -1578,7 +1617,10 @@ extern "C" {
 
 const char *golhip_version(void) { return "golhip 0.1 (gfx950)"; }
 
-const char *golhip_build_info(void) { return golk::build_info(); }
+const char *golhip_build_info(void) {
+    static const std::string info = std::string(golk::build_info()) + kConsentInfo;
+    return info.c_str();
+}
 
 const char *golhip_last_error(void) { return g_err.c_str(); }
 
@@ -1634,12 +1676,6 @@ int golhip_destroy(golhip_t h) {
     int rc = GOLHIP_OK;
     HIP_RC(hipSetDevice(h->device));
     if (h->stream) HIP_RC(hipStreamSynchronize(h->stream));
-    if (h->side) {
-        HIP_RC(hipStreamSynchronize(h->side));
-        HIP_RC(hipStreamDestroy(h->side));
-    }
-    if (h->ev_fork) HIP_RC(hipEventDestroy(h->ev_fork));
-    if (h->ev_x) HIP_RC(hipEventDestroy(h->ev_x));
     for (auto &p : h->ev_pending) {
         HIP_RC(hipEventDestroy(p.e0));
         HIP_RC(hipEventDestroy(p.e1));
@@ -1662,9 +1698,9 @@ int golhip_destroy(golhip_t h) {
     HIP_RC(hipFree(h->d_sync));
     HIP_RC(hipFree(h->d_trace));
     HIP_RC(hipFree(h->backup));
-    HIP_RC(hipFree(h->split_exp));
-    HIP_RC(hipFree(h->split_meet));
     HIP_RC(hipFree(h->lds_edge));
+    HIP_RC(hipFree(h->pipe_edge));
+    HIP_RC(hipFree(h->pipe_sync));
     if (h->h_err) HIP_RC(hipHostFree(h->h_err));
     if (h->skew_err) HIP_RC(hipHostFree(h->skew_err));
     if (h->own_stream && h->stream) HIP_RC(hipStreamDestroy(h->stream));
@@ -1728,11 +1764,6 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         h->persist_waves = (int)value;
         return GOLHIP_OK;
     }
-    if (!strcmp(key, "age_split")) {
-        if (value < -1 || value >= 100) return fail(GOLHIP_EINVAL, "age_split %lld", (long long)value);
-        h->age_split = (int)value;
-        return GOLHIP_OK;
-    }
     if (!strcmp(key, "dummy_rows")) {
         if (value < 0 || value > kHalo) return fail(GOLHIP_EINVAL, "dummy_rows %lld", (long long)value);
         h->dummy_rows = (int)value;
@@ -1776,6 +1807,8 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         if ((value & 3) && !measurement_env())
             return fail(GOLHIP_EINVAL, "flip_debug %lld gives wrong lists: measurement runs only (GOLHIP_MEASUREMENT=1)",
                         (long long)value);
+        if ((value & 4) && !test_hooks_env())
+            return fail(GOLHIP_EINVAL, "flip_debug 4 is a test hook (GOLHIP_TEST_HOOKS=1)");
         h->flip_debug = (int)value;
         return GOLHIP_OK;
     }
@@ -1787,11 +1820,6 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         if (value < 0 || value > h->dev_cu) return fail(GOLHIP_EINVAL, "cu_count %lld not in 0..%d", (long long)value, h->dev_cu);
         h->cu_count = value ? (int)value : h->dev_cu;
         for (int &c : h->auto_rpw) c = 0;
-        return GOLHIP_OK;
-    }
-    if (!strcmp(key, "overlap")) {
-        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "overlap %lld", (long long)value);
-        h->overlap = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "halo_skip")) {  // measurement only: the halo rows go stale (wrong results)
@@ -1831,11 +1859,6 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         h->skew_prio = (int)value;
         return GOLHIP_OK;
     }
-    if (!strcmp(key, "skew_nst")) {
-        if (value < 0 || value > 100000) return fail(GOLHIP_EINVAL, "skew_nst %lld", (long long)value);
-        h->skew_nst = (int)value;
-        return GOLHIP_OK;
-    }
     if (!strcmp(key, "skew_half")) {
         if (value < -1 || value > 1) return fail(GOLHIP_EINVAL, "skew_half %lld", (long long)value);
         h->skew_half = (int)value;
@@ -1849,6 +1872,11 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     if (!strcmp(key, "lds_band")) {
         if (value < -1 || value > 1) return fail(GOLHIP_EINVAL, "lds_band %lld", (long long)value);
         h->lds_band = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "lds_pipe")) {
+        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "lds_pipe %lld", (long long)value);
+        h->lds_pipe = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "lds_depth")) {
@@ -1873,12 +1901,9 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     }
     if (!strcmp(key, "resident_fault")) {
         if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "resident_fault %lld", (long long)value);
+        if (value && !test_hooks_env())
+            return fail(GOLHIP_EINVAL, "resident_fault is a test hook (GOLHIP_TEST_HOOKS=1)");
         h->resident_fault = (int)value;
-        return GOLHIP_OK;
-    }
-    if (!strcmp(key, "lds_split")) {
-        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "lds_split %lld", (long long)value);
-        h->lds_split = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "lds_stride")) {
@@ -1889,11 +1914,6 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     if (!strcmp(key, "lds_xcd")) {
         if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "lds_xcd %lld", (long long)value);
         h->lds_xcd = (int)value;
-        return GOLHIP_OK;
-    }
-    if (!strcmp(key, "split")) {
-        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "split %lld", (long long)value);
-        h->split = (int)value;
         return GOLHIP_OK;
     }
     return fail(GOLHIP_EINVAL, "unknown option %s", key);
@@ -2056,28 +2076,14 @@ int step_locked(golhip_t h, int64_t nturns, int32_t want_flips) {
         }
         const HaloRun hr = halo_next(depth_cap(h, true), sched_rows(h), persist_on(h), left - tail);
         const int d = hr.d, k = hr.k;
-        // the halos may have come with the previous round's last launch (overlap)
-        if (!(h->halo_ready >= k * d && h->halo_turn == h->turns))
-            if (int rc = exchange_rccl(h, k * d, h->stream)) return rc;
-        h->halo_ready = 0;
-        int prc = GOLHIP_OK;
+        if (int rc = exchange_rccl(h, k * d, h->stream)) return rc;
+            int prc = GOLHIP_OK;
         if (try_persist_halo(h, d, k, left - k * d == 0, &prc)) {
             left -= (int64_t)k * d;
             continue;
         }
         if (prc) return prc;
         for (int i = 0; i < k; ++i) {
-            const int64_t after = left - d;
-            if (i == k - 1 && h->overlap && after > tail && h->W % 32 == 0) {
-                // the next round's exchange rows (every rank plans alike)
-                const HaloRun nr = halo_next(depth_cap(h, true), sched_rows(h), persist_on(h), after - tail);
-                const int X = nr.k * nr.d;
-                if (h->rows >= 4 * X) {
-                    if (int rc = launch_overlap(h, d, X)) return rc;
-                    left = after;
-                    continue;
-                }
-            }
             if (int rc = launch_ext(h, d, left - d == 0, (k - 1 - i) * d)) return rc;
             left -= d;
         }
@@ -2106,8 +2112,9 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     // counters of this step, restored if a resident launch is abandoned below
     const int64_t persist_turns0 = h->persist_turns, persist_launches0 = h->persist_launches;
     const int64_t step_launches0 = h->step_launches, step_turns0 = h->step_turns;
-    const int64_t split_launches0 = h->split_launches, skew_launches0 = h->skew_launches;
+    const int64_t skew_launches0 = h->skew_launches;
     const int64_t skew_half_launches0 = h->skew_half_launches, lds_launches0 = h->lds_launches;
+    const int64_t pipe_launches0 = h->pipe_launches;
     const size_t ev0 = h->ev_pending.size();
     const int64_t halo_exchanges0 = h->halo_exchanges, halo_bytes0 = h->halo_bytes;
     int rc = step_locked(h, nturns, want_flips);
@@ -2132,10 +2139,10 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     h->persist_launches = persist_launches0;
     h->step_launches = step_launches0;
     h->step_turns = step_turns0;
-    h->split_launches = split_launches0;
     h->skew_launches = skew_launches0;
     h->skew_half_launches = skew_half_launches0;
     h->lds_launches = lds_launches0;
+    h->pipe_launches = pipe_launches0;
     h->halo_exchanges = halo_exchanges0;
     h->halo_bytes = halo_bytes0;
     if (h->ev_pending.size() >= ev0) {  // the abandoned attempt's launch timings (unless drained meanwhile)
@@ -2149,7 +2156,6 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
                                hipMemcpyDeviceToDevice, h->stream));
     h->cur = cur0;
     h->turns = turns0;
-    h->halo_ready = 0;
     h->alive_turn = -1;
     h->flips_valid = false;
     return step_locked(h, nturns, want_flips);
@@ -2462,7 +2468,7 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     memset(out, 0, sizeof *out);
     out->turns = h->turns;
     out->step_launches = h->step_launches;
-    out->split_launches = h->split_launches;
+    out->split_launches = 0;  // retired kernel families (round 5): the fields stay for the ABI
     out->step_turns = h->step_turns;
     out->step_kernel_ms = h->step_ms;
     out->persist_launches = h->persist_launches;
@@ -2483,9 +2489,10 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     out->skew_launches = h->skew_launches;
     out->halo_exchanges = h->halo_exchanges;
     out->halo_ms = h->halo_ms;
-    out->overlap_launches = h->overlap_launches;
+    out->overlap_launches = 0;
     out->skew_half_launches = h->skew_half_launches;
     out->lds_launches = h->lds_launches;
+    out->pipe_launches = h->pipe_launches;
     out->words_per_lane = h->W % 32 == 0 ? wpl_for(h) : 0;
     out->persist_depth = h->W % 32 == 0 ? persist_depth_for(h, wpl_for(h)) : 0;
     return GOLHIP_OK;
@@ -2521,15 +2528,15 @@ int golhip_perf_reset(golhip_t h) {
     if (int rc = set_dev(h)) return rc;
     if (int rc = drain_events(h)) return rc;
     h->step_ms = h->persist_ms = 0;
-    h->step_launches = h->step_turns = h->halo_bytes = h->split_launches = h->skew_launches = 0;
+    h->step_launches = h->step_turns = h->halo_bytes = h->skew_launches = 0;
     h->persist_launches = h->persist_turns = 0;
     h->flip_launches = h->flip_entries = 0;
     h->flip_ms = 0;
     h->halo_exchanges = 0;
     h->halo_ms = 0;
-    h->overlap_launches = 0;
     h->skew_half_launches = 0;
     h->lds_launches = 0;
+    h->pipe_launches = 0;
     return GOLHIP_OK;
 }
 

@@ -81,19 +81,19 @@ typedef struct golhip_perf {
     int32_t persist_depth;    /* turns per super-step of the resident kernel (its
                                  depths stop at 16 for two words per lane)       */
     int32_t reserved0;
-    int64_t split_launches;   /* of step_launches, those that ran split tiling
-                                 (gol_split_pair_kernel + gol_split_tri_kernel) */
+    int64_t split_launches;   /* always 0 (split tiling retired in round 5)     */
     int64_t skew_launches;    /* of step_launches, those that ran skewed band
                                  stacks (gol_skew_kernel, kernel_variant 3)     */
     int64_t halo_exchanges;   /* halo exchanges posted (RCCL ring)               */
     double halo_ms;           /* their summed time on the stream they ran on
                                  (GOLHIP_FLAG_TIMING)                           */
-    int64_t overlap_launches; /* step launches split into boundary rows + the next
-                                 exchange (side stream) and interior rows (option
-                                 "overlap")                                     */
+    int64_t overlap_launches; /* always 0 (option "overlap" retired in round 5)  */
     int64_t skew_half_launches; /* of skew_launches, those on half-wave tiles    */
     int64_t lds_launches;     /* of persist_launches, those that ran resident LDS
                                  bands (gol_lds_band_kernel, kernel_variant 4)  */
+    int64_t pipe_launches;    /* of persist_launches, those that ran the resident
+                                 LDS turn pipeline (gol_lds_pipe_kernel,
+                                 kernel_variant 5)                              */
 } golhip_perf_t;
 
 /* ---- library ---------------------------------------------------------- */
@@ -148,8 +148,7 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * a stack; "skew_half" (0 = when they need fewer wave-rows, 1 = whenever
  * possible, -1 = never): half-wave tiles (30 stored lanes each, two per
  * wave); "skew_prio" (0): s_setprio for the
- * younger waves; "split" (1): split tiling (gol_split_pair_kernel) for torus
- * steps when skew is off; "timing" (the GOLHIP_FLAG_TIMING flag after
+ * younger waves; "timing" (the GOLHIP_FLAG_TIMING flag after
  * creation: per-launch HIP events, ~5 us each); "persistent"
  * (default -1 = auto: off where the skewed band stacks fill the CUs, else on
  * for buffers of at most 64 MiB; 1 on, 0 off): resident multi-super-step kernel for long runs on a
@@ -161,21 +160,22 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * (0 = plan: 12, at most the rows): turns per LDS-band super-step; "lds_xcd"
  * (1): consecutive bands on one XCD; "lds_stride" (1): LDS rows at a
  * compile-time stride where one is instantiated; "lds_waves" (8 or 16) and
- * "lds_wg_cu" (1 or 2): waves per workgroup and bands per CU; "lds_split" (0):
- * full super-steps compute and publish their edge rows before the interior
- * (measured slower); "lds_pre" (2): a full super-step's
+ * "lds_wg_cu" (1 or 2): waves per workgroup and bands per CU; "lds_pre" (2): a full super-step's
  * first turns run on the rows that need no halo while the halos travel;
- * "resident_fault" (0, tests): the resident kernels' band / workgroup 0 never
- * reports, so its neighbours' bounded waits time out and the step is restored
- * and re-run;
+ * "lds_pipe" (default 0): 1 runs the resident LDS turn pipeline
+ * (gol_lds_pipe_kernel) on tori 2048, 4096 or 8192 cells wide whose bands fit
+ * one workgroup's LDS, under the resident guard (measured slower than the LDS
+ * bands);
+ * "resident_fault" (0, test hook: refused without GOLHIP_TEST_HOOKS=1): the
+ * resident kernels' band / workgroup 0 never reports, so its neighbours'
+ * bounded waits time out and the step is restored and re-run;
  * "persist_depth" (default 0 = tb_depth): turns per super-step;
  * "persist_half" (default 1): a remainder of half a super-step runs as the
  * resident kernel's last, half-depth super-step;
  * "persist_waves" (0 = auto, 8 or 16): waves per persistent workgroup;
  * "paired_bands" (default 1): the two waves of a SIMD stream one two-band
- * region from both ends and meet where they meet; "age_split" (-1 = auto,
- * 0 = equal, else %): static taller bands for the older waves when pairing
- * is off; "persist_wg_tx" (0 = plan): tiles across a persistent workgroup;
+ * region from both ends and meet where they meet (off: static taller bands
+ * for the older waves); "persist_wg_tx" (0 = plan): tiles across a persistent workgroup;
  * "dummy_rows" (0 = all halo rows): rows that absorb masked stores;
  * "trace" (0): persistent-kernel diagnostics (golhip_persist_trace);
  * "persist_timeout_us" (default 1000000): how long a resident workgroup waits
@@ -185,11 +185,10 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * multi-rank ring);
  * "force_halo" (0): after golhip_comm_init with one rank, run a whole board
  * through the multi-GPU path as a one-rank RCCL ring (tests, measurement);
- * "halo_skip" (0): measurement only, post no halo exchange (the halo rows go
- * stale: WRONG results; isolates the exchange's cost); "overlap" (0): in a
- * ring, the last launch before each exchange runs the rows the exchange sends
- * first, on a side stream followed by the exchange, while the interior rows
- * run on the engine stream (results identical). */
+ * "halo_skip" (0): measurement only, refused without GOLHIP_MEASUREMENT=1,
+ * post no halo exchange (the halo rows go stale: WRONG results; isolates the
+ * exchange's cost).  Retired in round 5 (refused as unknown keys): "split",
+ * "lds_split", "skew_nst", "age_split", "overlap". */
 int golhip_set_option(golhip_t h, const char *key, int64_t value);
 
 /* ---- multi-GPU -------------------------------------------------------- */

@@ -2,7 +2,7 @@
 # and SQ counter passes of one 8192^2 run.  usage: bash scripts/gpu_lds_probe.sh <tag> [sets]
 set -o pipefail
 tag=${1:-lds}
-sets=${2:-"lds_depth=8;lds_depth=12;lds_depth=4,lds_split=1;lds_depth=6,lds_split=1;lds_depth=8,lds_split=1"}
+sets=${2:-"lds_depth=8;lds_depth=12"}
 mkdir -p gpurun_out/$tag
 echo "== lds tests $(date +%T)"
 timeout -k 10 300 python -u -m pytest tests/test_gpu_lds.py -x -q --timeout 120 --timeout-method thread > gpurun_out/$tag/pytest_lds.log 2>&1; rc=$?

@@ -22,7 +22,7 @@ ap.add_argument("--rows", type=int, default=0, help="board height (0 = square)")
 a = ap.parse_args()
 variants = [v for v in a.variants.split(";") if v] or [""]
 # engine options are sticky on a handle: every variant starts from the defaults
-DEFAULTS = {"wpl": 0, "persistent": -1, "persist_depth": 0, "persist_waves": 0, "persist_wg_tx": 0, "dummy_rows": 0, "age_split": -1, "paired_bands": 1,
+DEFAULTS = {"wpl": 0, "persistent": -1, "persist_depth": 0, "persist_waves": 0, "persist_wg_tx": 0, "dummy_rows": 0, "paired_bands": 1,
             "fill_skip": 1}
 for N in map(int, a.sizes.split(",")):
     H = a.rows or N

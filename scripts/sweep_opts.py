@@ -58,7 +58,7 @@ for rep in range(a.reps):
                 best[key] = max(best.get(key, 0), g)
                 print(json.dumps({"case": case, "opts": opts, "lib": os.path.basename(golhip.LIB_PATH), "rep": rep, "gcups": round(g, 1),
                                   "launch_ms": round(p["step_kernel_ms"] / max(1, p["step_launches"]), 5),
-                                  "skew": p["skew_launches"], "split": p["split_launches"],
+                                  "skew": p["skew_launches"],
                                   "launches": p["step_launches"], "persist": p["persist_launches"],
                                   "exchanges": p["halo_exchanges"],
                                   "exchange_ms": round(p["halo_ms"] / max(1, p["halo_exchanges"]), 5)}), flush=True)

@@ -29,3 +29,10 @@ def fixtures():
 def manifest():
     with open(os.path.join(GOLDEN, "manifest.json")) as f:
         return json.load(f)
+
+
+@pytest.fixture
+def test_hooks(monkeypatch):
+    """Consent for the library's test hooks (resident_fault, flip_debug 4):
+    GOLHIP_TEST_HOOKS=1 for this test only."""
+    monkeypatch.setenv("GOLHIP_TEST_HOOKS", "1")

@@ -177,6 +177,7 @@ def test_flip_stream_dense_blocks(coracle):
 
 
 @pytest.mark.parametrize("fmt", [0, 1])
+@pytest.mark.usefixtures("test_hooks")
 def test_flip_stream_coresidency_fallback(fixtures, coracle, fmt):
     """A batch whose blockIdx-ordered prefix sums report a missing
     predecessor (forced by the test hook flip_debug 4) is restored and re-run
@@ -224,6 +225,7 @@ def test_step_flips_truncates_and_advances(fixtures):
 # ------------------------------------------------------------ resident-kernel guard
 @pytest.mark.parametrize("N,depth,wpl", [(4096, 16, 1), (2048, 8, 2)])
 @pytest.mark.parametrize("lds", [0, 1])
+@pytest.mark.usefixtures("test_hooks")
 def test_persistent_timeout_restores_and_reruns(coracle, N, depth, wpl, lds):
     """A resident launch (K1p, or K1r's LDS bands) whose workgroups give up
     waiting (a 1 us bound stands in for a co-tenant kernel holding CUs) is
@@ -253,6 +255,7 @@ def test_persistent_timeout_restores_and_reruns(coracle, N, depth, wpl, lds):
 
 
 @pytest.mark.parametrize("timeout_us", [1000000, 1])
+@pytest.mark.usefixtures("test_hooks")
 def test_persistent_timeout_one_rank_ring(coracle, timeout_us):  # 1: workgroup 0 never reports (test hook)
     """A strip run as a one-rank RCCL ring (force_halo) with the resident
     kernel between exchanges: the step is guarded like a torus step, so a

@@ -83,12 +83,12 @@ def test_config1_16384_10k_turns(full, opts):
 
 
 # ---------------------------------------------------------------- configs[2]
-@pytest.mark.parametrize("opts", [{}, {"skew": 0}, {"skew": 0, "split": 0}, {"tb_depth": 16}, {"wpl": 4},
+@pytest.mark.parametrize("opts", [{}, {"skew": 0}, {"tb_depth": 16}, {"wpl": 4},
                                   {"persistent": 1}, {"wpl": 1, "tb_depth": 32}, {"skew_tx": 2},
                                   {"skew_young": 70, "skew_prio": 1}])
 def test_config2_65536_1k_turns(full, opts):
     """configs[2]: 65536^2, 1,000 turns (default: skewed band stacks, 20-turn launches;
-    skew 0: split tiling; skew 0 split 0: the overlapped paired-band kernel)."""
+    skew 0: the overlapped paired-band kernel)."""
     run_checkpoints(full, "c2", **opts)
 
 
@@ -117,10 +117,9 @@ def test_config2_strips_in_process(full, nstrips):
             s.close()
 
 
-@pytest.mark.parametrize("persistent,overlap", [(-1, 0), (1, 0), (0, 0), (-1, 1)])
-def test_config2_rccl_ring_one_rank(full, persistent, overlap):
-    """configs[2] through the RCCL halo path (a one-rank ring, deep halos;
-    overlap: boundary rows + exchange on a side stream)."""
+@pytest.mark.parametrize("persistent", [-1, 1, 0])
+def test_config2_rccl_ring_one_rank(full, persistent):
+    """configs[2] through the RCCL halo path (a one-rank ring, deep halos)."""
     js, rows = full
     rec = js["c2"]
     N = rec["width"]
@@ -128,7 +127,6 @@ def test_config2_rccl_ring_one_rank(full, persistent, overlap):
         b.comm_init(golhip.unique_id(), 1, 0)
         b.set_option("force_halo", 1)
         b.set_option("persistent", persistent)
-        b.set_option("overlap", overlap)
         if persistent == 0:
             b.set_option("skew", 0)
         b.fill_random(rec["seed"])

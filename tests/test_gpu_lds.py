@@ -137,24 +137,6 @@ def test_lds_band_variants(coracle, W, H, opts):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("wpl", [1, 2])
-@pytest.mark.parametrize("depth", [1, 2, 3, 4, 5, 8, 12])
-@pytest.mark.parametrize("W,H", [(1024, 1024), (2048, 1003), (8192, 8192), (5120, 5120), (640, 384)])
-def test_lds_band_split_matches_oracle(coracle, wpl, depth, W, H):
-    """Boundary-first super-steps (option lds_split): the edge rows' D turns
-    first, their publish, then the interior while they travel.  Bands of
-    4D - 2 rows and more split cleanly; shorter ones compute the overlap of
-    the two edge regions twice (same values) and have no interior."""
-    if W * H > 2048 * 2048 and depth not in (3, 5, 8):
-        pytest.skip("large boards at a few depths")
-    board = coracle.fill_random(W, H, 0x5EED0047 + W + H + depth)
-    turns = 3 * depth + 2  # two full super-steps and a short one
-    want = coracle.run(board, turns)
-    got, p = run_lds(board, turns, depth, wpl, lds_split=1)
-    assert p["lds_launches"] == 1
-    assert np.array_equal(got, want)
-
-
 @pytest.mark.parametrize("W,H", [(128, 3), (128, 5), (256, 4), (256, 13), (384, 12), (128, 1000)])
 def test_lds_band_tiny_boards(coracle, W, H):
     """Rows of 2-6 pairs (many runs a wave, neighbours across the row's wrap in
@@ -172,8 +154,8 @@ def test_lds_band_tiny_boards(coracle, W, H):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("split", [0, 1])
-def test_lds_band_wait_timeout(coracle, split):
+@pytest.mark.usefixtures("test_hooks")
+def test_lds_band_wait_timeout(coracle):
     """Band 0 never publishes its edges (test hook resident_fault): its neighbours'
     flag waits reach the bound, every workgroup drains, and the step is
     restored and re-run on the per-launch kernels, exactly."""
@@ -181,7 +163,6 @@ def test_lds_band_wait_timeout(coracle, split):
     want = coracle.run(board, 51)
     with golhip.Board(2048, 1024) as b:
         b.set_option("persistent", 1)
-        b.set_option("lds_split", split)
         b.set_option("resident_fault", 1)
         b.set_option("lds_depth", 8)
         b.set_option("persist_timeout_us", 2000)
@@ -237,6 +218,7 @@ def test_lds_band_interior_first(coracle, pre, W, H, depth):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.usefixtures("test_hooks")
 def test_lds_band_interior_first_timeout(coracle):
     board = coracle.fill_random(2048, 1024, 0x5EED004D)
     want = coracle.run(board, 51)

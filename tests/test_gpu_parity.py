@@ -593,12 +593,12 @@ def test_rccl_halo_ring_full_size():
     assert res[0] == res[1] == res[2]
 
 
-@pytest.mark.parametrize("N,depth,wpl,nw,split,tx", [(2048, 16, 1, 8, 70, 1), (4096, 16, 2, 8, 80, 1),
-                                                     (2048, 8, 1, 16, 65, 1), (3968, 16, 1, 8, 75, 1),
-                                                     (4096, 16, 1, 8, 65, 2), (4096, 16, 2, 8, 60, 4),
-                                                     (3968, 8, 1, 16, 65, 4), (2048, 16, 1, 8, 65, 8)])
-def test_persistent_unequal_bands(coracle, N, depth, wpl, nw, split, tx):
-    """Persistent kernel with static taller bands for the oldest waves (age_split) vs the C oracle."""
+@pytest.mark.parametrize("N,depth,wpl,nw,tx", [(2048, 16, 1, 8, 1), (4096, 16, 2, 8, 1), (2048, 8, 1, 16, 1),
+                                              (3968, 16, 1, 8, 1), (4096, 16, 1, 8, 2), (4096, 16, 2, 8, 4),
+                                              (3968, 8, 1, 16, 4), (2048, 16, 1, 8, 8)])
+def test_persistent_unequal_bands(coracle, N, depth, wpl, nw, tx):
+    """Persistent kernel without pairing (paired_bands 0): static taller bands
+    for the oldest waves (65 % of the rows at 8 waves, equal at 16) vs the C oracle."""
     board = coracle.fill_random(N, N // 2, 0x5EED000F)
     turns = 4 * depth + 1
     want = coracle.run(board, turns)
@@ -606,7 +606,6 @@ def test_persistent_unequal_bands(coracle, N, depth, wpl, nw, split, tx):
         b.set_option("wpl", wpl)
         b.set_option("persist_waves", nw)
         b.set_option("paired_bands", 0)
-        b.set_option("age_split", split)
         b.set_option("persist_wg_tx", tx)
         b.set_option("persistent", 1)
         b.set_option("lds_band", 0)  # K1p itself (K1r: tests/test_gpu_lds.py)
@@ -670,11 +669,20 @@ def test_wrong_result_options_need_measurement_consent(monkeypatch):
     flip_debug 1-3) are refused unless GOLHIP_MEASUREMENT=1; the exact ones
     (flip_debug 4, the co-residency test hook) stay allowed."""
     monkeypatch.delenv("GOLHIP_MEASUREMENT", raising=False)
+    monkeypatch.delenv("GOLHIP_TEST_HOOKS", raising=False)
     with golhip.Board(64, 64) as b:
         for k, v in (("halo_skip", 1), ("flip_debug", 1), ("flip_debug", 3)):
             with pytest.raises(golhip.GolHipError, match="GOLHIP_MEASUREMENT"):
                 b.set_option(k, v)
+        # test hooks (exact results, forced failure paths): GOLHIP_TEST_HOOKS=1 (VERDICT r4 item 7)
+        for k, v in (("resident_fault", 1), ("flip_debug", 4)):
+            with pytest.raises(golhip.GolHipError, match="GOLHIP_TEST_HOOKS"):
+                b.set_option(k, v)
+        b.set_option("resident_fault", 0)
+        monkeypatch.setenv("GOLHIP_TEST_HOOKS", "1")
         b.set_option("flip_debug", 4)
+        b.set_option("resident_fault", 1)
+        b.set_option("resident_fault", 0)
         b.set_option("halo_skip", 0)
         monkeypatch.setenv("GOLHIP_MEASUREMENT", "1")
         b.set_option("halo_skip", 1)

@@ -115,33 +115,6 @@ def test_skew_rccl_ring_one_rank(coracle, depth, wpl, W, H):
         assert b.alive_count() == (int((want == 255).sum()), turns)
 
 
-@pytest.mark.parametrize("depth,wpl,W,H,turns", [(20, 2, 4096, 1500, 300), (9, 4, 4096, 1500, 300),
-                                                  (16, 1, 2048, 4096, 257), (8, 2, 2048, 4096, 257),
-                                                  (20, 2, 8192, 1000, 123), (9, 4, 8192, 1000, 123)])
-def test_overlap_rccl_ring_one_rank(coracle, depth, wpl, W, H, turns):
-    """Option "overlap": the last launch of each exchange round in three
-    parts (boundary rows on a side stream, then the next exchange there;
-    interior rows on the engine stream); results identical to the oracle."""
-    board = coracle.fill_random(W, H, 0x5EED0036 + W + depth)
-    want = coracle.run(board, turns)
-    with golhip.Board(W, H) as b:
-        b.comm_init(golhip.unique_id(), 1, 0)
-        b.set_option("force_halo", 1)
-        b.set_option("persistent", 0)  # (overlap splits per-launch rounds; small rings may run K1p)
-        b.set_option("overlap", 1)
-        b.set_option("wpl", wpl)
-        b.set_tb_depth(depth)
-        b.load_bytes(board)
-        b.step(turns)
-        p = b.perf()
-        assert p["overlap_launches"] >= 1 and p["halo_exchanges"] >= 2
-        assert np.array_equal(b.snapshot_bytes(), want)
-        assert b.alive_count() == (int((want == 255).sum()), turns)
-        b.step(depth + 1, want_flips=True)  # a short call after an overlapped round
-        want2 = coracle.run(want, depth + 1)
-        assert np.array_equal(b.snapshot_bytes(), want2)
-
-
 @pytest.mark.parametrize("nstrips", [2, 3, 5])
 @pytest.mark.parametrize("depth,wpl", [(20, 2), (9, 4)])
 def test_skew_group_strips(coracle, nstrips, depth, wpl):

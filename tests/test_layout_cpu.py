@@ -23,10 +23,8 @@ def disasm():
 
 
 @pytest.mark.parametrize("kernel", [
-    "gol_split_pair_kernelILi20ELi2E",       # K1s A at 65536^2 (option skew 0)
-    "gol_split_pair_kernelILi8ELi4E",        # configs[3]: 262144^2
     "gol_persist_kernelILi16ELi2ELi8E",      # configs[1]: 16384^2 resident
-    "gol_tb_pair_kernelILi20ELi2ELb0E",      # the paired-band kernel (split off, strips)
+    "gol_tb_pair_kernelILi20ELi2ELb0E",      # the paired-band kernel (skew off)
 ])
 def test_main_loop_on_fast_parity(disasm, kernel):
     import loop_parity

@@ -1,4 +1,4 @@
-"""The bit-sliced B3/S23 circuit of the step kernels (gol_kernels.hip `stage`),
+"""The bit-sliced B3/S23 circuit of the step kernels (gol_kernels.hip `stage`, LUTs in gol_bits.h),
 emulated with the same v_bitop3_b32 truth tables, against the reference rule
 (distributor.go:350-379 calculateNextState, :382-417 checkNeighbour) on all
 512 3x3 neighbourhoods.  CPU only: this pins the LUT constants the kernel
@@ -9,7 +9,7 @@ import os
 import re
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = os.path.join(ROOT, "game-of-life-distributed_amd", "csrc", "gol_kernels.hip")
+KERNELS = os.path.join(ROOT, "game-of-life-distributed_amd", "csrc", "gol_bits.h")  # the LUTs the kernels share
 
 
 def bitop3(lut: int, a: int, b: int, c: int) -> int:
@@ -28,7 +28,7 @@ def kernel_luts() -> dict:
     src = open(KERNELS).read()
     m = re.search(r"static_assert\(kG1 == (0x[0-9a-fA-F]+) && kG2 == (0x[0-9a-fA-F]+) && kNext == (0x[0-9a-fA-F]+)",
                   src)
-    assert m, "rule LUT static_assert not found in gol_kernels.hip"
+    assert m, "rule LUT static_assert not found in gol_bits.h"
     return {"g1": int(m.group(1), 16), "g2": int(m.group(2), 16), "next": int(m.group(3), 16)}
 
 
