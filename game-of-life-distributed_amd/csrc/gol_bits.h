@@ -89,4 +89,17 @@ struct LdsRow {
 typedef unsigned v4u32 __attribute__((ext_vector_type(4)));
 constexpr int kCpolSc1 = 16;  // buffer load/store aux bit: sc1 (write-through store, L1-bypassing load)
 
+// LDS words read / written as relaxed workgroup-scope atomics through an
+// address-space-3 pointer: plain ds_read_b32 / ds_write_b32 at immediate
+// offsets that the compiler neither caches in registers, nor turns into flat
+// accesses, nor merges into ds_read2 / ds_write2 (whose 8-bit offsets cost a
+// VALU address add per row once rows are more than 1 KB apart)
+typedef __attribute__((address_space(3))) uint32_t lds_word;
+__device__ __forceinline__ uint32_t lds_get(const lds_word *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_put(lds_word *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 }  // namespace golk

@@ -132,16 +132,17 @@ struct LdsBandArgs {
     int hmax;              // ceil(rows / nb)
     int xcd;               // 1: consecutive bands on one XCD (nb % 8 == 0)
     int nt;                // threads per workgroup: 512 or 1024
-    int stride;            // LDS words per row: lds_band_stride (>= Ww)
+    int stride;            // LDS words per row: lds_band_stride (Ww; pairs Ww + 8, two planes)
+    int rt_stride;         // 1: the runtime-stride kernel even where this stride is instantiated
     int fault;             // tests: band 0 never publishes, so its neighbours' waits time out
     int pre;               // > 0: full super-steps run their first `pre` turns on the interior rows
                            //      while the halos travel (lds_pre)
     unsigned long long *trace;  // nullable: [0..3] += ticks in compute, publish, wait, halo load; [4] += workgroups
 };
-__host__ __device__ inline int64_t lds_band_edge_words(int nb, int D, int Ww) { return 4ll * nb * D * Ww; }
+__host__ __device__ inline int64_t lds_band_edge_words(int nb, int D, int stride) { return 4ll * nb * D * stride; }
 inline int64_t lds_band_lds_bytes(int hmax, int D, int stride) { return 2ll * (hmax + 2 * D + 3) * stride * 4; }
 // Resident workgroups per CU at that LDS size (0: does not fit).
-// The LDS row stride for Ww-word rows: an instantiated compile-time stride >= Ww, else Ww.
+// The LDS row stride for Ww-word rows: Ww, pairs Ww + 8 (two planes with a ghost word each).
 int lds_band_stride(int Ww, int wpl, int nt);
 int lds_band_blocks_per_cu(int wpl, int nt, int stride, int64_t lds_bytes);
 hipError_t launch_lds_band(const LdsBandArgs &p, int wpl, hipStream_t s);

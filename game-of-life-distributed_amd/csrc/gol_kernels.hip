@@ -1338,10 +1338,19 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
 // then sc1 buffer loads), no cache-wide fence.  The edge buffers alternate
 // by super-step parity: the wait for a neighbour's super-step j flag also
 // proves it read our j - 1 edges, which the slot we overwrite held.
-// Per row and word: three LDS loads (own word or pair, one neighbour word
-// each side), the row sums (2 LUTs, and a funnel shift per pair side), the
+// Per row and word: the lane's word (pair) and one neighbour word each side
+// from LDS, the row sums (2 LUTs, and a funnel shift per pair side), the
 // column sums and the rule (7 LUTs), one LDS store; each buffer has 3 spare
 // rows for the row loop's prefetch.  Every wait is bounded (error word, all drain).
+// Pairs (WPL 2) sit in LDS as two planes (round 5): a row of LS = Ww + 8
+// words holds the even-cell words E[c] at [0, P) and the odd-cell words O[c]
+// at [PO + 1, PO + 1 + P), PO = LS / 2, with one ghost word each for the
+// column wrap: E[P] (= E[0]) at P and O[-1] (= O[P - 1]) at PO.  A lane's
+// four words E[c], E[c + 1], O[c - 1], O[c] are then two ds_read2_b32 of
+// consecutive words across the lanes (the interleaved layout's odd-word
+// reads were 2-way bank conflicts: 33 % of LDS cycles, profiles/r4k1rfinal),
+// and its store one ds_write2_b32 plus the ghost store (the lanes of
+// columns 0 and P - 1 write the ghosts, the others rewrite their E[c]).
 // ---------------------------------------------------------------------------
 // A row's words as loaded: the lane's own word (pair) and one neighbour word on each side.
 template <int WPL>
@@ -1355,18 +1364,22 @@ struct LdsRaw {
 // theirs, saved the 2-way bank conflicts of every-second-word reads but ran
 // 8192^2 at 24-26 instead of 31-32 TCUPS: load -> DPP -> alignbit is a longer
 // dependent chain at two waves per SIMD; profiles/r4o.)
+// WPL 1: o, ol, orr are the lane's word and its neighbours'; WPL 2 (planes):
+// o = c, and po the plane offset (compile-time where the stride is).
 template <int WPL>
-__device__ __forceinline__ LdsRaw<WPL> lds_load(const uint32_t *row, int o, int ol, int orr) {
+__device__ __forceinline__ LdsRaw<WPL> lds_load(const uint32_t *row, int o, int ol, int orr, int po) {
     LdsRaw<WPL> x;
     if constexpr (WPL == 1) {
         x.c[0] = row[o];
+        x.l = row[ol];   // the left word
+        x.r = row[orr];  // the right word
     } else {
-        const uint2 v = *reinterpret_cast<const uint2 *>(row + o);
-        x.c[0] = v.x;
-        x.c[1] = v.y;
+        const lds_word *r = (const lds_word *)(row + o);
+        x.c[0] = lds_get(r);           // E[c]
+        x.r = lds_get(r + 1);          // E[c + 1]: the right pair's even cells (bit 0 = its cell 0)
+        x.l = lds_get(r + po);         // O[c - 1]: the left pair's odd cells (bit 31 = its cell 63)
+        x.c[1] = lds_get(r + po + 1);  // O[c]
     }
-    x.l = row[ol];   // wpl 1: the left word; 2: the left pair's odd cells (bit 31 = its cell 63)
-    x.r = row[orr];  // wpl 1: the right word; 2: the right pair's even cells (bit 0 = its cell 0)
     return x;
 }
 
@@ -1398,7 +1411,11 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
     extern __shared__ uint4 lds_band_smem[];
     uint32_t *const L0 = reinterpret_cast<uint32_t *>(lds_band_smem);
     const int Ww = p.Ww, D = p.D, nb = p.nb;
-    const int LS = S > 0 ? S : Ww;  // LDS row stride (words)
+    const int LS = S > 0 ? S : p.stride;  // LDS row stride (words)
+    const int PO = LS / 2;                // WPL 2: the odd plane's offset (ghost O[-1] at PO)
+    // pairs at an instantiated stride: the pairs per row at compile time (the
+    // stride is exactly Ww + 8), so a wave's runs are uniform when they fill it
+    constexpr int PC = (S > 0 && WPL == 2) ? (S - 8) / 2 : 0;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // blocks are dealt round-robin over the 8 XCDs: give each XCD a run of
@@ -1413,23 +1430,39 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
     __shared__ int s_abort;
     if (threadIdx.x == 0) s_abort = 0;
 
+    const int P = PC > 0 ? PC : Ww / WPL;  // words (wpl 1) or pairs per row
     // generation 0: board rows r0 - D .. r0 + h + D - 1 (mod rows), 16-B words
+    // (pairs: 8-B pairs into the two planes and their ghosts)
     const int q4 = Ww / 4;
-    for (int i = threadIdx.x; i < R * q4; i += NT) {
-        const int r = i / q4, c = i - r * q4;
-        int br = r0 - D + r;
-        br = ((br % p.rows) + p.rows) % p.rows;
-        reinterpret_cast<uint4 *>(A + (size_t)r * LS)[c] = reinterpret_cast<const uint4 *>(p.src + (size_t)br * Ww)[c];
+    if constexpr (WPL == 1) {
+        for (int i = threadIdx.x; i < R * q4; i += NT) {
+            const int r = i / q4, c = i - r * q4;
+            int br = r0 - D + r;
+            br = ((br % p.rows) + p.rows) % p.rows;
+            reinterpret_cast<uint4 *>(A + (size_t)r * LS)[c] = reinterpret_cast<const uint4 *>(p.src + (size_t)br * Ww)[c];
+        }
+    } else {
+        for (int i = threadIdx.x; i < R * P; i += NT) {
+            const int r = i / P, c = i - r * P;
+            int br = r0 - D + r;
+            br = ((br % p.rows) + p.rows) % p.rows;
+            const uint2 v = reinterpret_cast<const uint2 *>(p.src + (size_t)br * Ww)[c];
+            uint32_t *row = A + (size_t)r * LS;
+            row[c] = v.x;
+            row[PO + 1 + c] = v.y;
+            if (c == 0) row[P] = v.x;
+            if (c == P - 1) row[PO] = v.y;
+        }
     }
     __syncthreads();
 
     const __amdgpu_buffer_rsrc_t ers = __builtin_amdgcn_make_buffer_rsrc(
-        p.edge, (short)0, (int)(lds_band_edge_words(nb, D, Ww) * 4), 0x00020000);
-    const int P = Ww / WPL;               // words (wpl 1) or pairs per row
+        p.edge, (short)0, (int)(lds_band_edge_words(nb, D, LS) * 4), 0x00020000);
     const int K = max(1, NT / P);        // row runs per column
     const int units = P * K;
     const int J = (int)(((int64_t)p.turns + D - 1) / D);  // turns <= kResidentMaxTurns (gol_limits.h)
-    const int eq4 = D * q4;               // 16-B granules of one edge side
+    const int rq4 = WPL == 1 ? q4 : LS / 4;  // 16-B granules of an edge row (pairs: the whole LDS row)
+    const int eq4 = D * rq4;                 // 16-B granules of one edge side
     // diagnostics (option "trace"): s_memrealtime ticks summed over the
     // workgroups in compute, publish, neighbour wait and halo load
     long long tr[4] = {0, 0, 0, 0}, tr_t = p.trace ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
@@ -1448,50 +1481,70 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
         // of those rows from Ab into Bb.
         auto run_rows = [&](const uint32_t *Ab, uint32_t *Bb, int lo, int hi, int c) {
             const int cl = c == 0 ? P - 1 : c - 1, cr = c == P - 1 ? 0 : c + 1;
-            const int o = WPL * c, ol = WPL == 1 ? cl : 2 * cl + 1, orr = WPL * cr;
-            // rows r - 1, r, r + 1 in s[(q + 0..2) % 3]; the words of rows r + 1 and
-            // r + 2 already loaded (n1, n2) while row r is computed: the LDS
-            // latency hides behind a row's rule (two waves per SIMD hide little)
-            // the raw words of row r0 + q + 1 in x[q], of r0 + q + 2 in x[q + 1]
-            // (in flight); row r0 + q + 3 goes to x[q + 2] (indices mod 3, all
-            // static in the unrolled body: no register copies, no early waits).
-            // Rows past R - 1 land in the buffer's 3 spare rows (never used).
-            LdsRow<WPL> s[3];
-            LdsRaw<WPL> x[3];
-            lds_sums<WPL>(lds_load<WPL>(Ab + (lo - 1) * LS, o, ol, orr), s[0]);
-            lds_sums<WPL>(lds_load<WPL>(Ab + lo * LS, o, ol, orr), s[1]);
-            x[0] = lds_load<WPL>(Ab + (lo + 1) * LS, o, ol, orr);
-            x[1] = lds_load<WPL>(Ab + (lo + 2) * LS, o, ol, orr);
-            const uint32_t *ld = Ab + (lo + 3) * LS;
-            uint32_t *st = Bb + lo * LS + o;
-            // one row of the rotation (q static): its sums from the prefetched words,
-            // the prefetch of row r + 3, the rule, the store
-            auto row = [&](auto qc) {
-                constexpr int q = decltype(qc)::value;
-                lds_sums<WPL>(x[q], s[(q + 2) % 3]);
-                x[(q + 2) % 3] = lds_load<WPL>(ld + q * LS, o, ol, orr);
-                const LdsRow<WPL> &a = s[q % 3], &b = s[(q + 1) % 3], &n = s[(q + 2) % 3];
+            const int o = c, ol = cl, orr = cr;  // (pairs: ol, orr unused, the ghosts wrap)
+            // pairs: the ghost store's word (E[P] for column 0, O[-1] for P - 1, else E[c] again)
+            const int goff = c == 0 ? P : c == P - 1 ? PO : c;
+            const bool godd = c == P - 1;
+            // Loop-carried: the sums of rows r - 1, r, r + 1 (sa, sb, sc; computed,
+            // so carrying them needs no wait).  An iteration of three rows issues
+            // the loads of rows r + 2 .. r + 4 first, then computes row r, the
+            // sums of r + 2, row r + 1, the sums of r + 3, row r + 2, the sums of
+            // r + 4: each load is consumed one to three rows after it was issued
+            // and none crosses the back edge (a loaded word carried over it made
+            // the compiler wait for every load at the loop head).  Rows past
+            // R - 1 land in the buffer's 3 spare rows (never used).
+            auto rule_store = [&](const LdsRow<WPL> &a, const LdsRow<WPL> &b, const LdsRow<WPL> &n, uint32_t *st,
+                                  uint32_t *gst) {
                 uint32_t out[WPL];
 #pragma unroll
                 for (int m = 0; m < WPL; ++m)
                     out[m] = rule_word(a.s0[m], a.s1[m], b.s0[m], b.s1[m], n.s0[m], n.s1[m], b.c[m]);
-                if constexpr (WPL == 1)
-                    st[q * LS] = out[0];
-                else
-                    *reinterpret_cast<uint2 *>(st + q * LS) = make_uint2(out[0], out[1]);
+                if constexpr (WPL == 1) {
+                    *st = out[0];
+                } else {
+                    lds_put((lds_word *)st, out[0]);
+                    lds_put((lds_word *)(st + PO + 1), out[1]);
+                    lds_put((lds_word *)gst, godd ? out[1] : out[0]);
+                }
             };
-            // whole groups of three rows with no branch between them (the
-            // scheduler interleaves three independent rows), then at most two
-            int r0 = lo;
-            for (; r0 + 3 <= hi; r0 += 3) {
-                row(std::integral_constant<int, 0>{});
-                row(std::integral_constant<int, 1>{});
-                row(std::integral_constant<int, 2>{});
+            LdsRow<WPL> sa, sb, sc;
+            {
+                const LdsRaw<WPL> x0 = lds_load<WPL>(Ab + (lo - 1) * LS, o, ol, orr, PO);
+                const LdsRaw<WPL> x1 = lds_load<WPL>(Ab + lo * LS, o, ol, orr, PO);
+                const LdsRaw<WPL> x2 = lds_load<WPL>(Ab + (lo + 1) * LS, o, ol, orr, PO);
+                lds_sums<WPL>(x0, sa);
+                lds_sums<WPL>(x1, sb);
+                lds_sums<WPL>(x2, sc);
+            }
+            const uint32_t *ld = Ab + (lo + 2) * LS;
+            uint32_t *st = Bb + lo * LS + o;
+            uint32_t *gst = Bb + lo * LS + goff;
+            int r = lo;
+            for (; r + 3 <= hi; r += 3) {
+                const LdsRaw<WPL> x0 = lds_load<WPL>(ld, o, ol, orr, PO);
+                const LdsRaw<WPL> x1 = lds_load<WPL>(ld + LS, o, ol, orr, PO);
+                const LdsRaw<WPL> x2 = lds_load<WPL>(ld + 2 * LS, o, ol, orr, PO);
+                // the loads first, row r's rule behind them (it needs none of them)
+                __builtin_amdgcn_sched_barrier(0);
+                rule_store(sa, sb, sc, st, gst);
+                __builtin_amdgcn_sched_barrier(0);  // (and only then the first wait)
+                lds_sums<WPL>(x0, sa);
+                rule_store(sb, sc, sa, st + LS, gst + LS);
+                lds_sums<WPL>(x1, sb);
+                rule_store(sc, sa, sb, st + 2 * LS, gst + 2 * LS);
+                lds_sums<WPL>(x2, sc);
                 ld += 3 * LS;
                 st += 3 * LS;
+                gst += 3 * LS;
             }
-            if (r0 < hi) row(std::integral_constant<int, 0>{});
-            if (r0 + 1 < hi) row(std::integral_constant<int, 1>{});
+            if (r < hi) {
+                rule_store(sa, sb, sc, st, gst);
+                if (r + 1 < hi) {
+                    LdsRow<WPL> sd;
+                    lds_sums<WPL>(lds_load<WPL>(ld, o, ol, orr, PO), sd);
+                    rule_store(sb, sc, sd, st + LS, gst + LS);
+                }
+            }
         };
         // One turn over the rows [lo0, hi0) and [lo1, hi1) (either may be empty):
         // K runs per column over the two ranges laid end to end, then a barrier.
@@ -1499,7 +1552,10 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
             const int n0 = max(0, hi0 - lo0), n = n0 + max(0, hi1 - lo1);
             const int len = (n + K - 1) / K;
             for (int u = threadIdx.x; u < units; u += NT) {
-                const int k = u / P, c = u - k * P;
+                int k = u / P;
+                // a wave's lanes share k when whole waves fit a row: scalar run bounds
+                if constexpr (PC > 0 && PC % 64 == 0) k = __builtin_amdgcn_readfirstlane(k);
+                const int c = u - k * P;
                 const int v0 = k * len, v1 = min(v0 + len, n);
                 if (v0 >= v1) continue;
                 if (v0 < n0) run_rows(Ab, Bb, lo0 + v0, lo0 + min(v1, n0), c);
@@ -1517,7 +1573,7 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
             for (int i = threadIdx.x; i < 2 * eq4; i += NT) {
                 const bool top = i < eq4;
                 const int g = top ? i : i - eq4;
-                const uint4 v = *reinterpret_cast<const uint4 *>(F + (size_t)(top ? D : h) * LS + 4 * (g % q4) + (size_t)(g / q4) * LS);
+                const uint4 v = *reinterpret_cast<const uint4 *>(F + (size_t)(top ? D : h) * LS + 4 * (g % rq4) + (size_t)(g / rq4) * LS);
                 __builtin_amdgcn_raw_buffer_store_b128((v4u32){v.x, v.y, v.z, v.w}, ers,
                                                        e0 + (top ? 0 : eq4 * 16) + g * 16, 0, kCpolSc1);
             }
@@ -1562,7 +1618,7 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
                 const bool top = i < eq4;
                 const int g = top ? i : i - eq4;
                 const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(ers, (top ? eu : ed) + g * 16, 0, kCpolSc1);
-                uint32_t *dstw = A + (size_t)(top ? 0 : D + h) * LS + 4 * (g % q4) + (size_t)(g / q4) * LS;
+                uint32_t *dstw = A + (size_t)(top ? 0 : D + h) * LS + 4 * (g % rq4) + (size_t)(g / rq4) * LS;
                 *reinterpret_cast<uint4 *>(dstw) = make_uint4(v.x, v.y, v.z, v.w);
             }
             __syncthreads();
@@ -1635,11 +1691,21 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
     }
     // the band's last generation: rows [D, D + h) of A -> board rows [r0, r0 + h)
     uint32_t cnt = 0;
-    for (int i = threadIdx.x; i < h * q4; i += NT) {
-        const int r = i / q4, c = i - r * q4;
-        const uint4 v = reinterpret_cast<const uint4 *>(A + (size_t)(D + r) * LS)[c];
-        reinterpret_cast<uint4 *>(p.dst + (size_t)(r0 + r) * Ww)[c] = v;
-        cnt += __builtin_popcount(v.x) + __builtin_popcount(v.y) + __builtin_popcount(v.z) + __builtin_popcount(v.w);
+    if constexpr (WPL == 1) {
+        for (int i = threadIdx.x; i < h * q4; i += NT) {
+            const int r = i / q4, c = i - r * q4;
+            const uint4 v = reinterpret_cast<const uint4 *>(A + (size_t)(D + r) * LS)[c];
+            reinterpret_cast<uint4 *>(p.dst + (size_t)(r0 + r) * Ww)[c] = v;
+            cnt += __builtin_popcount(v.x) + __builtin_popcount(v.y) + __builtin_popcount(v.z) + __builtin_popcount(v.w);
+        }
+    } else {
+        for (int i = threadIdx.x; i < h * P; i += NT) {
+            const int r = i / P, c = i - r * P;
+            const uint32_t *row = A + (size_t)(D + r) * LS;
+            const uint2 v = make_uint2(row[c], row[PO + 1 + c]);
+            reinterpret_cast<uint2 *>(p.dst + (size_t)(r0 + r) * Ww)[c] = v;
+            cnt += __builtin_popcount(v.x) + __builtin_popcount(v.y);
+        }
     }
     if (p.alive) {
         const uint32_t tot = wave_sum_u32(cnt);
@@ -1651,7 +1717,9 @@ template <typename F>
 static hipError_t dispatch_lds_band(int wpl, int nt, int stride, F &&f) {
 #define GOL_LCASE(WP, NT, S) \
     if (wpl == WP && nt == NT && stride == S) return f(gol_lds_band_kernel<WP, NT, S>, NT);
-    GOL_LCASE(2, 512, 0) GOL_LCASE(2, 512, 128) GOL_LCASE(2, 512, 256) GOL_LCASE(2, 1024, 0) GOL_LCASE(2, 1024, 256)
+    // pairs: the plane stride Ww + 8 of 1024^2, 2048^2, 4096^2, 5120^2, 8192^2
+    GOL_LCASE(2, 512, 0) GOL_LCASE(2, 512, 40) GOL_LCASE(2, 512, 72) GOL_LCASE(2, 512, 136) GOL_LCASE(2, 512, 168)
+    GOL_LCASE(2, 512, 264) GOL_LCASE(2, 1024, 0) GOL_LCASE(2, 1024, 264)
     GOL_LCASE(1, 512, 0) GOL_LCASE(1, 1024, 0)
 #undef GOL_LCASE
     return hipErrorInvalidValue;
@@ -1662,9 +1730,8 @@ static int lds_tmpl_stride(int wpl, int nt, int stride) {
     return dispatch_lds_band(wpl, nt, stride, [](auto, int) { return hipSuccess; }) == hipSuccess ? stride : 0;
 }
 int lds_band_stride(int Ww, int wpl, int nt) {
-    for (int S : {128, 256})
-        if (Ww <= S && lds_tmpl_stride(wpl, nt, S) == S) return S;
-    return Ww;
+    (void)nt;
+    return wpl == 2 ? Ww + 8 : Ww;  // pairs: the two-plane row (its kernel instantiated or not)
 }
 
 int lds_band_blocks_per_cu(int wpl, int nt, int stride, int64_t lds_bytes) {
@@ -1682,8 +1749,8 @@ int lds_band_blocks_per_cu(int wpl, int nt, int stride, int64_t lds_bytes) {
 
 hipError_t launch_lds_band(const LdsBandArgs &p, int wpl, hipStream_t s) {
     const size_t bytes = (size_t)lds_band_lds_bytes(p.hmax, p.D, p.stride);
-    const int S = lds_tmpl_stride(wpl, p.nt, p.stride);
-    if (S == 0 && p.stride != p.Ww) return hipErrorInvalidValue;
+    const int S = p.rt_stride ? 0 : lds_tmpl_stride(wpl, p.nt, p.stride);
+    if (p.stride != lds_band_stride(p.Ww, wpl, p.nt)) return hipErrorInvalidValue;
     return dispatch_lds_band(wpl, p.nt, S, [&](auto kern, int t) {
         hipLaunchKernelGGL(kern, dim3(p.nb), dim3(t), bytes, s, p);
         return hipGetLastError();

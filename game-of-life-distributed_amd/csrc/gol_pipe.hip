@@ -140,16 +140,6 @@ __device__ __forceinline__ void buf_store_sc1(__amdgpu_buffer_rsrc_t rs, int off
     }
 }
 #define GOL_CBAR() asm volatile("" ::: "memory")  // no compiler reordering of memory operations across
-// LDS words read / written as relaxed workgroup-scope atomics through an
-// address-space-3 pointer: plain ds_read_b32 / ds_write_b32 that the compiler
-// neither caches in registers nor turns into flat accesses
-typedef __attribute__((address_space(3))) uint32_t lds_word;
-__device__ __forceinline__ uint32_t lds_get(lds_word *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_put(lds_word *p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 
 // Edge rows as 8-byte {word, tag} granules, each written by one sc1 store
 // and read by one sc1 load (MI355X_MICROARCH.md, hand-off table: a granule is

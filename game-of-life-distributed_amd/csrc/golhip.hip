@@ -207,6 +207,13 @@ struct golhip {
 
     // ring
     ncclComm_t comm = nullptr;
+    // test hook (golhip_test_ring_init): a ring whose halo exchange runs
+    // through a host callback instead of RCCL (two processes on one device)
+    golhip_test_transport_fn xport = nullptr;
+    void *xport_user = nullptr;
+    uint32_t *xport_host = nullptr;  // pinned: send up, send down, recv top, recv bottom
+    int64_t xport_cap = 0;           // words per block
+    bool ringed() const { return comm || xport; }
     bool force_halo = false;    // option "force_halo": one-rank RCCL ring on a whole board (tests)
     int nranks = 1, rank = 0;
     int ring_rows = 0;          // smallest strip of the ring (every rank plans from it)
@@ -337,7 +344,7 @@ DepthRun depth_plan(int cap, int64_t left) {
 // Rows the launch schedule (depth, exchange depth, words per lane) is derived
 // from: in a multi-rank ring every rank must pick the same values, so they
 // all use the ring's smallest strip.
-int sched_rows(golhip_t h) { return (h->comm && h->nranks > 1 && h->ring_rows > 0) ? h->ring_rows : h->rows; }
+int sched_rows(golhip_t h) { return (h->ringed() && h->nranks > 1 && h->ring_rows > 0) ? h->ring_rows : h->rows; }
 
 // Relative rate of a (words per lane, waves per workgroup) choice for the
 // persistent torus kernel: stored fraction of the computed tile words x band
@@ -387,7 +394,7 @@ bool pipe_fits(golhip_t h, int wpl, golk::PipeArgs *out = nullptr);
 bool persist_on(golhip_t h) {
     // a multi-rank ring never runs the resident kernel (try_persist_halo):
     // plan words per lane and halos for the per-launch kernels that do run
-    if (h->comm && h->nranks > 1) return false;
+    if (h->ringed() && h->nranks > 1) return false;
     if (h->persistent >= 0) return h->persistent != 0;
     // round 3: K1w per launch wherever its stacks fill the CUs (16384^2: 82
     // vs 62 TCUPS); smaller boards keep the resident kernel (8192^2: 27.9
@@ -403,7 +410,7 @@ int wpl_for(golhip_t h) {
     if (h->W % 64 != 0) return 1;
     if (h->wpl_opt == 1 || h->wpl_opt == 2) return h->wpl_opt;
     if (h->wpl_opt == 4) return h->W % 128 == 0 ? 4 : 2;
-    if ((!h->torus() && !h->comm) || !persist_on(h)) return wpl_per_launch(h);
+    if ((!h->torus() && !h->ringed()) || !persist_on(h)) return wpl_per_launch(h);
     if (pipe_fits(h, pipe_wpl(h))) return pipe_wpl(h);  // K1t: a whole row per wave
     if (lds_fits(h, 2)) return 2;  // K1r: pairs (11 slots a word-turn against 15)
     auto best = [&](int wpl) {
@@ -579,12 +586,35 @@ int exchange_rccl(golhip_t h, int depth, hipStream_t st) {
         if (!e0 || !e1) return fail(GOLHIP_EHIP, "hipEventCreate failed");
         HIP_OR_FAIL(hipEventRecord(e0, st));
     }
+    if (h->xport) {
+        // test transport: the two send blocks to pinned memory, the callback
+        // trades them for the neighbours', the two receive blocks back
+        if ((int64_t)n > h->xport_cap) {
+            HIP_OR_FAIL(hipHostFree(h->xport_host));
+            h->xport_host = nullptr;
+            h->xport_cap = 0;
+            HIP_OR_FAIL(hipHostMalloc(&h->xport_host, 4 * n * 4, hipHostMallocDefault));
+            h->xport_cap = (int64_t)n;
+        }
+        uint32_t *hb = h->xport_host;
+        const size_t bytes = n * 4;
+        HIP_OR_FAIL(hipMemcpyAsync(hb, b + (int64_t)p.send_up_row * h->Ww, bytes, hipMemcpyDeviceToHost, st));
+        HIP_OR_FAIL(hipMemcpyAsync(hb + n, b + (int64_t)p.send_down_row * h->Ww, bytes, hipMemcpyDeviceToHost, st));
+        HIP_OR_FAIL(hipStreamSynchronize(st));
+        if (int r = h->xport(h->xport_user, p.prev_rank, p.next_rank, hb, hb + n, hb + 2 * n, hb + 3 * n,
+                             (int64_t)bytes))
+            return fail(GOLHIP_ERCCL, "test transport returned %d", r);
+        HIP_OR_FAIL(hipMemcpyAsync(b + (int64_t)p.recv_top_row * h->Ww, hb + 2 * n, bytes, hipMemcpyHostToDevice, st));
+        HIP_OR_FAIL(hipMemcpyAsync(b + (int64_t)p.recv_bottom_row * h->Ww, hb + 3 * n, bytes, hipMemcpyHostToDevice, st));
+        HIP_OR_FAIL(hipStreamSynchronize(st));  // the pinned blocks are reused by the next exchange
+    } else {
     NCCL_OR_FAIL(ncclGroupStart());
     NCCL_OR_FAIL(ncclSend(b + (int64_t)p.send_up_row * h->Ww, n, ncclUint32, p.prev_rank, h->comm, st));
     NCCL_OR_FAIL(ncclRecv(b + (int64_t)p.recv_bottom_row * h->Ww, n, ncclUint32, p.next_rank, h->comm, st));
     NCCL_OR_FAIL(ncclSend(b + (int64_t)p.send_down_row * h->Ww, n, ncclUint32, p.next_rank, h->comm, st));
     NCCL_OR_FAIL(ncclRecv(b + (int64_t)p.recv_top_row * h->Ww, n, ncclUint32, p.prev_rank, h->comm, st));
     NCCL_OR_FAIL(ncclGroupEnd());
+    }
     if (e1) {
         HIP_OR_FAIL(hipEventRecord(e1, st));
         h->ev_pending.push_back({e0, e1, 3});
@@ -857,7 +887,7 @@ bool test_hooks_env() {
 // The consent-gated options, as golhip_build_info() reports them (the CPU
 // suite checks the list against the product contract).
 constexpr const char *kConsentInfo =
-    " CONSENT_MEASUREMENT=halo_skip,flip_debug:1-3 CONSENT_TEST_HOOKS=resident_fault,flip_debug:4";
+    " CONSENT_MEASUREMENT=halo_skip,flip_debug:1-3 CONSENT_TEST_HOOKS=resident_fault,flip_debug:4,golhip_test_ring_init";
 
 // After the stream has synchronised: the K1w spin-bound flag of the launches
 // it ran (reported by the call that ran them, then cleared).
@@ -1014,8 +1044,8 @@ bool lds_fits(golhip_t h, int wpl, golk::LdsBandArgs *out) {
     const int nb = std::min(std::min(h->cu_count, h->dev_cu) * h->lds_wg_cu, h->rows / D);
     if (nb < 1) return false;
     const int hmax = (h->rows + nb - 1) / nb;
-    int stride = h->lds_stride ? golk::lds_band_stride(h->Ww, wpl, nt) : h->Ww;
-    if (golk::lds_band_lds_bytes(hmax, D, stride) > 160 * 1024 - 256) stride = h->Ww;  // the padded rows do not fit
+    // the row stride: pairs always the two-plane row (Ww + 8, gol_kernels.hip K1r)
+    const int stride = golk::lds_band_stride(h->Ww, wpl, nt);
     const int64_t bytes = golk::lds_band_lds_bytes(hmax, D, stride);
     if (bytes > 160 * 1024 - 256) return false;  // (the kernel's few static LDS bytes)
     const int slot = (wpl == 2 ? 1 : 0) + (nt == 1024 ? 2 : 0);
@@ -1035,6 +1065,7 @@ bool lds_fits(golhip_t h, int wpl, golk::LdsBandArgs *out) {
         out->xcd = h->lds_xcd;
         out->nt = nt;
         out->stride = stride;
+        out->rt_stride = h->lds_stride ? 0 : 1;
         out->fault = h->resident_fault;
         out->pre = h->lds_pre;
     }
@@ -1177,7 +1208,7 @@ int64_t try_lds(golhip_t h, int64_t left, bool count_last, int *rc) {
     const int wpl = h->il == 2 ? 2 : 1;
     golk::LdsBandArgs p{};
     if (!lds_fits(h, wpl, &p)) return 0;
-    const int64_t ew = golk::lds_band_edge_words(p.nb, p.D, p.Ww);
+    const int64_t ew = golk::lds_band_edge_words(p.nb, p.D, p.stride);
     if (ew > h->lds_edge_cap) {
         if (hipFree(h->lds_edge) != hipSuccess) {
             *rc = fail(GOLHIP_EHIP, "hipFree (K1r edges)");
@@ -1279,7 +1310,7 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
 bool try_persist_halo(golhip_t h, int d, int k, bool count, int *rc) {
     *rc = GOLHIP_OK;
     if (!persist_on(h) || h->W % 32 != 0 || k < 2 || d < 4) return false;
-    if ((h->comm && h->nranks > 1) || !h->guarded) return false;
+    if ((h->ringed() && h->nranks > 1) || !h->guarded) return false;
     const int wpl = wpl_for(h);
     if (d != persist_depth_for(h, wpl)) return false;
     const int e = (k - 1) * d;
@@ -1415,7 +1446,7 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
     if (int rc = set_dev(h)) return rc;
     h->flips_valid = false;
     if (nturns == 0) return GOLHIP_OK;
-    const bool halo = h->comm && (h->nranks > 1 || h->force_halo);
+    const bool halo = h->ringed() && (h->nranks > 1 || h->force_halo);
     const int esz = format == GOLHIP_FLIPS_XY ? 8 : 4;
     const int64_t nw = h->local_words();
     const uint64_t most = (uint64_t)nturns * (uint64_t)h->W * (uint64_t)h->rows;
@@ -1487,7 +1518,7 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
     // every block resident at once (with a 10 % margin): block order = blockIdx.
     // Not in a multi-rank ring: its fallback (restore, re-run in ticket order)
     // would redo the batch's exchanges on this rank alone and hang the ring.
-    const bool coresident = !h->ft_ticket && !(h->comm && h->nranks > 1) && bpc > 0 &&
+    const bool coresident = !h->ft_ticket && !(h->ringed() && h->nranks > 1) && bpc > 0 &&
                             nb * 10 <= (int64_t)h->cu_count * bpc * 9;
     // launch the turns the buffer probably holds (the last batch's largest
     // list); turns past an overflow would only return at once
@@ -1703,6 +1734,7 @@ int golhip_destroy(golhip_t h) {
     HIP_RC(hipFree(h->pipe_sync));
     if (h->h_err) HIP_RC(hipHostFree(h->h_err));
     if (h->skew_err) HIP_RC(hipHostFree(h->skew_err));
+    if (h->xport_host) HIP_RC(hipHostFree(h->xport_host));
     if (h->own_stream && h->stream) HIP_RC(hipStreamDestroy(h->stream));
     delete h;
     return rc;
@@ -1933,7 +1965,7 @@ int golhip_comm_init(golhip_t h, const uint8_t id[GOLHIP_UNIQUE_ID_BYTES], int32
     if (!id || nranks < 1 || rank < 0 || rank >= nranks) return fail(GOLHIP_EINVAL, "rank %d of %d", rank, nranks);
     std::lock_guard<std::mutex> g(h->mu);
     if (int rc = set_dev(h)) return rc;
-    if (h->comm) return fail(GOLHIP_EINVAL, "comm already initialised");
+    if (h->ringed()) return fail(GOLHIP_EINVAL, "comm already initialised");
     if (nranks > 1 && h->rows < 1) return fail(GOLHIP_EINVAL, "empty strip");
     ncclUniqueId u;
     memcpy(&u, id, sizeof u);
@@ -1955,14 +1987,31 @@ int golhip_comm_init(golhip_t h, const uint8_t id[GOLHIP_UNIQUE_ID_BYTES], int32
     return GOLHIP_OK;
 }
 
+int golhip_test_ring_init(golhip_t h, int32_t nranks, int32_t rank, int32_t ring_rows, golhip_test_transport_fn fn,
+                          void *user) {
+    if (int rc = check(h)) return rc;
+    if (!test_hooks_env()) return fail(GOLHIP_EINVAL, "golhip_test_ring_init is a test hook: set GOLHIP_TEST_HOOKS=1");
+    if (!fn || nranks < 1 || rank < 0 || rank >= nranks) return fail(GOLHIP_EINVAL, "rank %d of %d", rank, nranks);
+    std::lock_guard<std::mutex> g(h->mu);
+    if (h->ringed()) return fail(GOLHIP_EINVAL, "comm already initialised");
+    if (!h->strip || h->rows < 1 || ring_rows < 1 || ring_rows > h->rows)
+        return fail(GOLHIP_EINVAL, "a strip handle and 1 <= ring_rows <= its rows");
+    h->xport = fn;
+    h->xport_user = user;
+    h->nranks = nranks;
+    h->rank = rank;
+    h->ring_rows = ring_rows;
+    return GOLHIP_OK;
+}
+
 int golhip_comm_info(golhip_t h, int32_t *nranks, int32_t *rank, int32_t *ring_rows) {
     if (int rc = check(h)) return rc;
     if (!nranks || !rank || !ring_rows) return fail(GOLHIP_EINVAL, "null output");
     std::lock_guard<std::mutex> g(h->mu);
-    if (!h->comm) {  // no ring: this handle alone
-        *nranks = 1;
-        *rank = 0;
-        *ring_rows = h->rows;
+    if (!h->comm) {  // no ring: this handle alone (or the test transport's ring)
+        *nranks = h->xport ? h->nranks : 1;
+        *rank = h->xport ? h->rank : 0;
+        *ring_rows = h->xport ? h->ring_rows : h->rows;
         return GOLHIP_OK;
     }
     int n = 0, r = 0;
@@ -2051,7 +2100,7 @@ int step_locked(golhip_t h, int64_t nturns, int32_t want_flips) {
     const int64_t tail = want_flips ? 1 : 0;
     // halo mode: row strips of a multi-rank ring, or (option force_halo) a
     // whole board run as a one-rank RCCL ring
-    const bool halo = h->comm && (h->nranks > 1 || h->force_halo);
+    const bool halo = h->ringed() && (h->nranks > 1 || h->force_halo);
     if (!halo) {
         // resident launches while they apply (more than one only past
         // golk::kResidentMaxTurns turns), then per-launch kernels for the rest
@@ -2306,7 +2355,8 @@ int golhip_alive_count_global(golhip_t h, uint64_t *count, int64_t *at_turn) {
     // same turn (a concurrent golhip_step cannot advance the board between them)
     std::lock_guard<std::mutex> g(h->mu);
     if (int rc = alive_count_locked(h, count, at_turn)) return rc;
-    if (h->nranks == 1 || !h->comm) return GOLHIP_OK;
+    if (h->nranks == 1 || !h->ringed()) return GOLHIP_OK;
+    if (!h->comm) return fail(GOLHIP_EINVAL, "the test transport has no allreduce: sum golhip_alive_count over the ranks");
     HIP_OR_FAIL(hipMemcpyAsync(h->d_scalars + 3, h->d_scalars, sizeof(unsigned long long), hipMemcpyDeviceToDevice,
                                h->stream));
     NCCL_OR_FAIL(ncclAllReduce(h->d_scalars + 3, h->d_scalars + 3, 1, ncclUint64, ncclSum, h->comm, h->stream));
@@ -2372,7 +2422,7 @@ int golhip_flip_stream(golhip_t h, int64_t nturns, int32_t format, void *out, ui
     if (format == GOLHIP_FLIPS_INDEX && (uint64_t)h->W * (uint64_t)h->H > (1ull << 32))
         return fail(GOLHIP_EINVAL, "cell indices of a %dx%d board do not fit in 32 bits", h->W, h->H);
     std::lock_guard<std::mutex> g(h->mu);
-    if (h->comm && h->nranks > 1)
+    if (h->ringed() && h->nranks > 1)
         return fail(GOLHIP_EINVAL, "golhip_flip_stream stops early on one rank alone: use golhip_step_flips in a ring");
     int64_t done = 0;
     uint64_t total = 0;
@@ -2482,7 +2532,7 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     out->cell_updates = (int64_t)h->W * h->rows * (h->step_turns + h->persist_turns + h->flip_launches);
     out->alg_bytes = out->cell_updates / 4;
     out->halo_bytes = h->halo_bytes;
-    const bool halo = h->comm && (h->nranks > 1 || h->force_halo);
+    const bool halo = h->ringed() && (h->nranks > 1 || h->force_halo);
     out->tb_depth = depth_cap(h, halo);
     out->rows_per_wave = rows_per_wave_for(h, next_depth(h, h->tb_depth, halo));
     out->kernel_variant = h->last_variant;

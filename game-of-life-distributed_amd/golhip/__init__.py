@@ -79,6 +79,11 @@ class HaloPlan(ctypes.Structure):
 
 _lib = None
 
+# golhip_test_transport_fn (test hook): user, prev_rank, next_rank, send_up,
+# send_down, recv_top, recv_bottom, bytes -> 0
+TRANSPORT_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
+
 
 def header_symbols(path: str = HEADER) -> list[str]:
     """Every function declared in include/golhip.h."""
@@ -116,6 +121,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "golhip_comm_unique_id": ([ctypes.c_char_p], ctypes.c_int),
         "golhip_comm_init": ([H, ctypes.c_char_p, i32, i32], ctypes.c_int),
         "golhip_comm_info": ([H, P(i32), P(i32), P(i32)], ctypes.c_int),
+        "golhip_test_ring_init": ([H, i32, i32, i32, TRANSPORT_FN, ctypes.c_void_p], ctypes.c_int),
         "golhip_group_step": ([P(H), i32, i64], ctypes.c_int),
         "golhip_group_step_ex": ([P(H), i32, i64, i32], ctypes.c_int),
         "golhip_halo_plan": ([i32, i32, i32, i32, i32, P(HaloPlan)], ctypes.c_int),
@@ -264,6 +270,24 @@ class Board:
 
     def comm_init(self, uid: bytes, nranks: int, rank: int) -> None:
         _check(load().golhip_comm_init(self._h, uid, nranks, rank))
+
+    def test_ring_init(self, nranks: int, rank: int, ring_rows: int, exchange) -> None:
+        """Test hook (GOLHIP_TEST_HOOKS=1, golhip_test_ring_init): this strip is
+        rank `rank` of a ring whose halos move through
+        exchange(prev_rank, next_rank, send_up: bytes, send_down: bytes) ->
+        (recv_top, recv_bottom) instead of RCCL."""
+        def cb(_user, prev, nxt, up, down, top, bottom, nbytes):
+            try:
+                t, b = exchange(prev, nxt, ctypes.string_at(up, nbytes), ctypes.string_at(down, nbytes))
+                if len(t) != nbytes or len(b) != nbytes:
+                    return 2
+                ctypes.memmove(top, t, nbytes)
+                ctypes.memmove(bottom, b, nbytes)
+                return 0
+            except Exception:  # noqa: BLE001 - reported to the library as a failed exchange
+                return 1
+        self._transport = TRANSPORT_FN(cb)  # kept alive with the handle
+        _check(load().golhip_test_ring_init(self._h, nranks, rank, ring_rows, self._transport, None))
 
     def comm_info(self) -> dict:
         """The ring as RCCL reports it (golhip_comm_info): nranks, rank, ring_rows."""

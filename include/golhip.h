@@ -158,7 +158,7 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * 1 the same, 0 off): resident LDS bands (gol_lds_band_kernel, W % 128 == 0;
  * under the same guard and timeout as the resident kernel); "lds_depth"
  * (0 = plan: 12, at most the rows): turns per LDS-band super-step; "lds_xcd"
- * (1): consecutive bands on one XCD; "lds_stride" (1): LDS rows at a
+ * (1): consecutive bands on one XCD; "lds_stride" (1; 0: the runtime-stride kernel): LDS rows at a
  * compile-time stride where one is instantiated; "lds_waves" (8 or 16) and
  * "lds_wg_cu" (1 or 2): waves per workgroup and bands per CU; "lds_pre" (2): a full super-step's
  * first turns run on the rows that need no halo while the halos travel;
@@ -202,6 +202,23 @@ int golhip_comm_init(golhip_t h, const uint8_t id[GOLHIP_UNIQUE_ID_BYTES], int32
  * smallest strip, agreed at golhip_comm_init).  Without a comm: 1, 0, and
  * this handle's rows.  No reference counterpart (measurement). */
 int golhip_comm_info(golhip_t h, int32_t *nranks, int32_t *rank, int32_t *ring_rows);
+
+/* Test hook, refused without GOLHIP_TEST_HOOKS=1 (no reference counterpart):
+ * make a strip handle rank `rank` of an `nranks` ring whose halo exchange
+ * runs through `fn` instead of RCCL, so that two processes can drive a ring
+ * on one device.  At each exchange the library stages the strip's two send
+ * blocks (its first and last `bytes / 4 / row words` rows beyond the halo
+ * plan's send rows) in pinned memory and calls fn(user, prev_rank, next_rank,
+ * send_up, send_down, recv_top, recv_bottom, bytes): fn must fill recv_top
+ * with prev_rank's send_down and recv_bottom with next_rank's send_up, and
+ * return 0.  Everything else (golhip_halo_schedule's rounds, the deep-halo
+ * launches, the kernels) is the RCCL ring's; ring_rows is the ring's smallest
+ * strip (golhip_comm_init agrees it by allreduce; here the caller passes it).
+ * golhip_alive_count_global is refused (no allreduce). */
+typedef int (*golhip_test_transport_fn)(void *user, int32_t prev_rank, int32_t next_rank, const void *send_up,
+                                        const void *send_down, void *recv_top, void *recv_bottom, int64_t bytes);
+int golhip_test_ring_init(golhip_t h, int32_t nranks, int32_t rank, int32_t ring_rows, golhip_test_transport_fn fn,
+                          void *user);
 
 /* Steps n strips (ring order = array order) driven from one process; halos
  * move with peer/device copies.  Same semantics as golhip_step on each. */

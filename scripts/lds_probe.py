@@ -20,13 +20,14 @@ ap.add_argument("--cases", default="8192x8192,5120x5120")
 ap.add_argument("--sets", default="lds_depth=8")
 ap.add_argument("--turns", type=int, default=2000)
 ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--traces", default="0,1", help="trace settings to run (0: untraced only, e.g. under rocprofv3 --pmc)")
 a = ap.parse_args()
 sets = [dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in s.split(",") if kv) for s in a.sets.split(";")]
 for rep in range(a.reps):
     for case in a.cases.split(","):
         W, H = (int(x) for x in case.split("x"))
         for opts in sets:
-            for trace in (0, 1):
+            for trace in (int(t) for t in a.traces.split(",")):
                 with golhip.Board(W, H) as b:
                     b.set_option("persistent", 1)
                     b.set_option("lds_band", 1)
@@ -50,7 +51,7 @@ for rep in range(a.reps):
                     if trace:
                         t = b.persist_trace()
                         wgs = max(1, t["workgroups"])
-                        D = opts.get("lds_depth", 8)
+                        D = opts.get("lds_depth", 12)
                         ss = (a.turns + D - 1) // D
                         # ticks are 10 ns: per workgroup, per super-step, in us
                         names = ["compute", "publish", "wait", "halo"]

@@ -8,6 +8,11 @@ SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles per wave
 barrier / sleep) + WAIT_INST_ANY (ready but not issued: dependency, pipe or
 instruction-fetch stall) + ACTIVE_INST_ANY (issuing) ~= WAVE_CYCLES.
 GRBM_GUI_ACTIVE (summed over 8 XCDs) / 8 / dispatch time = effective clock.
+
+Only the timed dispatches count: a pass keeps the dispatches at least half
+as long as its longest one (probes run a short warmup launch before the
+timed one, e.g. 200 then 1000 turns; round 5), and the
+summary records how many it kept and dropped.
 """
 import collections
 import csv
@@ -35,7 +40,13 @@ for path in sorted(glob.glob(os.path.join(src, "stall_*", "**", "*counter_collec
         names[r["Dispatch_Id"]] = r["Kernel_Name"]
     if not rows:
         continue
-    rec = res.setdefault(tag, {"kernel": sorted(set(names.values())), "counters": {}, "dispatches": 0})
+    longest = max(d["_dur"] for d in rows.values())
+    dropped = [k for k, d in rows.items() if d["_dur"] < 0.5 * longest]
+    for k in dropped:
+        del rows[k]
+    rec = res.setdefault(tag, {"kernel": sorted(set(names.values())), "counters": {}, "dispatches": 0,
+                               "dropped_short_dispatches": 0})
+    rec["dropped_short_dispatches"] = max(rec["dropped_short_dispatches"], len(dropped))
     keys = set().union(*[set(d) for d in rows.values()])
     for k in sorted(keys):
         vals = [d[k] for d in rows.values() if k in d]

@@ -129,7 +129,7 @@ def test_product_build_macros():
             # options that give wrong results by design need
             # GOLHIP_MEASUREMENT=1, test hooks GOLHIP_TEST_HOOKS=1 (refused otherwise:
             # tests/test_gpu_parity.py::test_wrong_result_options_need_measurement_consent)
-            "CONSENT_MEASUREMENT": "halo_skip,flip_debug:1-3", "CONSENT_TEST_HOOKS": "resident_fault,flip_debug:4"}
+            "CONSENT_MEASUREMENT": "halo_skip,flip_debug:1-3", "CONSENT_TEST_HOOKS": "resident_fault,flip_debug:4,golhip_test_ring_init"}
     got = dict(kv.split("=", 1) for kv in info.split())
     assert got == want, info
 
