@@ -130,7 +130,7 @@ struct golhip {
     int lds_band = -1;              // option "lds_band": resident LDS bands K1r (1 on where it fits, 0 off, -1 auto)
     int lds_depth = 0;              // option "lds_depth": turns per K1r super-step (0: plan)
     int lds_xcd = 1;                // option "lds_xcd": consecutive K1r bands on one XCD
-    int lds_waves = 8;              // option "lds_waves": K1r waves per workgroup (8 or 16)
+    int lds_waves = 0;              // option "lds_waves": K1r waves per workgroup (8 or 16; 0: plan)
     int lds_wg_cu = 1;              // option "lds_wg_cu": K1r bands (workgroups) per CU (1 or 2)
     int lds_stride = 1;             // option "lds_stride": K1r LDS rows at a compile-time stride where instantiated
     int resident_fault = 0;         // option "resident_fault" (tests): K1r band 0 / K1p workgroup 0 never report
@@ -1028,9 +1028,18 @@ bool take_guard(golhip_t h, int *rc) {
 bool lds_fits(golhip_t h, int wpl, golk::LdsBandArgs *out) {
     if (h->lds_band == 0 || !h->torus() || h->W % 128 != 0 || (wpl == 2 && h->W % 64 != 0)) return false;
     if (h->nranks > 1) return false;
-    const int D = h->lds_depth > 0 ? h->lds_depth : std::min(12, h->rows);
+    // waves: 16 where a row's pairs fill whole waves at least twice and the
+    // 1024 threads exactly (8192 wide: 40.9 vs 39.4 TCUPS at depth 10; 5120 /
+    // 4096 wide lose a quarter with 16, their runs too short; 12288 wide, 960
+    // of 1024 threads busy: 12.0 against K1p's 13.0 at 12288 x 2048;
+    // profiles/r5m, r5n), else 8; depth 10 at 16 waves, else 12 (r5m: 8192^2
+    // at 8 waves 39.8 / 39.4 / 38.9 at 10 / 12 / 14, 5120^2 21.2 / 21.6 / 21.2)
+    const int P2 = h->Ww / 2;
+    const int waves = h->lds_waves > 0 ? h->lds_waves
+                      : (wpl == 2 && P2 % 64 == 0 && P2 >= 128 && 1024 % P2 == 0) ? 16 : 8;
+    const int D = h->lds_depth > 0 ? h->lds_depth : std::min(waves == 16 ? 10 : 12, h->rows);
     if (h->rows < D || D < 1) return false;
-    const int nt = 64 * h->lds_waves;
+    const int nt = 64 * waves;
     // auto: only where the rows' pairs (words) keep >= 90 % of the threads busy
     // (runs of whole columns: 512 / P runs each; 12288 x 2048 = 192 pairs a row
     // keeps 384 of 512 and ran 11.0 vs K1p's 13.0 TCUPS, while 1024^2 .. 8192^2,
@@ -1917,7 +1926,8 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         return GOLHIP_OK;
     }
     if (!strcmp(key, "lds_waves")) {
-        if (value != 8 && value != 16) return fail(GOLHIP_EINVAL, "lds_waves %lld not 8 or 16", (long long)value);
+        if (value != 0 && value != 8 && value != 16)
+            return fail(GOLHIP_EINVAL, "lds_waves %lld not 0, 8 or 16", (long long)value);
         h->lds_waves = (int)value;
         return GOLHIP_OK;
     }

@@ -157,9 +157,10 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * band of >= lds_depth full-width rows per CU fits both its LDS buffers;
  * 1 the same, 0 off): resident LDS bands (gol_lds_band_kernel, W % 128 == 0;
  * under the same guard and timeout as the resident kernel); "lds_depth"
- * (0 = plan: 12, at most the rows): turns per LDS-band super-step; "lds_xcd"
+ * (0 = plan: 10 at 16 waves, else 12; at most the rows): turns per LDS-band super-step; "lds_xcd"
  * (1): consecutive bands on one XCD; "lds_stride" (1; 0: the runtime-stride kernel): LDS rows at a
- * compile-time stride where one is instantiated; "lds_waves" (8 or 16) and
+ * compile-time stride where one is instantiated; "lds_waves" (0 = plan: 16 where a row's pairs fill
+ * whole waves twice or more, else 8; or 8, 16) and
  * "lds_wg_cu" (1 or 2): waves per workgroup and bands per CU; "lds_pre" (2): a full super-step's
  * first turns run on the rows that need no halo while the halos travel;
  * "lds_pipe" (default 0): 1 runs the resident LDS turn pipeline

@@ -125,6 +125,7 @@ def test_lds_band_then_other_kernels(coracle):
                                       (2048, 1000, {"lds_stride": 0}),       # 64 words at their own stride
                                       (5120, 640, {"lds_stride": 0}),
                                       (8192, 1024, {"lds_waves": 16}),       # 16 waves a workgroup
+                                      (8192, 1024, {"lds_waves": 8}),        # 8192 wide on 8 (auto: 16)
                                       (5120, 1280, {"lds_waves": 16}),
                                       (8192, 2048, {"lds_wg_cu": 2}),        # two bands a CU
                                       (4096, 3000, {"lds_wg_cu": 2})])
