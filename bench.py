@@ -810,6 +810,12 @@ class RankEnv:
         self.dist.broadcast_object_list(uid, src=0)
         return uid[0]
 
+    def ring_init(self, board, tag: str = "") -> None:
+        """This rank's strip joins the halo ring: the library's own RCCL
+        communicator (rank 0's unique id broadcast over the process group)."""
+        self.stage(tag + "golhip_comm_init (ncclCommInitRank + strip-row allreduce)")
+        board.comm_init(self.unique_id(), self.world, self.rank)
+
     def barrier(self, board) -> None:
         if self.dist is not None:
             self.dist.barrier()
@@ -896,8 +902,7 @@ def measure(a, env, workload: int, steps: int, warmup: int, warmup_seconds: floa
             board.set_option(k, int(v))
         comm = None
         if world > 1:
-            env.stage(tag + "golhip_comm_init (ncclCommInitRank + strip-row allreduce)")
-            board.comm_init(env.unique_id(), world, rank)
+            env.ring_init(board, tag)
             comm = board.comm_info()
             if comm["nranks"] != world or comm["rank"] != rank:
                 raise SystemExit(f"RCCL ring reports rank {comm['rank']} of {comm['nranks']}, "

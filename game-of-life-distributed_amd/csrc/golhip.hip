@@ -168,6 +168,7 @@ struct golhip {
     // launch times out (its workgroups were not all co-resident)
     uint32_t *backup = nullptr;
     bool guarded = false;
+    bool guard_light = false;  // the guarded step is one source-keeping launch: its source is the copy
     int64_t persist_fallbacks = 0;
     int64_t persist_timeout_ticks = 100000000ll;  // 1 s at the 100 MHz s_memrealtime clock (option "persist_timeout_us")
     int auto_rpw[kNumDepths] = {};  // cache per depth index
@@ -1002,9 +1003,17 @@ int persist_depth_for(golhip_t h, int wpl) {
 // of this handle's rows that golhip_step restores (and then re-runs the step
 // on the per-launch kernels) if a resident launch times out.  False (rc 0)
 // if there is no room for the copy: then no resident launch this step.
-bool take_guard(golhip_t h, int *rc) {
+// keeps_src: the step is one launch that never writes its source buffer (K1r,
+// K1t read it once into LDS and write only the other buffer) and nothing runs
+// after it, so the source itself is the copy (a timeout leaves it intact).
+bool take_guard(golhip_t h, int *rc, bool keeps_src = false) {
     *rc = GOLHIP_OK;
     if (h->guarded) return true;  // a step of several resident launches keeps its first copy
+    if (keeps_src) {
+        h->guarded = true;
+        h->guard_light = true;
+        return true;
+    }
     const size_t bytes = (size_t)h->local_words() * 4;
     if (!h->backup && hipMalloc(&h->backup, bytes) != hipSuccess) {
         h->backup = nullptr;
@@ -1160,7 +1169,7 @@ int64_t try_pipe(golhip_t h, int64_t left, bool count_last, int *rc) {
         }
         *h->h_err = 0;
     }
-    if (!take_guard(h, rc)) return 0;
+    if (!take_guard(h, rc, count_last && run == left)) return 0;
     const bool count = count_last && run == left;
     hipError_t e = count ? hipMemsetAsync(h->d_scalars, 0, sizeof(unsigned long long), h->stream) : hipSuccess;
     if (e == hipSuccess) e = hipMemsetAsync(h->pipe_sync, 0, (size_t)sw * 4, h->stream);
@@ -1239,7 +1248,7 @@ int64_t try_lds(golhip_t h, int64_t left, bool count_last, int *rc) {
         }
         *h->h_err = 0;
     }
-    if (!take_guard(h, rc)) return 0;
+    if (!take_guard(h, rc, count_last && run == left)) return 0;
     const bool count = count_last && run == left;
     hipError_t e = count ? hipMemsetAsync(h->d_scalars, 0, sizeof(unsigned long long), h->stream) : hipSuccess;
     if (e == hipSuccess) e = hipMemsetAsync(h->d_sync, 0, (size_t)(p.nb + 1) * sizeof(unsigned), h->stream);
@@ -2177,6 +2186,8 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     const size_t ev0 = h->ev_pending.size();
     const int64_t halo_exchanges0 = h->halo_exchanges, halo_bytes0 = h->halo_bytes;
     int rc = step_locked(h, nturns, want_flips);
+    const bool light = h->guard_light;
+    h->guard_light = false;
     if (rc || !h->guarded) {
         h->guarded = false;
         return rc;
@@ -2211,8 +2222,9 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
         }
         h->ev_pending.resize(ev0);
     }
-    HIP_OR_FAIL(hipMemcpyAsync(h->buf[cur0] + (int64_t)kHalo * h->Ww, h->backup, (size_t)h->local_words() * 4,
-                               hipMemcpyDeviceToDevice, h->stream));
+    if (!light)  // (a source-keeping launch left the step's board in buf[cur0])
+        HIP_OR_FAIL(hipMemcpyAsync(h->buf[cur0] + (int64_t)kHalo * h->Ww, h->backup, (size_t)h->local_words() * 4,
+                                   hipMemcpyDeviceToDevice, h->stream));
     h->cur = cur0;
     h->turns = turns0;
     h->alive_turn = -1;

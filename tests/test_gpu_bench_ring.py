@@ -1,0 +1,147 @@
+"""bench.py's multi-rank path end to end on one GPU:
+two rank processes run bench.main() exactly as `bench.py --gpus 2` ranks do
+(measure() of configs[2] and the configs3 block, parity against the
+full-size fixtures, the barrier-bracketed timed region, max over ranks, the
+per-rank rows, rank 0's one JSON line), with two substitutions a single GPU
+forces: the process group is gloo instead of RCCL, and each strip joins its
+halo ring through golhip_test_ring_init (GOLHIP_TEST_HOOKS=1), the exchange
+riding gloo point-to-point messages at the place of the RCCL group.  The
+line's timings are meaningless (two ranks share one GPU); its parity, plan
+and plumbing are what is checked.  RCCL's own transport is left to the
+driver's multi-GPU run.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+RANK_MAIN = r'''
+import os, sys
+sys.path[:0] = [{root!r}, os.path.join({root!r}, "game-of-life-distributed_amd")]
+sys.argv = ["bench.py"] + {argv!r}
+import numpy as np
+import torch
+import torch.distributed as dist
+import bench
+import golhip
+
+
+class HostBoard(golhip.Board):
+    """golhip_alive_count_global has no allreduce on the test transport: sum over gloo."""
+
+    def alive_count(self, global_sum=False):
+        c, t = super().alive_count()
+        if global_sum:
+            x = torch.tensor([c], dtype=torch.int64)
+            dist.all_reduce(x)
+            c = int(x.item())
+        return c, t
+
+
+class HostRingEnv(bench.RankEnv):
+    """bench.RankEnv on one shared GPU: gloo collectives on CPU tensors and
+    the library's test transport for the halo ring."""
+
+    def __init__(self, a, world, rank, local):
+        self.a, self.world, self.rank, self.local = a, world, rank, 0
+        self.wd = bench.Watchdog(a, rank)
+        self.torch = torch
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+        self.dist = dist
+
+    def board(self, W, H, row0, rows):
+        return HostBoard(W, H, device=0, row0=row0, rows=rows)
+
+    def ring_init(self, board, tag=""):
+        self.stage(tag + "golhip_test_ring_init (host transport over gloo)")
+        rows = [None] * self.world
+        dist.all_gather_object(rows, board.rows)
+
+        def exchange(prev, nxt, up, down):
+            n = len(up)
+            top, bottom = torch.empty(n, dtype=torch.uint8), torch.empty(n, dtype=torch.uint8)
+            reqs = [dist.isend(torch.frombuffer(bytearray(up), dtype=torch.uint8), prev, tag=0),
+                    dist.isend(torch.frombuffer(bytearray(down), dtype=torch.uint8), nxt, tag=1),
+                    dist.irecv(top, prev, tag=1), dist.irecv(bottom, nxt, tag=0)]
+            for r in reqs:
+                r.wait()
+            return top.numpy().tobytes(), bottom.numpy().tobytes()
+
+        board.test_ring_init(self.world, self.rank, min(rows), exchange)
+
+    def barrier(self, board):
+        dist.barrier()
+        board.sync()
+        torch.cuda.synchronize()
+
+    def gsum(self, x):
+        t = torch.tensor([x - (1 << 64) if x >= (1 << 63) else x], dtype=torch.int64)
+        dist.all_reduce(t)
+        return int(t.item()) % (1 << 64)
+
+    def gmax(self, x):
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def bcast(self, x):
+        t = torch.tensor([x], dtype=torch.int64)
+        dist.broadcast(t, src=0)
+        return int(t.item())
+
+
+bench.main(env_factory=HostRingEnv)
+'''
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.timeout(450)
+def test_bench_two_ranks_host_ring(tmp_path):
+    world = 2
+    argv = ["--gpus", str(world), "--steps", "1", "--warmup", "1", "--warmup-seconds", "0",
+            "--configs3-warmup-seconds", "0", "--stage-timeout", "200"]
+    script = tmp_path / "rank_main.py"
+    script.write_text(RANK_MAIN.format(root=ROOT, argv=argv))
+    port = _free_port()
+    procs, files = [], []
+    for r in range(world):
+        env = dict(os.environ, GOLHIP_TEST_HOOKS="1", RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(world),
+                   LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        out, err = tmp_path / f"rank{r}.out", tmp_path / f"rank{r}.err"
+        files.append((out, err))
+        with open(out, "w") as fo, open(err, "w") as fe:
+            procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=fo, stderr=fe))
+    try:
+        for p in procs:
+            p.wait(timeout=400)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    outs = [(o.read_text(), e.read_text()) for o, e in files]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+    lines = [ln for ln in outs[0][0].splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, outs[0][0][-2000:]
+    assert not [ln for ln in outs[1][0].splitlines() if ln.startswith("{")]  # rank 0 alone prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == world and d["parity"] is True, d.get("parity_check")
+    assert d["parity_check"]["ok"] is True and d["configs3"]["parity"] is True, d["configs3"].get("parity_check")
+    for blk in (d, d["configs3"]):
+        ranks = blk["config"]["ranks"]
+        assert [r["rank"] for r in ranks] == list(range(world)), ranks
+        assert blk["config"]["comm"]["nranks"] == world
+        assert blk["value"] > 0 and blk["ms_per_step"] > 0
