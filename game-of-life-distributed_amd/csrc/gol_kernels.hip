@@ -1353,6 +1353,8 @@ __global__ __launch_bounds__(NW * 64) void gol_persist_kernel(PersistArgs p) {
 // columns 0 and P - 1 write the ghosts, the others rewrite their E[c]).
 // ---------------------------------------------------------------------------
 // A row's words as loaded: the lane's own word (pair) and one neighbour word on each side.
+constexpr int kHaloRegs = 4;  // K1r: 16-B halo granules per thread loaded ahead (more: loaded at the store)
+
 template <int WPL>
 struct LdsRaw {
     uint32_t c[WPL], l, r;
@@ -1587,8 +1589,14 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
         };
         // Neighbours' super-step j edges (generation j D) into the halo rows of A;
         // false if the wait timed out (every workgroup drains).
-        auto wait_halos = [&]() -> bool {
-            // neighbours' super-step j edges (generation j D)
+        // Neighbours' super-step j edges (generation j D) into the halo rows of
+        // A, in three parts: wait_flags (wave 0 polls both flags; false if the
+        // wait timed out, every workgroup drains), halo_issue (every thread's
+        // first kHaloRegs 16-B granules in flight at once, into registers) and
+        // halo_store (those to LDS, any further granules loaded and stored, a
+        // barrier): the granules of a thread travel together, not one round
+        // trip after another.
+        auto wait_flags = [&]() -> bool {
             if (w == 0) {
                 const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
                 const int nbr = lane == 0 ? up : down;
@@ -1611,19 +1619,37 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
             __syncthreads();
             if (s_abort) return false;  // uniform over the workgroup
             lap(2);
-            const int slot = j & 1;
-            const int eu = (((slot * nb + up) * 2 + 1) * eq4) * 16;    // up's bottom D rows -> rows [0, D)
-            const int ed = (((slot * nb + down) * 2 + 0) * eq4) * 16;  // down's top D rows -> rows [D + h, R)
-            for (int i = threadIdx.x; i < 2 * eq4; i += NT) {
-                const bool top = i < eq4;
-                const int g = top ? i : i - eq4;
-                const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(ers, (top ? eu : ed) + g * 16, 0, kCpolSc1);
-                uint32_t *dstw = A + (size_t)(top ? 0 : D + h) * LS + 4 * (g % rq4) + (size_t)(g / rq4) * LS;
-                *reinterpret_cast<uint4 *>(dstw) = make_uint4(v.x, v.y, v.z, v.w);
+            return true;
+        };
+        const int eu = (((j & 1) * nb + up) * 2 + 1) * eq4 * 16;    // up's bottom D rows -> rows [0, D)
+        const int ed = (((j & 1) * nb + down) * 2 + 0) * eq4 * 16;  // down's top D rows -> rows [D + h, R)
+        auto halo_load = [&](int i) -> v4u32 {
+            const bool top = i < eq4;
+            return __builtin_amdgcn_raw_buffer_load_b128(ers, (top ? eu : ed) + (top ? i : i - eq4) * 16, 0, kCpolSc1);
+        };
+        auto halo_put = [&](int i, const v4u32 &v) {
+            const bool top = i < eq4;
+            const int g = top ? i : i - eq4;
+            uint32_t *dstw = A + (size_t)(top ? 0 : D + h) * LS + 4 * (g % rq4) + (size_t)(g / rq4) * LS;
+            *reinterpret_cast<uint4 *>(dstw) = make_uint4(v.x, v.y, v.z, v.w);
+        };
+        v4u32 hreg[kHaloRegs];
+        auto halo_issue = [&]() {
+#pragma unroll
+            for (int k = 0; k < kHaloRegs; ++k) {
+                const int i = (int)threadIdx.x + k * NT;
+                if (i < 2 * eq4) hreg[k] = halo_load(i);
             }
+        };
+        auto halo_store = [&]() {
+#pragma unroll
+            for (int k = 0; k < kHaloRegs; ++k) {
+                const int i = (int)threadIdx.x + k * NT;
+                if (i < 2 * eq4) halo_put(i, hreg[k]);
+            }
+            for (int i = (int)threadIdx.x + kHaloRegs * NT; i < 2 * eq4; i += NT) halo_put(i, halo_load(i));
             __syncthreads();
             lap(3);
-            return true;
         };
         // interior first (option lds_pre = k): the first k turns of a full
         // super-step run on the rows that need no halo, [D + t, D + h - t), while
@@ -1643,7 +1669,12 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
                 }
             }
             lap(0);
-            if (!wait_halos()) return;
+            // (the flags waited for before the last interior turn and the loads
+            // in flight during it ran 8192^2 39.0 vs 40.9 TCUPS: the earlier
+            // wait costs more than the hidden loads save; profiles/r5t)
+            if (!wait_flags()) return;
+            halo_issue();
+            halo_store();
             for (int t = 1; t <= pre; ++t)
                 do_turn((t & 1) ? A : B, (t & 1) ? B : A, t, D + t, D + h - t, R - t);
             for (int t = pre + 1; t <= D; ++t) do_turn((t & 1) ? A : B, (t & 1) ? B : A, t, R - t, 0, 0);
@@ -1664,7 +1695,11 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
             signal((unsigned)j);
             pending = false;
         }
-        if (j > 0 && !wait_halos()) return;
+        if (j > 0) {
+            if (!wait_flags()) return;
+            halo_issue();
+            halo_store();
+        }
         // whole turns (a shorter last super-step needs only Dj halo rows of the D)
         const int skip = D - Dj;
         for (int t = 1; t <= Dj; ++t) {
