@@ -287,13 +287,15 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str, 
         kname = ("gol_skew_kernel" if 2 * perf.get("skew_launches", 0) > perf["step_launches"] else
                  "gol_tb_pair_kernel")
         launches, kms, kturns = perf["step_launches"], region_ms, perf["step_turns"]
-        depth = perf["tb_depth"]
+        depth = None  # the turns a launch fused (the plan may cap tb_depth)
     launches = max(1, launches)
     avg_s = kms / launches * 1e-3
     wpl = max(1, perf["words_per_lane"])
     spw = 9.0 + 8.0 / wpl
     words = rows * ((W + 31) // 32)
     tpl = kturns / launches
+    if depth is None:
+        depth = int(round(tpl)) if abs(tpl - round(tpl)) < 1e-9 else f"{tpl:.2f} turns a launch on average"
     slots = words * tpl / 64.0 * spw
     achieved = slots / avg_s / 1e9 if avg_s > 0 else None
     alg_bytes = W * rows * tpl * ALG_BYTES_PER_UPDATE

@@ -1,5 +1,5 @@
-// gol_bits.h — device helpers shared by the step kernels (gol_kernels.hip,
-// gol_pipe.hip): the bit-sliced B3/S23 circuit (v_bitop3 LUTs), DPP lane
+// gol_bits.h — device helpers of the step kernels (gol_kernels.hip): the
+// bit-sliced B3/S23 circuit (v_bitop3 LUTs), LDS word access, DPP lane
 // shifts, wave reductions, the counter hash of the synthetic boards and the
 // write-through buffer-access policy bit.
 #pragma once
@@ -81,7 +81,7 @@ __device__ __forceinline__ uint32_t rule_word(uint32_t a0, uint32_t a1, uint32_t
     return bop<kNext>(u0, g1, g2);
 }
 
-// Row sums and centre words of one row (K1r / K1t).
+// Row sums and centre words of one row (K1r).
 template <int WPL>
 struct LdsRow {
     uint32_t s0[WPL], s1[WPL], c[WPL];

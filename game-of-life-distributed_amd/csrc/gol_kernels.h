@@ -147,46 +147,6 @@ int lds_band_stride(int Ww, int wpl, int nt);
 int lds_band_blocks_per_cu(int wpl, int nt, int stride, int64_t lds_bytes);
 hipError_t launch_lds_band(const LdsBandArgs &p, int wpl, hipStream_t s);
 
-// Resident LDS turn pipeline (K1t, gol_kernels.hip; small tori whose rows are
-// one wavefront wide: Ww == 64 * wpl).  Workgroup b of nb owns a band of
-// h_b rows, skewed: generation t of the band is the rows [r_b + t, r_{b+1} + t)
-// (mod rows), so generation t needs only generation t - 1's rows of the band
-// plus the first two rows of the band below (no trapezoid, no super-steps).
-// Wave w of the kPipeWaves computes the turns w + 1, w + 1 + kPipeWaves, ...:
-// it streams its band's rows top to bottom, reading the previous turn's rows
-// from the previous wave's LDS ring and writing its own into its ring (the
-// last wave's ring feeds the first: the turns circulate).  Each turn's first
-// two rows also go to `edge` for the band above (write-through {word, tag}
-// granules per (band, turn mod kPipeQ)); `econs` returns which turns were read.
-// The last turn's rows go to dst at [r_b + turns, r_{b+1} + turns).
-constexpr int kPipeWaves = 8;   // waves (stages) per workgroup
-constexpr int kPipeQ = 32;      // edge slots per band: turns a band may run ahead of the band above
-constexpr int kPipeK = 8;       // slots of each ring but the last (the last holds the band: kw >= hmax + 4)
-struct PipeArgs {
-    const uint32_t *src;   // generation 0: rows x Ww words
-    uint32_t *dst;         // the last generation (the other buffer)
-    uint32_t *edge;        // pipe_edge_words(nb, Ww): {word, tag} granules, tag = tag_base + turn
-    unsigned *econs;       // nb, zeroed: turns of band b's edges (0, 1, ...) band b - 1 has read
-    unsigned *error;       // zeroed; set on a spin timeout (every wave then drains)
-    unsigned long long *alive;  // nullable: += popcount of the last generation
-    unsigned long long *trace;  // nullable: [0..3] += wave ticks waiting for ring rows, ring room, imports,
-                                // edge room; [4] += wave ticks in the kernel; [8..10] += ticks in the
-                                // steady-state row loop, its rows, ring-row waits among them
-    long long timeout_ticks;    // s_memrealtime ticks (100 MHz) a wait may take
-    int Ww, rows, nb, turns;
-    int hmax;              // ceil(rows / nb)
-    int kw;                // slots of the last wave's ring: a power of two >= hmax + 4
-    int xcd;               // 1: consecutive bands on one XCD (nb % 8 == 0)
-    unsigned tag_base;     // edge tags of this launch are tag_base + turn (> every tag in the buffer)
-};
-__host__ __device__ inline int64_t pipe_edge_words(int nb, int Ww) { return 4ll * nb * kPipeQ * Ww; }
-__host__ __device__ inline int pipe_slots(int kw) { return (kPipeWaves - 1) * kPipeK + kw; }
-// rows, one tag per row slot, CONS[kPipeWaves], 64 dummy words (the lanes
-// other than lane 0 of a signal store write there: no same-address stores)
-inline int64_t pipe_lds_bytes(int Ww, int kw) { return ((int64_t)pipe_slots(kw) * (Ww + 1) + kPipeWaves + 64) * 4; }
-int pipe_blocks_per_cu(int wpl, int64_t lds_bytes);
-hipError_t launch_pipe(const PipeArgs &p, int wpl, hipStream_t s);
-
 hipError_t launch_pack(const uint8_t *bytes, uint32_t *words, int W, int Ww, int rows, hipStream_t s);
 // il: the words are in the interleaved pair layout of the wpl = 2 step kernels
 // (W % 64 == 0); pack / fill_random / load write canonical words, which the

@@ -137,16 +137,6 @@ struct golhip {
                                     // (their neighbours' bounded waits time out: the restore-and-re-run path)
     int lds_pre = 2;                // option "lds_pre": K1r interior-first turns while the halos travel
                                     // (profiles/r4pre: 8192^2 31.4 -> 33.9 TCUPS at 2; 1: 33.2, 3: 33.1, 4: 32.3)
-    int lds_pipe = 0;               // option "lds_pipe": resident LDS turn pipeline K1t where it fits (1; 0 off:
-                                    // slower than K1r at every width it runs)
-    uint32_t *pipe_edge = nullptr;  // K1t edge rows (golk::pipe_edge_words)
-    int64_t pipe_edge_cap = 0;
-    unsigned *pipe_sync = nullptr;  // K1t [0] error, then econs[nb]
-    uint32_t pipe_tag_base = 0;     // K1t edge tags: next launch's base (0: edge buffer not zeroed yet)
-    int64_t pipe_sync_cap = 0;
-    int pipe_bpc[3] = {};           // K1t workgroups per CU by wpl at pipe_bpc_bytes of LDS
-    int64_t pipe_bpc_bytes[3] = {};
-    int64_t pipe_launches = 0;
     uint32_t *lds_edge = nullptr;   // K1r edge rows (golk::lds_band_edge_words)
     int64_t lds_edge_cap = 0;
     int64_t lds_launches = 0;
@@ -390,8 +380,6 @@ constexpr int64_t kPersistAutoMaxBytes = 64ll << 20;
 int wpl_per_launch(golhip_t h);
 bool skew_fills(golhip_t h);
 bool lds_fits(golhip_t h, int wpl, golk::LdsBandArgs *out = nullptr);
-int pipe_wpl(golhip_t h);
-bool pipe_fits(golhip_t h, int wpl, golk::PipeArgs *out = nullptr);
 bool persist_on(golhip_t h) {
     // a multi-rank ring never runs the resident kernel (try_persist_halo):
     // plan words per lane and halos for the per-launch kernels that do run
@@ -412,7 +400,6 @@ int wpl_for(golhip_t h) {
     if (h->wpl_opt == 1 || h->wpl_opt == 2) return h->wpl_opt;
     if (h->wpl_opt == 4) return h->W % 128 == 0 ? 4 : 2;
     if ((!h->torus() && !h->ringed()) || !persist_on(h)) return wpl_per_launch(h);
-    if (pipe_fits(h, pipe_wpl(h))) return pipe_wpl(h);  // K1t: a whole row per wave
     if (lds_fits(h, 2)) return 2;  // K1r: pairs (11 slots a word-turn against 15)
     auto best = [&](int wpl) {
         const int d = default_depth(h, wpl);
@@ -470,12 +457,21 @@ int loaded_canonical(golhip_t h) {
 
 // Most turns one launch may fuse.  In halo mode the `depth` halo rows must
 // all come from one neighbour strip, so depth <= strip rows.
+bool skew_dims(golhip_t h, int depth, int wpl, int L, golk::SkewArgs *sk);
+
 int depth_cap(golhip_t h, bool halo) {
     if (h->W % 32 != 0) return 1;  // generic kernel: one turn per launch
     // a strip between exchanges runs the resident kernel (its depths) when on
     const int wpl = wpl_for(h);
     int cap = std::min(h->tb_depth, (halo && persist_on(h)) ? golk::persist_max_depth(wpl) : golk::max_depth_for(wpl));
     if (halo) cap = std::min(cap, sched_rows(h));
+    // whole tori whose K1w plan takes half-wave tiles (bands of ~2D rows, the
+    // launch mostly ramps) fuse 16 turns: 16384^2 86.3-86.5
+    // vs 85.5-85.7 TCUPS at 20 (profiles/r5v; 82.1 vs 81.2 in r4y)
+    if (!halo && wpl == 2 && cap > 16) {
+        golk::SkewArgs sk{};
+        if (skew_dims(h, 20, 2, h->rows, &sk) && sk.half) cap = 16;
+    }
     if (cap == 9 && (wpl != 4 || (halo && persist_on(h)))) cap = 8;  // only per-launch quads have 9
     return cap;
 }
@@ -1004,7 +1000,7 @@ int persist_depth_for(golhip_t h, int wpl) {
 // on the per-launch kernels) if a resident launch times out.  False (rc 0)
 // if there is no room for the copy: then no resident launch this step.
 // keeps_src: the step is one launch that never writes its source buffer (K1r,
-// K1t read it once into LDS and write only the other buffer) and nothing runs
+// reads it once into LDS and writes only the other buffer) and nothing runs
 // after it, so the source itself is the copy (a timeout leaves it intact).
 bool take_guard(golhip_t h, int *rc, bool keeps_src = false) {
     *rc = GOLHIP_OK;
@@ -1090,133 +1086,6 @@ bool lds_fits(golhip_t h, int wpl, golk::LdsBandArgs *out) {
     return true;
 }
 
-// K1t (gol_lds_pipe_kernel): words per lane of a torus whose rows are one
-// wavefront wide (Ww == 64 wpl), else 0.
-int pipe_wpl(golhip_t h) {
-    if (h->W % 32 != 0) return 0;
-    for (int wpl : {1, 2, 4})
-        if (h->Ww == 64 * wpl && (wpl == 1 || h->W % (32 * wpl) == 0)) return wpl;
-    return 0;
-}
-
-// The K1t plan of this torus at `wpl` words per lane (no side effects): one
-// band per CU of at least two rows, the rings of a band in one workgroup's
-// LDS, every workgroup resident (the bands wait on each other around the
-// torus).  False if K1t does not apply.
-bool pipe_fits(golhip_t h, int wpl, golk::PipeArgs *out) {
-    if (h->lds_pipe == 0 || !h->torus() || h->nranks > 1 || wpl < 1 || wpl != pipe_wpl(h)) return false;
-    const int nb = std::min(std::min(h->cu_count, h->dev_cu), h->rows / 2);
-    if (nb < 1) return false;
-    const int hmax = (h->rows + nb - 1) / nb;
-    int kw = 1;
-    while (kw < hmax + 4) kw <<= 1;
-    const int64_t bytes = golk::pipe_lds_bytes(h->Ww, kw);
-    if (bytes > 160 * 1024 - 256) return false;
-    const int slot = wpl == 4 ? 2 : wpl - 1;
-    int &bpc = h->pipe_bpc[slot];
-    if (bpc == 0 || h->pipe_bpc_bytes[slot] != bytes) {
-        bpc = std::max(0, golk::pipe_blocks_per_cu(wpl, bytes));
-        h->pipe_bpc_bytes[slot] = bytes;
-    }
-    if (bpc < 1 || (int64_t)nb > (int64_t)bpc * h->cu_count) return false;
-    if (out) {
-        out->Ww = h->Ww;
-        out->rows = h->rows;
-        out->nb = nb;
-        out->hmax = hmax;
-        out->kw = kw;
-        out->xcd = h->lds_xcd;
-    }
-    return true;
-}
-
-// Torus: the turns as K1t launches (one unless past golk::kResidentMaxTurns),
-// under the step guard like K1r / K1p; returns the turns run (0: K1t does
-// not apply).
-int64_t try_pipe(golhip_t h, int64_t left, bool count_last, int *rc) {
-    *rc = GOLHIP_OK;
-    if (left < 1) return 0;
-    const int wpl = h->il == 0 ? 1 : h->il;
-    golk::PipeArgs p{};
-    if (!pipe_fits(h, wpl, &p)) return 0;
-    const int64_t run = golk::resident_turns(left);
-    const int64_t ew = golk::pipe_edge_words(p.nb, p.Ww);
-    const int64_t sw = 1 + p.nb;  // error, econs[nb]
-    if (ew > h->pipe_edge_cap || sw > h->pipe_sync_cap) {
-        if (hipFree(h->pipe_edge) != hipSuccess || hipFree(h->pipe_sync) != hipSuccess) {
-            *rc = fail(GOLHIP_EHIP, "hipFree (K1t buffers)");
-            return 0;
-        }
-        h->pipe_edge = nullptr;
-        h->pipe_sync = nullptr;
-        h->pipe_edge_cap = h->pipe_sync_cap = 0;
-        if (hipMalloc(&h->pipe_edge, (size_t)ew * 4) != hipSuccess ||
-            hipMalloc(&h->pipe_sync, (size_t)sw * 4) != hipSuccess) {
-            (void)hipFree(h->pipe_edge);
-            h->pipe_edge = nullptr;
-            h->pipe_sync = nullptr;
-            return 0;
-        }
-        h->pipe_edge_cap = ew;
-        h->pipe_sync_cap = sw;
-        h->pipe_tag_base = 0;  // a fresh buffer: zero it before use
-    }
-    if (!h->h_err) {
-        if (hipHostMalloc(&h->h_err, sizeof(unsigned), hipHostMallocDefault) != hipSuccess) {
-            h->h_err = nullptr;
-            *rc = fail(GOLHIP_ENOMEM, "resident error word");
-            return 0;
-        }
-        *h->h_err = 0;
-    }
-    if (!take_guard(h, rc, count_last && run == left)) return 0;
-    const bool count = count_last && run == left;
-    hipError_t e = count ? hipMemsetAsync(h->d_scalars, 0, sizeof(unsigned long long), h->stream) : hipSuccess;
-    if (e == hipSuccess) e = hipMemsetAsync(h->pipe_sync, 0, (size_t)sw * 4, h->stream);
-    p.src = h->cur_rows();
-    p.dst = h->prev_rows();
-    p.edge = h->pipe_edge;
-    p.error = h->pipe_sync;
-    p.econs = h->pipe_sync + 1;
-    // edge tags: this launch's are above every tag already in the buffer
-    // (turn numbers restart at 1 each launch); on a wrap the buffer is zeroed
-    if ((uint64_t)h->pipe_tag_base + (uint64_t)run + 1 >= 0xFFFFFFFFull || h->pipe_tag_base == 0) {
-        if (e == hipSuccess) e = hipMemsetAsync(h->pipe_edge, 0, (size_t)h->pipe_edge_cap * 4, h->stream);
-        h->pipe_tag_base = 1;
-    }
-    p.tag_base = h->pipe_tag_base;
-    h->pipe_tag_base += (uint32_t)run + 1;
-    p.alive = count ? h->d_scalars : nullptr;
-    p.trace = h->d_trace;
-    p.timeout_ticks = h->persist_timeout_ticks;
-    p.turns = (int)run;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (e == hipSuccess && (h->flags & GOLHIP_FLAG_TIMING)) {
-        e0 = take_event(h);
-        e1 = take_event(h);
-        if (e0 && e1) e = hipEventRecord(e0, h->stream);
-    }
-    if (e == hipSuccess) e = golk::launch_pipe(p, wpl, h->stream);
-    if (e == hipSuccess && e1) {
-        e = hipEventRecord(e1, h->stream);
-        h->ev_pending.push_back({e0, e1, 1});
-    }
-    if (e == hipSuccess) e = hipMemcpyAsync(h->h_err, h->pipe_sync, sizeof(unsigned), hipMemcpyDeviceToHost, h->stream);
-    if (e != hipSuccess) {
-        *rc = fail(GOLHIP_EHIP, "resident LDS turn-pipeline launch: %s", hipGetErrorString(e));
-        return 0;
-    }
-    h->persist_pending = true;
-    h->cur ^= 1;
-    h->last_variant = 5;
-    h->turns += run;
-    h->persist_turns += run;
-    h->persist_launches++;
-    h->pipe_launches++;
-    if (count) h->alive_turn = h->turns;
-    return run;
-}
-
 // Torus: all `left` turns as one K1r launch (under the step guard, like
 // K1p); returns the turns run (0 if K1r does not apply).
 int64_t try_lds(golhip_t h, int64_t left, bool count_last, int *rc) {
@@ -1293,8 +1162,6 @@ int64_t try_lds(golhip_t h, int64_t left, bool count_last, int *rc) {
 int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     *rc = GOLHIP_OK;
     if (!persist_on(h) || h->W % 32 != 0 || !h->torus()) return 0;
-    if (int64_t n = try_pipe(h, left, count_last, rc)) return n;
-    if (*rc) return 0;
     if (int64_t n = try_lds(h, left, count_last, rc)) return n;
     if (*rc) return 0;
     const int wpl = wpl_for(h);
@@ -1748,8 +1615,6 @@ int golhip_destroy(golhip_t h) {
     HIP_RC(hipFree(h->d_trace));
     HIP_RC(hipFree(h->backup));
     HIP_RC(hipFree(h->lds_edge));
-    HIP_RC(hipFree(h->pipe_edge));
-    HIP_RC(hipFree(h->pipe_sync));
     if (h->h_err) HIP_RC(hipHostFree(h->h_err));
     if (h->skew_err) HIP_RC(hipHostFree(h->skew_err));
     if (h->xport_host) HIP_RC(hipHostFree(h->xport_host));
@@ -1922,11 +1787,6 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     if (!strcmp(key, "lds_band")) {
         if (value < -1 || value > 1) return fail(GOLHIP_EINVAL, "lds_band %lld", (long long)value);
         h->lds_band = (int)value;
-        return GOLHIP_OK;
-    }
-    if (!strcmp(key, "lds_pipe")) {
-        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "lds_pipe %lld", (long long)value);
-        h->lds_pipe = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "lds_depth")) {
@@ -2182,7 +2042,6 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     const int64_t step_launches0 = h->step_launches, step_turns0 = h->step_turns;
     const int64_t skew_launches0 = h->skew_launches;
     const int64_t skew_half_launches0 = h->skew_half_launches, lds_launches0 = h->lds_launches;
-    const int64_t pipe_launches0 = h->pipe_launches;
     const size_t ev0 = h->ev_pending.size();
     const int64_t halo_exchanges0 = h->halo_exchanges, halo_bytes0 = h->halo_bytes;
     int rc = step_locked(h, nturns, want_flips);
@@ -2212,7 +2071,6 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     h->skew_launches = skew_launches0;
     h->skew_half_launches = skew_half_launches0;
     h->lds_launches = lds_launches0;
-    h->pipe_launches = pipe_launches0;
     h->halo_exchanges = halo_exchanges0;
     h->halo_bytes = halo_bytes0;
     if (h->ev_pending.size() >= ev0) {  // the abandoned attempt's launch timings (unless drained meanwhile)
@@ -2564,7 +2422,6 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     out->overlap_launches = 0;
     out->skew_half_launches = h->skew_half_launches;
     out->lds_launches = h->lds_launches;
-    out->pipe_launches = h->pipe_launches;
     out->words_per_lane = h->W % 32 == 0 ? wpl_for(h) : 0;
     out->persist_depth = h->W % 32 == 0 ? persist_depth_for(h, wpl_for(h)) : 0;
     return GOLHIP_OK;
@@ -2608,7 +2465,6 @@ int golhip_perf_reset(golhip_t h) {
     h->halo_ms = 0;
     h->skew_half_launches = 0;
     h->lds_launches = 0;
-    h->pipe_launches = 0;
     return GOLHIP_OK;
 }
 

@@ -61,7 +61,6 @@ class Perf(ctypes.Structure):
         ("overlap_launches", ctypes.c_int64),
         ("skew_half_launches", ctypes.c_int64),
         ("lds_launches", ctypes.c_int64),
-        ("pipe_launches", ctypes.c_int64),
     ]
 
     def as_dict(self) -> dict:

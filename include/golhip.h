@@ -91,9 +91,6 @@ typedef struct golhip_perf {
     int64_t skew_half_launches; /* of skew_launches, those on half-wave tiles    */
     int64_t lds_launches;     /* of persist_launches, those that ran resident LDS
                                  bands (gol_lds_band_kernel, kernel_variant 4)  */
-    int64_t pipe_launches;    /* of persist_launches, those that ran the resident
-                                 LDS turn pipeline (gol_lds_pipe_kernel,
-                                 kernel_variant 5)                              */
 } golhip_perf_t;
 
 /* ---- library ---------------------------------------------------------- */
@@ -163,10 +160,6 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * whole waves twice or more, else 8; or 8, 16) and
  * "lds_wg_cu" (1 or 2): waves per workgroup and bands per CU; "lds_pre" (2): a full super-step's
  * first turns run on the rows that need no halo while the halos travel;
- * "lds_pipe" (default 0): 1 runs the resident LDS turn pipeline
- * (gol_lds_pipe_kernel) on tori 2048, 4096 or 8192 cells wide whose bands fit
- * one workgroup's LDS, under the resident guard (measured slower than the LDS
- * bands);
  * "resident_fault" (0, test hook: refused without GOLHIP_TEST_HOOKS=1): the
  * resident kernels' band / workgroup 0 never reports, so its neighbours'
  * bounded waits time out and the step is restored and re-run;

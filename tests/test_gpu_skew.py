@@ -227,17 +227,19 @@ def test_skew_half_tiles_rccl_ring_and_strips(coracle, W, H):
 
 def test_default_plans_by_board_size():
     """The default plan: half-wave tiles at 16384^2 (configs[1]: 4.5 instead
-    of 5 waves a row), full tiles at 65536^2, and the resident kernel for tori
-    whose K1w stacks would not fill the CUs (8192^2)."""
+    of 5 waves a row) with 16-turn launches (its bands are mostly ramp),
+    full tiles and 20-turn launches at 65536^2, and the resident kernel for
+    tori whose K1w stacks would not fill the CUs (8192^2)."""
     with golhip.Board(16384, 16384) as b:
         b.fill_random(0x5EED0001)
-        b.step(40)
+        b.step(32)
         p = b.perf()
-        assert p["skew_launches"] == 2 and p["skew_half_launches"] == 2
+        assert p["skew_launches"] == 2 and p["skew_half_launches"] == 2 and p["step_turns"] == 32
     with golhip.Board(65536, 4096) as b:
         b.fill_random(0x5EED0002)
         b.step(20)
-        assert b.perf()["skew_half_launches"] == 0
+        p = b.perf()
+        assert p["skew_half_launches"] == 0 and p["skew_launches"] == 1
     with golhip.Board(8192, 8192) as b:
         b.fill_random(0x5EED0003)
         b.step(64)
