@@ -135,6 +135,8 @@ struct LdsBandArgs {
     int stride;            // LDS words per row: lds_band_stride (Ww; pairs Ww + 8, two planes)
     int rt_stride;         // 1: the runtime-stride kernel even where this stride is instantiated
     int fault;             // tests: band 0 never publishes, so its neighbours' waits time out
+    int age;               // % row share of each younger wave rank against the next older one (100: equal
+                           // runs; applies where whole waves fill a row's pairs, PC % 64 == 0)
     int pre;               // > 0: full super-steps run their first `pre` turns on the interior rows
                            //      while the halos travel (lds_pre)
     unsigned long long *trace;  // nullable: [0..3] += ticks in compute, publish, wait, halo load; [4] += workgroups

@@ -1475,6 +1475,27 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
             tr_t = now;
         }
     };
+    long long bar_ticks = 0, bar_turns = 0;  // option trace
+    // age-weighted runs (PC % 64 == 0): cumulative weights of runs [0, k) and
+    // [0, k + 1) for this wave's run k, and of all K runs
+    int run_m0 = 0, run_m1 = 65536;  // this thread's run: row-share bounds in [0, 1], 16-bit fixed point
+    if (p.age != 100) {
+        const int kme = (int)threadIdx.x / P;
+        int wgt = 1 << 12, w0 = 0, w1 = 0, wsum = 0;
+        for (int k = 0, rank = 0; k < K; ++k) {
+            const int r = (k * P / 64) / 4;  // the age rank of the wave of run k's first column (4 SIMDs)
+            for (; rank < r; ++rank) wgt = wgt * p.age / 100;
+            if (k == kme) w0 = wsum;
+            wsum += max(wgt, 1);
+            if (k == kme) w1 = wsum;
+        }
+        run_m0 = (int)(((int64_t)w0 << 16) / wsum);
+        run_m1 = kme >= K - 1 ? 65536 : (int)(((int64_t)w1 << 16) / wsum);
+        if constexpr (PC > 0 && PC % 64 == 0) {  // (a wave's lanes share their run)
+            run_m0 = __builtin_amdgcn_readfirstlane(run_m0);
+            run_m1 = __builtin_amdgcn_readfirstlane(run_m1);
+        }
+    }
     bool pending = false;  // lds_pre: our last edges are out, their flag not yet raised
     for (int j = 0; j < J; ++j) {
         const int Dj = min(D, p.turns - j * D);
@@ -1558,12 +1579,26 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
                 // a wave's lanes share k when whole waves fit a row: scalar run bounds
                 if constexpr (PC > 0 && PC % 64 == 0) k = __builtin_amdgcn_readfirstlane(k);
                 const int c = u - k * P;
-                const int v0 = k * len, v1 = min(v0 + len, n);
+                int v0 = k * len, v1 = min(v0 + len, n);
+                // age-weighted runs: the SIMD arbiter serves a SIMD's older waves
+                // first, so run k (the wave of its first column: rank = wave / 4)
+                // gets (age / 100)^rank of the oldest rank's row share
+                if (p.age != 100) {  // 16-bit fixed point (a scalar division costs ~40 instructions)
+                    v0 = (n * run_m0 + 32768) >> 16;
+                    v1 = (n * run_m1 + 32768) >> 16;
+                }
                 if (v0 >= v1) continue;
                 if (v0 < n0) run_rows(Ab, Bb, lo0 + v0, lo0 + min(v1, n0), c);
                 if (v1 > n0) run_rows(Ab, Bb, lo1 + max(v0, n0) - n0, lo1 + v1 - n0, c);
             }
-            __syncthreads();
+            if (p.trace) {  // (option trace: each wave's ticks in the turn barrier)
+                const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+                __syncthreads();
+                bar_ticks += (long long)__builtin_amdgcn_s_memrealtime() - t0;
+                ++bar_turns;
+            } else {
+                __syncthreads();
+            }
         };
         // Edge rows of generation (j + 1) D from F: [D, 2D) (side 0) and [h, h + D)
         // (side 1) to slot (j + 1) & 1, write-through; signal() waits for them
@@ -1723,6 +1758,10 @@ __global__ __launch_bounds__(NT) void gol_lds_band_kernel(LdsBandArgs p) {
     if (p.trace && threadIdx.x == 0) {
         for (int k = 0; k < 4; ++k) atomicAdd(&p.trace[k], (unsigned long long)tr[k]);
         atomicAdd(&p.trace[4], 1ull);
+    }
+    if (p.trace && lane == 0 && blockIdx.x < 1024) {  // (workgroup, wave): barrier ticks, turns
+        p.trace[8 + 2 * (blockIdx.x * 64 + w)] = (unsigned long long)bar_ticks;
+        p.trace[8 + 2 * (blockIdx.x * 64 + w) + 1] = (unsigned long long)bar_turns;
     }
     // the band's last generation: rows [D, D + h) of A -> board rows [r0, r0 + h)
     uint32_t cnt = 0;

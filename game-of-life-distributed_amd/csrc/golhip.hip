@@ -135,6 +135,7 @@ struct golhip {
     int lds_stride = 1;             // option "lds_stride": K1r LDS rows at a compile-time stride where instantiated
     int resident_fault = 0;         // option "resident_fault" (tests): K1r band 0 / K1p workgroup 0 never report
                                     // (their neighbours' bounded waits time out: the restore-and-re-run path)
+    int lds_age = 0;                // option "lds_age": K1r run rows of a younger wave rank, % of the older's (0: plan)
     int lds_pre = 2;                // option "lds_pre": K1r interior-first turns while the halos travel
                                     // (profiles/r4pre: 8192^2 31.4 -> 33.9 TCUPS at 2; 1: 33.2, 3: 33.1, 4: 32.3)
     uint32_t *lds_edge = nullptr;   // K1r edge rows (golk::lds_band_edge_words)
@@ -1082,6 +1083,12 @@ bool lds_fits(golhip_t h, int wpl, golk::LdsBandArgs *out) {
         out->rt_stride = h->lds_stride ? 0 : 1;
         out->fault = h->resident_fault;
         out->pre = h->lds_pre;
+        // the SIMD arbiter's age order, where whole waves share a run (a row's
+        // pairs a multiple of 64): 16 waves (4 ranks) 60 %, 8 waves 70 %
+        // (profiles/r5z: 8192^2 40.2 -> 43.8 TCUPS, 4096^2 17.1 -> 17.8); runs
+        // that straddle waves stay equal (5120^2 +1 % at 80, 2048^2 -5 %)
+        const bool whole = wpl == 2 && P2 % 64 == 0;
+        out->age = h->lds_age > 0 ? h->lds_age : !whole ? 100 : waves == 16 ? 60 : 70;
     }
     return true;
 }
@@ -1803,6 +1810,11 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     if (!strcmp(key, "lds_wg_cu")) {
         if (value < 1 || value > 2) return fail(GOLHIP_EINVAL, "lds_wg_cu %lld", (long long)value);
         h->lds_wg_cu = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "lds_age")) {
+        if (value != 0 && (value < 25 || value > 400)) return fail(GOLHIP_EINVAL, "lds_age %lld", (long long)value);
+        h->lds_age = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "lds_pre")) {

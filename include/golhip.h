@@ -158,7 +158,10 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * (1): consecutive bands on one XCD; "lds_stride" (1; 0: the runtime-stride kernel): LDS rows at a
  * compile-time stride where one is instantiated; "lds_waves" (0 = plan: 16 where a row's pairs fill
  * whole waves twice or more, else 8; or 8, 16) and
- * "lds_wg_cu" (1 or 2): waves per workgroup and bands per CU; "lds_pre" (2): a full super-step's
+ * "lds_wg_cu" (1 or 2): waves per workgroup and bands per CU; "lds_age" (0 = plan: 60 at 16
+ * waves and 70 at 8 where a row's pairs fill whole waves, else 100; 25-400): the rows of a
+ * turn's run for each younger wave rank of a SIMD, % of the next older rank's (the arbiter
+ * serves older waves first); "lds_pre" (2): a full super-step's
  * first turns run on the rows that need no halo while the halos travel;
  * "resident_fault" (0, test hook: refused without GOLHIP_TEST_HOOKS=1): the
  * resident kernels' band / workgroup 0 never reports, so its neighbours'

@@ -11,6 +11,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "game-of-life-distributed_amd")]
 import golhip  # noqa: E402
@@ -57,4 +59,12 @@ for rep in range(a.reps):
                         names = ["compute", "publish", "wait", "halo"]
                         vals = [t["band_ticks"], t["max_band_ticks"], t["wait_ticks"], t["kernel_ticks"]]
                         rec["us_per_superstep"] = {n: round(v / wgs / ss / 100, 3) for n, v in zip(names, vals)}
+                        # per wave: ticks in the turn barriers (slots 8.. of the trace)
+                        tw = b.persist_trace_waves(min(wgs, 1024)).astype(np.int64)
+                        bt, bn = tw[:, :, 0], tw[:, :, 1]
+                        live = bn > 0
+                        if live.any():
+                            rec["barrier"] = {
+                                "us_per_turn_per_wave": round(float((bt[live] / bn[live]).mean()) / 100, 3),
+                                "share_of_compute": round(float(bt[live].mean()) / max(1.0, vals[0] / wgs), 3)}
                     print(json.dumps(rec), flush=True)

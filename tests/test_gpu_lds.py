@@ -126,6 +126,12 @@ def test_lds_band_then_other_kernels(coracle):
                                       (5120, 640, {"lds_stride": 0}),
                                       (8192, 1024, {"lds_waves": 16}),       # 16 waves a workgroup
                                       (8192, 1024, {"lds_waves": 8}),        # 8192 wide on 8 (auto: 16)
+                                      (8192, 1000, {"lds_age": 70}),         # age-weighted runs
+                                      (8192, 1000, {"lds_age": 100}),        # equal runs (auto: 60)
+                                      (4096, 3001, {"lds_age": 130}),
+                                      (8192, 2048, {"lds_age": 40, "lds_waves": 8}),
+                                      (5120, 1280, {"lds_age": 60}),         # runs straddling waves
+                                      (2048, 1000, {"lds_age": 150}),        # two runs a wave
                                       (5120, 1280, {"lds_waves": 16}),
                                       (8192, 2048, {"lds_wg_cu": 2}),        # two bands a CU
                                       (4096, 3000, {"lds_wg_cu": 2})])
