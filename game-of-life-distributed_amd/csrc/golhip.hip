@@ -606,12 +606,12 @@ int exchange_rccl(golhip_t h, int depth, hipStream_t st) {
         HIP_OR_FAIL(hipMemcpyAsync(b + (int64_t)p.recv_bottom_row * h->Ww, hb + 3 * n, bytes, hipMemcpyHostToDevice, st));
         HIP_OR_FAIL(hipStreamSynchronize(st));  // the pinned blocks are reused by the next exchange
     } else {
-    NCCL_OR_FAIL(ncclGroupStart());
-    NCCL_OR_FAIL(ncclSend(b + (int64_t)p.send_up_row * h->Ww, n, ncclUint32, p.prev_rank, h->comm, st));
-    NCCL_OR_FAIL(ncclRecv(b + (int64_t)p.recv_bottom_row * h->Ww, n, ncclUint32, p.next_rank, h->comm, st));
-    NCCL_OR_FAIL(ncclSend(b + (int64_t)p.send_down_row * h->Ww, n, ncclUint32, p.next_rank, h->comm, st));
-    NCCL_OR_FAIL(ncclRecv(b + (int64_t)p.recv_top_row * h->Ww, n, ncclUint32, p.prev_rank, h->comm, st));
-    NCCL_OR_FAIL(ncclGroupEnd());
+        NCCL_OR_FAIL(ncclGroupStart());
+        NCCL_OR_FAIL(ncclSend(b + (int64_t)p.send_up_row * h->Ww, n, ncclUint32, p.prev_rank, h->comm, st));
+        NCCL_OR_FAIL(ncclRecv(b + (int64_t)p.recv_bottom_row * h->Ww, n, ncclUint32, p.next_rank, h->comm, st));
+        NCCL_OR_FAIL(ncclSend(b + (int64_t)p.send_down_row * h->Ww, n, ncclUint32, p.next_rank, h->comm, st));
+        NCCL_OR_FAIL(ncclRecv(b + (int64_t)p.recv_top_row * h->Ww, n, ncclUint32, p.prev_rank, h->comm, st));
+        NCCL_OR_FAIL(ncclGroupEnd());
     }
     if (e1) {
         HIP_OR_FAIL(hipEventRecord(e1, st));
@@ -2019,7 +2019,7 @@ int step_locked(golhip_t h, int64_t nturns, int32_t want_flips) {
         const HaloRun hr = halo_next(depth_cap(h, true), sched_rows(h), persist_on(h), left - tail);
         const int d = hr.d, k = hr.k;
         if (int rc = exchange_rccl(h, k * d, h->stream)) return rc;
-            int prc = GOLHIP_OK;
+        int prc = GOLHIP_OK;
         if (try_persist_halo(h, d, k, left - k * d == 0, &prc)) {
             left -= (int64_t)k * d;
             continue;
