@@ -736,8 +736,14 @@ bool skew_plan(golhip_t h, int depth, int wpl, const golk::StepArgs &a, golk::Sk
     // (round-3 skew_young sweeps, scripts/sweep_opts.py): two words per lane
     // 66-70 %, quads at depth 9 76-82 %.
     // half-wave-tile plans (16-turn launches of ramp-dominated bands): 60 %
-    // (16384^2 87.6 vs 86.4 at 68, 83.7 at 55; profiles/r6b)
-    const int young = h->skew_young > 0 ? h->skew_young : wpl == 4 ? 78 : sk->half ? 60 : 68;
+    // (16384^2 87.6 vs 86.4 at 68, 83.7 at 55; profiles/r6b); whole tori on
+    // full tiles 70 % (65536^2 128.7 vs 127.5-127.8 at 68, 126.4 at 74;
+    // profiles/r6i); ring strips 68 % (their sweep is within its noise, r6d)
+    const int young = h->skew_young > 0 ? h->skew_young
+                      : wpl == 4             ? 78
+                      : sk->half             ? 60
+                      : a.in.wrap > 0        ? 70
+                                             : 68;
     for (int q = 0; q < 8; ++q) sk->wgt[q] = (q < sy && q * sk->tx >= 4) ? young : 100;
     sk->prio_young = h->skew_prio;
     sk->error = h->skew_err_dev;

@@ -139,7 +139,7 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * most 8 turns a launch and needs width % 128 == 0); "skew" (default 1):
  * skewed band stacks (gol_skew_kernel) for per-launch steps of a torus or a
  * ring strip when they fill the CUs (2: always, 0: off); "skew_young"
- * (0 = by kernel: 68 %, quads 78 %, half-wave tiles 60 %): band height of waves 4..7 relative to
+ * (0 = by kernel: 68 %, whole tori 70 %, quads 78 %, half-wave tiles 60 %): band height of waves 4..7 relative to
  * waves 0..3; "skew_hcap" (-1 = 3 D / 4): rows a stack's bottom band gives
  * up (it computes its own drain); "skew_tx" (0 = plan, 1, 2): tiles across
  * a stack; "skew_half" (0 = when they need fewer wave-rows, 1 = whenever
