@@ -8,7 +8,8 @@ wls=${@:-65536 16384 262144}
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp
 for wl in $wls; do
-  args="$GRAFT_REPO_ROOT/bench.py --workload $wl --steps 2 --warmup 1 --warmup-seconds 0 --no-cpu-baseline"
+  # (--no-configs3: the default line's configs3 block would mix 262144^2 dispatches into 65536^2's)
+  args="$GRAFT_REPO_ROOT/bench.py --workload $wl --steps 2 --warmup 1 --warmup-seconds 0 --no-cpu-baseline --no-configs3"
   timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex gol_ -d $out/pmc_${wl}_fetch -o run --output-format csv -- python3 $args > $out/pmc_${wl}_fetch.log 2>&1 || { tail $out/pmc_${wl}_fetch.log; exit 1; }
   timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex gol_ -d $out/pmc_${wl}_write -o run --output-format csv -- python3 $args > $out/pmc_${wl}_write.log 2>&1 || { tail $out/pmc_${wl}_write.log; exit 1; }
   timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex gol_ -d $out/pmc_${wl}_sq -o run --output-format csv -- python3 $args > $out/pmc_${wl}_sq.log 2>&1 || { tail $out/pmc_${wl}_sq.log; exit 1; }
