@@ -12,7 +12,7 @@ if [ "$1" = "--" ]; then
   shift
   args="$GRAFT_REPO_ROOT/$*"
 else
-  args="$GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --warmup-seconds 0 --no-cpu-baseline $@"
+  args="$GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --warmup-seconds 0 --no-cpu-baseline --no-configs3 $@"
 fi
 tag=$(echo "$@" | tr -c 'a-zA-Z0-9\n' '_')
 mkdir -p $out
