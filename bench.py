@@ -96,6 +96,9 @@ def parse():
     ap.add_argument("--stage-timeout", type=float, default=300.0,
                     help="multi-rank runs: the longest one stage (comm init, parity step, warmup, timed "
                          "steps) may take before the watchdog ends the rank with a JSON error line")
+    ap.add_argument("--ring", action="store_true",
+                    help="one GPU: run the board as a one-rank RCCL ring (force_halo) through the multi-rank path "
+                         "(gloo control plane, golhip_comm_init, halo exchanges, the library's allreduce)")
     ap.add_argument("--no-configs3", dest="configs3", action="store_false",
                     help="default workload: skip the configs[3] block (262144^2 x 100 turns over the same ranks)")
     ap.add_argument("--configs3-warmup-seconds", type=float, default=1.0)
@@ -294,8 +297,8 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str, 
     spw = 9.0 + 8.0 / wpl
     words = rows * ((W + 31) // 32)
     tpl = kturns / launches
-    if depth is None:
-        depth = int(round(tpl)) if abs(tpl - round(tpl)) < 1e-9 else f"{tpl:.2f} turns a launch on average"
+    if depth is None and abs(tpl - round(tpl)) < 1e-9:
+        depth = int(round(tpl))  # every launch fused the same turns
     slots = words * tpl / 64.0 * spw
     achieved = slots / avg_s / 1e9 if avg_s > 0 else None
     alg_bytes = W * rows * tpl * ALG_BYTES_PER_UPDATE
@@ -306,7 +309,10 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str, 
         "unit": "Gslot/s (wave64 VALU issue slots)",
         "frac": round(achieved / VALU_PEAK_GSLOTS, 4) if achieved else None,
         "traffic": None,
-        "kernel": f"{kname}<{depth}, {wpl}>",
+        # the instantiation when every launch fused the same turns, else the
+        # family (turns_per_launch holds the average)
+        "kernel": f"{kname}<{depth}, {wpl}>" if depth is not None else kname,
+        "words_per_lane": wpl,
         "launch_time": "HIP events on the engine stream around the timed region / launches (boundaries included)",
         "avg_launch_ms": round(avg_s * 1e3, 5),
         "launches": launches,
@@ -779,23 +785,45 @@ def run_main(a) -> None:
 
 
 class RankEnv:
-    """One rank's view of the job: its rank, device and the torch.distributed
-    group (None at N = 1), and the few collectives bench.py needs around the
-    timed region (none of them on the data path: the halo ring is the
-    library's own RCCL communicator)."""
+    """One rank's view of the job: its rank, device and host control plane,
+    and the few collectives bench.py needs around the timed region.
+
+    The control plane is a **gloo** process group on CPU tensors (rank 0's
+    RCCL unique id, the parity digest sum, the max-over-ranks time, the
+    warmup count, the per-rank rows, barriers): none of it is on the data
+    path, and with gloo the library's own RCCL communicator (golhip_comm_init:
+    the halo ring and golhip_alive_count_global's allreduce) is the only GPU
+    communication of the job -- no second communicator per device.  The
+    one-GPU ring tests (tests/test_gpu_bench_ring.py) subclass this class and
+    override ring_init alone, so every other line here is what the driver's
+    multi-GPU run executes."""
 
     def __init__(self, a, world: int, rank: int, local: int):
         self.a, self.world, self.rank, self.local = a, world, rank, local
-        self.wd = Watchdog(a, rank) if world > 1 else None
+        self.ringed = world > 1 or bool(getattr(a, "ring", False))
+        self.wd = Watchdog(a, rank) if self.ringed else None
         import torch
         self.torch = torch
         torch.cuda.set_device(local)
         self.dist = None
-        if world > 1:
-            import torch.distributed as dist
-            self.stage("process group init (RCCL)")
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-            self.dist = dist
+        if self.ringed:
+            # RCCL's own warnings on stderr: a failed comm init or exchange is
+            # diagnosable from the run's log (the driver keeps stderr)
+            os.environ.setdefault("NCCL_DEBUG", "WARN")
+            self.init_control()
+
+    def init_control(self) -> None:
+        """The gloo process group (host control plane).  A launcher's
+        MASTER_ADDR / MASTER_PORT when present, else (one rank, --ring) a
+        local port on 127.0.0.1."""
+        import torch.distributed as dist
+        self.stage("control plane init (gloo process group)")
+        if "MASTER_ADDR" in os.environ and "MASTER_PORT" in os.environ:
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+        else:
+            dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{free_port()}", rank=self.rank,
+                                    world_size=self.world)
+        self.dist = dist
 
     def stage(self, name: str) -> None:  # bound the next multi-rank stage
         if self.wd is not None:
@@ -814,8 +842,12 @@ class RankEnv:
 
     def ring_init(self, board, tag: str = "") -> None:
         """This rank's strip joins the halo ring: the library's own RCCL
-        communicator (rank 0's unique id broadcast over the process group)."""
+        communicator (rank 0's unique id broadcast over the control plane).
+        One rank (--ring): the whole board as a one-rank RCCL ring
+        (force_halo), the exchanges and the allreduce of the N-rank run."""
         self.stage(tag + "golhip_comm_init (ncclCommInitRank + strip-row allreduce)")
+        if self.world == 1:
+            board.set_option("force_halo", 1)
         board.comm_init(self.unique_id(), self.world, self.rank)
 
     def barrier(self, board) -> None:
@@ -824,24 +856,27 @@ class RankEnv:
         board.sync()
         self.torch.cuda.synchronize()
 
+    def _cpu(self, x, dtype):
+        return self.torch.tensor([x], dtype=dtype)  # gloo: CPU tensors
+
     def gsum(self, x: int) -> int:  # mod 2^64 over ranks
         if self.dist is None:
             return x % (1 << 64)
-        t = self.torch.tensor([x - (1 << 64) if x >= (1 << 63) else x], dtype=self.torch.int64, device="cuda")
+        t = self._cpu(x - (1 << 64) if x >= (1 << 63) else x, self.torch.int64)
         self.dist.all_reduce(t)
         return int(t.item()) % (1 << 64)
 
     def gmax(self, x: float) -> float:
         if self.dist is None:
             return x
-        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        t = self._cpu(x, self.torch.float64)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
     def bcast(self, x: int) -> int:  # rank 0's value
         if self.dist is None:
             return x
-        t = self.torch.tensor([x], dtype=self.torch.int64, device="cuda")
+        t = self._cpu(x, self.torch.int64)
         self.dist.broadcast(t, src=0)
         return int(t.item())
 
@@ -899,11 +934,14 @@ def measure(a, env, workload: int, steps: int, warmup: int, warmup_seconds: floa
     try:
         board.set_tb_depth(a.tb_depth)
         board.set_rows_per_wave(a.rows_per_wave)
+        if a.option:  # A/B runs: the plan's tuning knobs need the library's consent
+            os.environ.setdefault("GOLHIP_TUNING", "1")
         for kv in a.option:
             k, v = kv.split("=")
             board.set_option(k, int(v))
         comm = None
-        if world > 1:
+        ringed = getattr(env, "ringed", world > 1)
+        if ringed:
             env.ring_init(board, tag)
             comm = board.comm_info()
             if comm["nranks"] != world or comm["rank"] != rank:
@@ -916,7 +954,9 @@ def measure(a, env, workload: int, steps: int, warmup: int, warmup_seconds: floa
         board.step(tps)
         board.sync()
         digest = env.gsum(board.board_hash())
-        alive = env.gsum(board.alive_count()[0])
+        # the ring's own allreduce (golhip_alive_count_global: ncclAllReduce on
+        # the library's communicator), checked against the fixture every run
+        alive = board.alive_count(global_sum=ringed)[0]
         parity = {"turns": tps, "digest": f"{digest:016x}", "alive": alive}
         try:
             with open(FULLSIZE) as f:
@@ -951,7 +991,7 @@ def measure(a, env, workload: int, steps: int, warmup: int, warmup_seconds: floa
         if env.dist is not None:
             env.dist.barrier()
         perf = board.perf()
-        alive_end, at_turn = board.alive_count(global_sum=world > 1)
+        alive_end, at_turn = board.alive_count(global_sum=ringed)
         me = {"rank": rank, "row0": row0, "rows": rows, "comm": comm, "seconds": round(dt_rank, 6),
               "region_ms": round(region_ms, 3), "launches": perf["step_launches"] + perf["persist_launches"],
               "words_per_lane": perf["words_per_lane"], "halo_exchanges": perf.get("halo_exchanges", 0),
@@ -964,7 +1004,9 @@ def measure(a, env, workload: int, steps: int, warmup: int, warmup_seconds: floa
             "config": {"workload": wl["desc"], "board": [H, W], "rows_per_rank": rows, "turns_per_step": tps,
                        "tb_depth": a.tb_depth, "rows_per_wave": perf["rows_per_wave"],
                        "words_per_lane": perf["words_per_lane"],
-                       "parallelism": f"row strips x{world} (RCCL halo ring)" if world > 1 else "single GPU torus",
+                       "parallelism": f"row strips x{world} (RCCL halo ring)" if world > 1 else
+                       "one-rank RCCL ring (force_halo)" if ringed else "single GPU torus",
+                       "control_plane": "gloo process group (CPU tensors)" if ringed else None,
                        # halo traffic of this rank over the timed steps (deep halos: one
                        # exchange of k x depth rows feeds k launches)
                        "halo_exchanges": perf.get("halo_exchanges", 0),

@@ -189,9 +189,17 @@ class Chan {
     int try_recv(T &out) {
         if (cap_ == 0) {
             // a receiver blocked in recv0 holds recv_mu_ for its whole wait: then
-            // the offer (if any) is that receiver's, and this call must not block
-            std::unique_lock<std::mutex> rg(recv_mu_, std::try_to_lock);
-            if (!rg.owns_lock()) return closed_a_.load(std::memory_order_acquire) ? -1 : 0;
+            // the offer (if any) is that receiver's, and this call must not
+            // block.  Any other holder (a concurrent try_recv) holds it for a
+            // few instructions: retry rather than report "empty" while a sender
+            // may be parked with a value (Go's select-with-default fails only
+            // when no sender is ready).
+            std::unique_lock<std::mutex> rg(recv_mu_, std::defer_lock);
+            for (int i = 0; !rg.try_lock(); ++i) {
+                if (recv_waiting_.load(std::memory_order_acquire) > 0 || i == 4096)
+                    return closed_a_.load(std::memory_order_acquire) ? -1 : 0;
+                __builtin_ia32_pause();
+            }
             const uint64_t q = box_.seq.load(std::memory_order_acquire);
             if (q & 1) {
                 out = std::move(box_.value);
@@ -239,8 +247,10 @@ class Chan {
     }
     bool recv0(T &out) {
         std::lock_guard<std::mutex> rg(recv_mu_);
+        recv_waiting_.fetch_add(1, std::memory_order_release);  // (try_recv: this receiver owns the next offer)
         wait0([&] { return (box_.seq.load(std::memory_order_acquire) & 1) || closed_a_.load(std::memory_order_acquire); },
               recv_sleepers0_, recv_cv_);
+        recv_waiting_.fetch_sub(1, std::memory_order_release);
         const uint64_t q = box_.seq.load(std::memory_order_acquire);
         if (!(q & 1)) return false;  // closed, nothing offered
         out = std::move(box_.value);
@@ -311,6 +321,7 @@ class Chan {
     } box_;
     alignas(64) std::atomic<int> send_sleepers0_{0};
     alignas(64) std::atomic<int> recv_sleepers0_{0};
+    std::atomic<int> recv_waiting_{0};     // receivers inside recv0 (they own the next offer)
 };
 
 // Host-mirror options beyond the Go API (all default to the reference's

@@ -15,6 +15,9 @@ constexpr int64_t kResidentMaxTurns = int64_t(1) << 30;
 constexpr int kResidentMaxDepth = 64;
 static_assert(kResidentMaxTurns + 2 * kResidentMaxDepth < INT32_MAX, "resident turn arithmetic must fit in int32");
 
-inline int64_t resident_turns(int64_t left) { return left < kResidentMaxTurns ? left : kResidentMaxTurns; }
+inline int64_t resident_turns(int64_t left, int64_t cap = kResidentMaxTurns) {
+    if (cap > kResidentMaxTurns || cap < 1) cap = kResidentMaxTurns;  // (a test hook lowers it, never raises it)
+    return left < cap ? left : cap;
+}
 
 }  // namespace golk

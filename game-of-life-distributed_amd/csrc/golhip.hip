@@ -160,6 +160,12 @@ struct golhip {
     uint32_t *backup = nullptr;
     bool guarded = false;
     bool guard_light = false;  // the guarded step is one source-keeping launch: its source is the copy
+    // the error word d_sync[0] is sticky over a guarded step: only its first
+    // resident launch clears it, so a later launch (steps past resident_max
+    // turns, a one-rank ring's rounds) can neither wipe an earlier timeout nor
+    // run on a drained board unnoticed (its waits see the word and drain too)
+    bool err_clear = true;
+    int64_t resident_max = golk::kResidentMaxTurns;  // turns a resident launch takes (test hook "resident_max_turns")
     int64_t persist_fallbacks = 0;
     int64_t persist_timeout_ticks = 100000000ll;  // 1 s at the 100 MHz s_memrealtime clock (option "persist_timeout_us")
     int auto_rpw[kNumDepths] = {};  // cache per depth index
@@ -890,10 +896,28 @@ bool test_hooks_env() {
     const char *v = getenv("GOLHIP_TEST_HOOKS");
     return v && !strcmp(v, "1");
 }
+// Result-neutral A/B knobs of the kernel plans: the
+// defaults are the plans the sweeps under profiles/ chose, and a product
+// caller has no reason to move them, so they need GOLHIP_TUNING=1 (or the
+// stronger GOLHIP_MEASUREMENT=1).  The product options without consent are
+// wpl, persistent, lds_band, skew, timing, persist_timeout_us, force_halo.
+constexpr const char *kTuningKeys[] = {
+    "persist_depth", "persist_waves", "dummy_rows", "paired_bands", "persist_half", "persist_wg_tx", "trace",
+    "cu_count", "fill_skip", "skew_young", "skew_hcap", "skew_prio", "skew_half", "skew_tx", "lds_depth",
+    "lds_waves", "lds_wg_cu", "lds_age", "lds_pre", "lds_stride", "lds_xcd"};
+bool tuning_env() {
+    const char *v = getenv("GOLHIP_TUNING");
+    return (v && !strcmp(v, "1")) || measurement_env();
+}
 // The consent-gated options, as golhip_build_info() reports them (the CPU
 // suite checks the list against the product contract).
 constexpr const char *kConsentInfo =
-    " CONSENT_MEASUREMENT=halo_skip,flip_debug:1-3 CONSENT_TEST_HOOKS=resident_fault,flip_debug:4,golhip_test_ring_init";
+    " CONSENT_MEASUREMENT=halo_skip,flip_debug:1-3"
+    " CONSENT_TEST_HOOKS=resident_fault,resident_max_turns,flip_debug:4,golhip_test_ring_init"
+    " CONSENT_TUNING=persist_depth,persist_waves,dummy_rows,paired_bands,persist_half,persist_wg_tx,trace,cu_count,"
+    "fill_skip,skew_young,skew_hcap,skew_prio,skew_half,skew_tx,lds_depth,lds_waves,lds_wg_cu,lds_age,lds_pre,"
+    "lds_stride,lds_xcd"
+    " PRODUCT_OPTIONS=wpl,persistent,lds_band,skew,timing,persist_timeout_us,force_halo";
 
 // After the stream has synchronised: the K1w spin-bound flag of the launches
 // it ran (reported by the call that ran them, then cleared).
@@ -910,6 +934,13 @@ int sync_stream(golhip_t h) {
     HIP_OR_FAIL(hipStreamSynchronize(h->stream));
     if (int rc = take_skew_err(h)) return rc;
     return check_persist(h);
+}
+
+// Test hook "resident_fault": 1 = every resident launch's band / workgroup 0
+// never reports, 2 = only the first launch of a guarded step (a transient
+// starvation: the step's later launches are healthy and must not hide it).
+int resident_fault_now(golhip_t h, bool first) {
+    return h->resident_fault == 1 || (h->resident_fault == 2 && first) ? 1 : 0;
 }
 
 // One resident launch of J super-steps of `depth` turns over the rows of
@@ -955,7 +986,10 @@ bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int w
         hipError_t e = hipMemsetAsync(h->d_scalars, 0, sizeof(unsigned long long), h->stream);
         if (e != hipSuccess) { *rc = fail(GOLHIP_EHIP, "memset: %s", hipGetErrorString(e)); return false; }
     }
-    hipError_t e = hipMemsetAsync(h->d_sync, 0, (size_t)(h->cu_count + 2) * sizeof(unsigned), h->stream);
+    const int e0w = h->err_clear ? 0 : 1;  // the error word is sticky over the guarded step
+    h->err_clear = false;
+    hipError_t e = hipMemsetAsync(h->d_sync + e0w, 0, (size_t)(h->cu_count + 2 - e0w) * sizeof(unsigned), h->stream);
+    const int fault = resident_fault_now(h, e0w == 0);
     p.base = base;
     p.base.alive = count ? h->d_scalars : nullptr;
     p.buf0 = h->buf[0];
@@ -967,7 +1001,7 @@ bool persist_launch(golhip_t h, golk::StepArgs base, int64_t J, int depth, int w
     p.progress = h->d_sync + 1;
     p.timeout_ticks = h->persist_timeout_ticks;
     p.trace = h->d_trace;
-    p.fault = h->resident_fault;
+    p.fault = fault;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (e == hipSuccess && (h->flags & GOLHIP_FLAG_TIMING)) {
         e0 = take_event(h);
@@ -1014,6 +1048,7 @@ int persist_depth_for(golhip_t h, int wpl) {
 bool take_guard(golhip_t h, int *rc, bool keeps_src = false) {
     *rc = GOLHIP_OK;
     if (h->guarded) return true;  // a step of several resident launches keeps its first copy
+    h->err_clear = true;          // the step's first resident launch clears the error word
     if (keeps_src) {
         h->guarded = true;
         h->guard_light = true;
@@ -1089,7 +1124,7 @@ bool lds_fits(golhip_t h, int wpl, golk::LdsBandArgs *out) {
         out->nt = nt;
         out->stride = stride;
         out->rt_stride = h->lds_stride ? 0 : 1;
-        out->fault = h->resident_fault;
+        out->fault = h->resident_fault != 0;
         out->pre = h->lds_pre;
         // the SIMD arbiter's age order, where whole waves share a run (a row's
         // pairs a multiple of 64): 16 waves (4 ranks) 60 %, 8 waves 70 %
@@ -1106,7 +1141,7 @@ bool lds_fits(golhip_t h, int wpl, golk::LdsBandArgs *out) {
 int64_t try_lds(golhip_t h, int64_t left, bool count_last, int *rc) {
     *rc = GOLHIP_OK;
     if (left < 2 || !(h->il == 0 || h->il == 2)) return 0;
-    const int64_t run = golk::resident_turns(left);  // 32-bit super-step arithmetic in the kernel
+    const int64_t run = golk::resident_turns(left, h->resident_max);  // 32-bit super-step arithmetic in the kernel
     const int wpl = h->il == 2 ? 2 : 1;
     golk::LdsBandArgs p{};
     if (!lds_fits(h, wpl, &p)) return 0;
@@ -1135,7 +1170,10 @@ int64_t try_lds(golhip_t h, int64_t left, bool count_last, int *rc) {
     if (!take_guard(h, rc, count_last && run == left)) return 0;
     const bool count = count_last && run == left;
     hipError_t e = count ? hipMemsetAsync(h->d_scalars, 0, sizeof(unsigned long long), h->stream) : hipSuccess;
-    if (e == hipSuccess) e = hipMemsetAsync(h->d_sync, 0, (size_t)(p.nb + 1) * sizeof(unsigned), h->stream);
+    const int e0w = h->err_clear ? 0 : 1;  // the error word is sticky over the guarded step
+    h->err_clear = false;
+    if (e == hipSuccess) e = hipMemsetAsync(h->d_sync + e0w, 0, (size_t)(p.nb + 1 - e0w) * sizeof(unsigned), h->stream);
+    p.fault = resident_fault_now(h, e0w == 0);
     p.src = h->cur_rows();
     p.dst = h->prev_rows();
     p.edge = h->lds_edge;
@@ -1182,7 +1220,7 @@ int64_t try_persist(golhip_t h, int64_t left, bool count_last, int *rc) {
     const int wpl = wpl_for(h);
     const int depth = persist_depth_for(h, wpl);
     if (depth < 4 || golk::persist_blocks_per_cu(depth, wpl, persist_nw_for(h, depth, wpl)) < 1) return 0;
-    int64_t J = golk::resident_turns(left) / depth;  // (32-bit super-step counts in the kernel)
+    int64_t J = golk::resident_turns(left, h->resident_max) / depth;  // (32-bit super-step counts in the kernel)
     if (J < 2) return 0;
     // a remainder of exactly depth / 2 turns (1000 = 62 x 16 + 8) becomes a
     // last, half-depth super-step
@@ -1670,7 +1708,17 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t r) {
 int golhip_set_option(golhip_t h, const char *key, int64_t value) {
     if (int rc = check(h)) return rc;
     if (!key) return fail(GOLHIP_EINVAL, "null option");
+    for (const char *k : kTuningKeys)
+        if (!strcmp(key, k) && !tuning_env())
+            return fail(GOLHIP_EINVAL, "%s is an A/B tuning knob of the kernel plans: set GOLHIP_TUNING=1", key);
     std::lock_guard<std::mutex> g(h->mu);
+    if (!strcmp(key, "resident_max_turns")) {  // test hook: several resident launches in one step
+        if (value < 1 || value > golk::kResidentMaxTurns)
+            return fail(GOLHIP_EINVAL, "resident_max_turns %lld", (long long)value);
+        if (!test_hooks_env()) return fail(GOLHIP_EINVAL, "resident_max_turns is a test hook (GOLHIP_TEST_HOOKS=1)");
+        h->resident_max = value;
+        return GOLHIP_OK;
+    }
     if (!strcmp(key, "wpl")) {
         if (value != 0 && value != 1 && value != 2 && value != 4)
             return fail(GOLHIP_EINVAL, "wpl %lld not in {0,1,2,4}", (long long)value);
@@ -1831,7 +1879,7 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         return GOLHIP_OK;
     }
     if (!strcmp(key, "resident_fault")) {
-        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "resident_fault %lld", (long long)value);
+        if (value < 0 || value > 2) return fail(GOLHIP_EINVAL, "resident_fault %lld", (long long)value);
         if (value && !test_hooks_env())
             return fail(GOLHIP_EINVAL, "resident_fault is a test hook (GOLHIP_TEST_HOOKS=1)");
         h->resident_fault = (int)value;
@@ -2255,8 +2303,17 @@ int golhip_alive_count_global(golhip_t h, uint64_t *count, int64_t *at_turn) {
     // same turn (a concurrent golhip_step cannot advance the board between them)
     std::lock_guard<std::mutex> g(h->mu);
     if (int rc = alive_count_locked(h, count, at_turn)) return rc;
-    if (h->nranks == 1 || !h->ringed()) return GOLHIP_OK;
-    if (!h->comm) return fail(GOLHIP_EINVAL, "the test transport has no allreduce: sum golhip_alive_count over the ranks");
+    if (!h->ringed()) return GOLHIP_OK;
+    if (!h->comm) {
+        // test transport: the sum rides the same host callback (prev = next =
+        // -1 marks an allreduce of one uint64, golhip_test_transport_fn)
+        unsigned long long in = *count, out = 0;
+        if (int r = h->xport(h->xport_user, -1, -1, &in, nullptr, &out, nullptr, (int64_t)sizeof in))
+            return fail(GOLHIP_ERCCL, "test transport allreduce returned %d", r);
+        *count = out;
+        return GOLHIP_OK;
+    }
+    // the ring's RCCL communicator (also a one-rank ring: the same call as at 8 GPUs)
     HIP_OR_FAIL(hipMemcpyAsync(h->d_scalars + 3, h->d_scalars, sizeof(unsigned long long), hipMemcpyDeviceToDevice,
                                h->stream));
     NCCL_OR_FAIL(ncclAllReduce(h->d_scalars + 3, h->d_scalars + 3, 1, ncclUint64, ncclSum, h->comm, h->stream));
@@ -2418,7 +2475,7 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     memset(out, 0, sizeof *out);
     out->turns = h->turns;
     out->step_launches = h->step_launches;
-    out->split_launches = 0;  // retired kernel families (round 5): the fields stay for the ABI
+    out->reserved1 = 0;  // retired kernel families (round 5): the fields stay for the ABI
     out->step_turns = h->step_turns;
     out->step_kernel_ms = h->step_ms;
     out->persist_launches = h->persist_launches;
@@ -2439,7 +2496,7 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     out->skew_launches = h->skew_launches;
     out->halo_exchanges = h->halo_exchanges;
     out->halo_ms = h->halo_ms;
-    out->overlap_launches = 0;
+    out->reserved2 = 0;
     out->skew_half_launches = h->skew_half_launches;
     out->lds_launches = h->lds_launches;
     out->words_per_lane = h->W % 32 == 0 ? wpl_for(h) : 0;

@@ -54,11 +54,11 @@ class Perf(ctypes.Structure):
         ("flip_fallbacks", ctypes.c_int64),
         ("persist_depth", ctypes.c_int32),
         ("reserved0", ctypes.c_int32),
-        ("split_launches", ctypes.c_int64),
+        ("reserved1", ctypes.c_int64),
         ("skew_launches", ctypes.c_int64),
         ("halo_exchanges", ctypes.c_int64),
         ("halo_ms", ctypes.c_double),
-        ("overlap_launches", ctypes.c_int64),
+        ("reserved2", ctypes.c_int64),
         ("skew_half_launches", ctypes.c_int64),
         ("lds_launches", ctypes.c_int64),
     ]
@@ -270,13 +270,21 @@ class Board:
     def comm_init(self, uid: bytes, nranks: int, rank: int) -> None:
         _check(load().golhip_comm_init(self._h, uid, nranks, rank))
 
-    def test_ring_init(self, nranks: int, rank: int, ring_rows: int, exchange) -> None:
+    def test_ring_init(self, nranks: int, rank: int, ring_rows: int, exchange, allreduce=None) -> None:
         """Test hook (GOLHIP_TEST_HOOKS=1, golhip_test_ring_init): this strip is
         rank `rank` of a ring whose halos move through
         exchange(prev_rank, next_rank, send_up: bytes, send_down: bytes) ->
-        (recv_top, recv_bottom) instead of RCCL."""
+        (recv_top, recv_bottom) instead of RCCL, and whose
+        golhip_alive_count_global sums through allreduce(count: int) -> int
+        (the transport call with prev = next = -1)."""
         def cb(_user, prev, nxt, up, down, top, bottom, nbytes):
             try:
+                if prev < 0:  # the allreduce of golhip_alive_count_global: one uint64
+                    if allreduce is None or nbytes != 8:
+                        return 3
+                    s = allreduce(int.from_bytes(ctypes.string_at(up, 8), "little")) % (1 << 64)
+                    ctypes.memmove(top, s.to_bytes(8, "little"), 8)
+                    return 0
                 t, b = exchange(prev, nxt, ctypes.string_at(up, nbytes), ctypes.string_at(down, nbytes))
                 if len(t) != nbytes or len(b) != nbytes:
                     return 2

@@ -81,13 +81,13 @@ typedef struct golhip_perf {
     int32_t persist_depth;    /* turns per super-step of the resident kernel (its
                                  depths stop at 16 for two words per lane)       */
     int32_t reserved0;
-    int64_t split_launches;   /* always 0 (split tiling retired in round 5)     */
+    int64_t reserved1;        /* 0 (was split_launches: split tiling retired in round 5) */
     int64_t skew_launches;    /* of step_launches, those that ran skewed band
                                  stacks (gol_skew_kernel, kernel_variant 3)     */
     int64_t halo_exchanges;   /* halo exchanges posted (RCCL ring)               */
     double halo_ms;           /* their summed time on the stream they ran on
                                  (GOLHIP_FLAG_TIMING)                           */
-    int64_t overlap_launches; /* always 0 (option "overlap" retired in round 5)  */
+    int64_t reserved2;        /* 0 (was overlap_launches: option "overlap" retired in round 5) */
     int64_t skew_half_launches; /* of skew_launches, those on half-wave tiles    */
     int64_t lds_launches;     /* of persist_launches, those that ran resident LDS
                                  bands (gol_lds_band_kernel, kernel_variant 4)  */
@@ -132,60 +132,45 @@ void *golhip_stream(golhip_t h);
  * kernel's occupancy).  Results never depend on them. */
 int golhip_set_tb_depth(golhip_t h, int32_t turns);
 int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
-/* Named engine options (kernel variants for A/B measurement); results never
- * depend on them.  "fill_skip" (default 1): skip pipeline-fill stage-rows;
+/* Named engine options; results never depend on them.
+ *
+ * Product options (no consent needed):
  * "wpl" (default 0 = auto): words per lane, 1, 2 or 4 (2 and 4 run on the
- * interleaved pair / quad layouts, converted at the I/O boundary; 4 fuses at
- * most 8 turns a launch and needs width % 128 == 0); "skew" (default 1):
- * skewed band stacks (gol_skew_kernel) for per-launch steps of a torus or a
- * ring strip when they fill the CUs (2: always, 0: off); "skew_young"
- * (0 = by kernel: 68 %, whole tori 70 %, quads 78 %, half-wave tiles 60 %): band height of waves 4..7 relative to
- * waves 0..3; "skew_hcap" (-1 = 3 D / 4): rows a stack's bottom band gives
- * up (it computes its own drain); "skew_tx" (0 = plan, 1, 2): tiles across
- * a stack; "skew_half" (0 = when they need fewer wave-rows, 1 = whenever
- * possible, -1 = never): half-wave tiles (30 stored lanes each, two per
- * wave); "skew_prio" (0): s_setprio for the
- * younger waves; "timing" (the GOLHIP_FLAG_TIMING flag after
- * creation: per-launch HIP events, ~5 us each); "persistent"
- * (default -1 = auto: off where the skewed band stacks fill the CUs, else on
- * for buffers of at most 64 MiB; 1 on, 0 off): resident multi-super-step kernel for long runs on a
- * whole torus (never in a multi-rank ring);
- * "lds_band" (default -1 = auto: on wherever the resident kernel runs and a
- * band of >= lds_depth full-width rows per CU fits both its LDS buffers;
- * 1 the same, 0 off): resident LDS bands (gol_lds_band_kernel, W % 128 == 0;
- * under the same guard and timeout as the resident kernel); "lds_depth"
- * (0 = plan: 10 at 16 waves, else 12; at most the rows): turns per LDS-band super-step; "lds_xcd"
- * (1): consecutive bands on one XCD; "lds_stride" (1; 0: the runtime-stride kernel): LDS rows at a
- * compile-time stride where one is instantiated; "lds_waves" (0 = plan: 16 where a row's pairs fill
- * whole waves twice or more, else 8; or 8, 16) and
- * "lds_wg_cu" (1 or 2): waves per workgroup and bands per CU; "lds_age" (0 = plan: 60 at 16
- * waves and 70 at 8 where a row's pairs fill whole waves, else 100; 25-400): the rows of a
- * turn's run for each younger wave rank of a SIMD, % of the next older rank's (the arbiter
- * serves older waves first); "lds_pre" (2): a full super-step's
- * first turns run on the rows that need no halo while the halos travel;
- * "resident_fault" (0, test hook: refused without GOLHIP_TEST_HOOKS=1): the
- * resident kernels' band / workgroup 0 never reports, so its neighbours'
- * bounded waits time out and the step is restored and re-run;
- * "persist_depth" (default 0 = tb_depth): turns per super-step;
- * "persist_half" (default 1): a remainder of half a super-step runs as the
- * resident kernel's last, half-depth super-step;
- * "persist_waves" (0 = auto, 8 or 16): waves per persistent workgroup;
- * "paired_bands" (default 1): the two waves of a SIMD stream one two-band
- * region from both ends and meet where they meet (off: static taller bands
- * for the older waves); "persist_wg_tx" (0 = plan): tiles across a persistent workgroup;
- * "dummy_rows" (0 = all halo rows): rows that absorb masked stores;
- * "trace" (0): persistent-kernel diagnostics (golhip_persist_trace);
- * "persist_timeout_us" (default 1000000): how long a resident workgroup waits
- * for a neighbour before the launch is abandoned (the board is restored and
- * the step re-run on per-launch kernels, persist_fallbacks; the resident
- * kernel runs only on a whole torus or a one-rank ring, never in a
- * multi-rank ring);
+ *   interleaved pair / quad layouts, converted at the I/O boundary; 4 needs
+ *   width % 128 == 0);
+ * "persistent" (-1 = auto: off where the skewed band stacks fill the CUs,
+ *   else on for buffers of at most 64 MiB; 1 on, 0 off): resident kernels
+ *   (K1p, K1r) for long runs on a whole torus, never in a multi-rank ring --
+ *   0 keeps a shared GPU free of kernels that wait on co-resident workgroups;
+ * "lds_band" (-1 = auto, 1, 0): resident LDS bands (K1r, W % 128 == 0);
+ * "skew" (1; 2 always, 0 off): skewed band stacks (K1w) for per-launch steps;
+ * "timing" (GOLHIP_FLAG_TIMING after creation: per-launch HIP events);
+ * "persist_timeout_us" (1000000): how long a resident workgroup waits for a
+ *   neighbour before the launch is abandoned (the board is restored and the
+ *   step re-run on per-launch kernels, perf.persist_fallbacks);
  * "force_halo" (0): after golhip_comm_init with one rank, run a whole board
- * through the multi-GPU path as a one-rank RCCL ring (tests, measurement);
- * "halo_skip" (0): measurement only, refused without GOLHIP_MEASUREMENT=1,
- * post no halo exchange (the halo rows go stale: WRONG results; isolates the
- * exchange's cost).  Retired in round 5 (refused as unknown keys): "split",
- * "lds_split", "skew_nst", "age_split", "overlap". */
+ *   through the multi-GPU path as a one-rank RCCL ring.
+ *
+ * A/B tuning knobs of the kernel plans, refused without GOLHIP_TUNING=1 (or
+ * GOLHIP_MEASUREMENT=1); the defaults are the measured plans:
+ * persist_depth, persist_waves, persist_half, persist_wg_tx, paired_bands,
+ * dummy_rows, trace (golhip_persist_trace), cu_count, fill_skip, skew_young,
+ * skew_hcap, skew_prio, skew_half, skew_tx, lds_depth, lds_waves, lds_wg_cu,
+ * lds_age, lds_pre, lds_stride, lds_xcd.
+ *
+ * Measurement only, refused without GOLHIP_MEASUREMENT=1 (WRONG results by
+ * design): "halo_skip" (post no halo exchange), "flip_debug" 1-3.
+ *
+ * Test hooks, refused without GOLHIP_TEST_HOOKS=1 (exact results, forced
+ * failure paths): "resident_fault" (1: the resident kernels' band /
+ * workgroup 0 never reports in any launch, 2: only in a step's first
+ * resident launch; the neighbours' bounded waits time out and the step is
+ * restored and re-run), "resident_max_turns" (lowers the turns one resident
+ * launch takes, so a step runs several), "flip_debug" 4.
+ *
+ * golhip_build_info() lists the three consent sets and the product options.
+ * Retired (refused as unknown keys): "split", "lds_split", "skew_nst",
+ * "age_split", "overlap". */
 int golhip_set_option(golhip_t h, const char *key, int64_t value);
 
 /* ---- multi-GPU -------------------------------------------------------- */
@@ -211,7 +196,9 @@ int golhip_comm_info(golhip_t h, int32_t *nranks, int32_t *rank, int32_t *ring_r
  * return 0.  Everything else (golhip_halo_schedule's rounds, the deep-halo
  * launches, the kernels) is the RCCL ring's; ring_rows is the ring's smallest
  * strip (golhip_comm_init agrees it by allreduce; here the caller passes it).
- * golhip_alive_count_global is refused (no allreduce). */
+ * golhip_alive_count_global's allreduce runs through the same fn: prev_rank =
+ * next_rank = -1, send_up = this rank's uint64 count, recv_top = where the
+ * ring's sum goes, bytes = 8 (send_down, recv_bottom null). */
 typedef int (*golhip_test_transport_fn)(void *user, int32_t prev_rank, int32_t next_rank, const void *send_up,
                                         const void *send_down, void *recv_top, void *recv_bottom, int64_t bytes);
 int golhip_test_ring_init(golhip_t h, int32_t nranks, int32_t rank, int32_t ring_rows, golhip_test_transport_fn fn,

@@ -6,6 +6,8 @@ usage: python scripts/bench_halo.py [--size 16384] [--turns 1024] [--depths 16,3
 import argparse
 import json
 import os
+
+os.environ.setdefault("GOLHIP_TUNING", "1")  # A/B knobs of the kernel plans (golhip.h)
 import sys
 import time
 

@@ -12,6 +12,8 @@ chosen on measurements.  Prints one JSON line per (strip, persistent).
 import argparse
 import json
 import os
+
+os.environ.setdefault("GOLHIP_TUNING", "1")  # A/B knobs of the kernel plans (golhip.h)
 import sys
 import time
 

@@ -3,6 +3,8 @@ kernel, the per-launch kernel (depth 16) and the per-launch kernel at depth 1
 (the referee), for both words-per-lane layouts."""
 import json
 import os
+
+os.environ.setdefault("GOLHIP_TUNING", "1")  # A/B knobs of the kernel plans (golhip.h)
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

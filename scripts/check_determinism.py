@@ -3,6 +3,8 @@ board digest / alive count (after fill and after the steps)."""
 import argparse
 import json
 import os
+
+os.environ.setdefault("GOLHIP_TUNING", "1")  # A/B knobs of the kernel plans (golhip.h)
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -3,6 +3,8 @@ test_persistent_full_size_matches_per_launch and report any digest that
 differs from the first run of the same path (nondeterminism hunt)."""
 import json
 import os
+
+os.environ.setdefault("GOLHIP_TUNING", "1")  # A/B knobs of the kernel plans (golhip.h)
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

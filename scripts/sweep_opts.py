@@ -10,6 +10,8 @@ run and a summary (best GCUPS per set and case).
 import argparse
 import json
 import os
+
+os.environ.setdefault("GOLHIP_TUNING", "1")  # A/B knobs of the kernel plans (golhip.h)
 import sys
 import time
 

@@ -3,6 +3,8 @@ usage: python scripts/trace_persist.py --size 16384 --variants "persist_waves=8;
 import argparse
 import json
 import os
+
+os.environ.setdefault("GOLHIP_TUNING", "1")  # A/B knobs of the kernel plans (golhip.h)
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -10,6 +10,8 @@ Times in us (s_memrealtime, 100 MHz).
 import argparse
 import json
 import os
+
+os.environ.setdefault("GOLHIP_TUNING", "1")  # A/B knobs of the kernel plans (golhip.h)
 import sys
 
 import numpy as np

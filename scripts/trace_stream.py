@@ -6,6 +6,8 @@ measurement only).  Each leg: 60 launches from the configs[4] board at turn
 """
 import json
 import os
+
+os.environ.setdefault("GOLHIP_TUNING", "1")  # A/B knobs of the kernel plans (golhip.h)
 import sys
 
 import numpy as np

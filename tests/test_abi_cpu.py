@@ -129,7 +129,14 @@ def test_product_build_macros():
             # options that give wrong results by design need
             # GOLHIP_MEASUREMENT=1, test hooks GOLHIP_TEST_HOOKS=1 (refused otherwise:
             # tests/test_gpu_parity.py::test_wrong_result_options_need_measurement_consent)
-            "CONSENT_MEASUREMENT": "halo_skip,flip_debug:1-3", "CONSENT_TEST_HOOKS": "resident_fault,flip_debug:4,golhip_test_ring_init"}
+            "CONSENT_MEASUREMENT": "halo_skip,flip_debug:1-3",
+            "CONSENT_TEST_HOOKS": "resident_fault,resident_max_turns,flip_debug:4,golhip_test_ring_init",
+            # the A/B knobs no default plan varies need
+            # GOLHIP_TUNING=1; a product caller has the options below alone
+            "CONSENT_TUNING": "persist_depth,persist_waves,dummy_rows,paired_bands,persist_half,persist_wg_tx,trace,"
+                              "cu_count,fill_skip,skew_young,skew_hcap,skew_prio,skew_half,skew_tx,lds_depth,lds_waves,"
+                              "lds_wg_cu,lds_age,lds_pre,lds_stride,lds_xcd",
+            "PRODUCT_OPTIONS": "wpl,persistent,lds_band,skew,timing,persist_timeout_us,force_halo"}
     got = dict(kv.split("=", 1) for kv in info.split())
     assert got == want, info
 

@@ -140,7 +140,7 @@ class _FakeBoard:
     def perf(self):
         wpl = 4 if self.W == 262144 else 2
         return {"persist_turns": 0, "step_turns": 100, "step_launches": 10, "skew_launches": 10,
-                "split_launches": 0, "tb_depth": 9 if wpl == 4 else 20, "words_per_lane": wpl,
+                "tb_depth": 9 if wpl == 4 else 20, "words_per_lane": wpl,
                 "persist_launches": 0, "persist_depth": 0, "rows_per_wave": 0, "halo_bytes": 0,
                 "halo_exchanges": 0}
 

@@ -101,3 +101,58 @@ def test_gloo_strips_match_golden(fixtures, splits, tb, resident):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert np.array_equal(got, unpack_bits(fixtures["check_64x100"], 64))
+
+
+def _rankenv_worker(rank, world, port, q):
+    """bench.RankEnv's control plane as the driver's ranks run it (gloo, CPU
+    tensors), without the device half of __init__ (no GPU here)."""
+    import argparse
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "game-of-life-distributed_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import bench
+    import golhip as g
+    g.unique_id = lambda: b"rccl-id-of-rank-0"  # ncclGetUniqueId needs no peer, but keep RCCL out of the CPU suite
+    env = bench.RankEnv.__new__(bench.RankEnv)
+    env.a = argparse.Namespace(stage_timeout=60.0)
+    env.world, env.rank, env.local, env.wd, env.torch = world, rank, rank, None, torch
+    env.init_control()
+    res = {
+        "backend": dist.get_backend(),
+        # digests are uint64: the sum wraps mod 2^64 over ranks
+        "gsum": env.gsum((1 << 64) - 1 - rank if rank % 2 else (1 << 63) + rank),
+        "gmax": env.gmax(0.5 + rank),
+        "bcast": env.bcast(1000 + rank),
+        "gather": env.gather({"rank": rank}),
+        "uid": env.unique_id(),
+    }
+    dist.barrier()
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_rankenv_control_plane_is_gloo_on_cpu(world):
+    """the production RankEnv's collectives (the unique-id
+    broadcast, digest sum mod 2^64, max-over-ranks time, warmup broadcast,
+    per-rank rows) run on a gloo process group over CPU tensors, so the
+    library's RCCL communicator is the job's only GPU communication."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rankenv_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    vals = [(1 << 64) - 1 - r if r % 2 else (1 << 63) + r for r in range(world)]
+    for r in range(world):
+        res = got[r]
+        assert res["backend"] == "gloo"
+        assert res["gsum"] == sum(vals) % (1 << 64)
+        assert res["gmax"] == world - 0.5 and res["bcast"] == 1000
+        assert res["gather"] == [{"rank": i} for i in range(world)]
+        assert res["uid"] == b"rccl-id-of-rank-0"

@@ -2,10 +2,11 @@
 two rank processes run bench.main() exactly as `bench.py --gpus 2` ranks do
 (measure() of configs[2] and the configs3 block, parity against the
 full-size fixtures, the barrier-bracketed timed region, max over ranks, the
-per-rank rows, rank 0's one JSON line), with two substitutions a single GPU
-forces: the process group is gloo instead of RCCL, and each strip joins its
-halo ring through golhip_test_ring_init (GOLHIP_TEST_HOOKS=1), the exchange
-riding gloo point-to-point messages at the place of the RCCL group.  The
+per-rank rows, rank 0's one JSON line), through bench.RankEnv itself (its
+gloo control plane, as in production) with one substitution a single GPU
+forces: RankEnv.ring_init, so each strip joins its halo ring through
+golhip_test_ring_init (GOLHIP_TEST_HOOKS=1), the exchange and the global
+alive count's allreduce riding gloo messages at the place of the RCCL calls.  The
 line's timings are meaningless (two ranks share one GPU); its parity, plan
 and plumbing are what is checked.  RCCL's own transport is left to the
 driver's multi-GPU run.
@@ -26,39 +27,16 @@ RANK_MAIN = r'''
 import os, sys
 sys.path[:0] = [{root!r}, os.path.join({root!r}, "game-of-life-distributed_amd")]
 sys.argv = ["bench.py"] + {argv!r}
-import numpy as np
 import torch
 import torch.distributed as dist
 import bench
-import golhip
-
-
-class HostBoard(golhip.Board):
-    """golhip_alive_count_global has no allreduce on the test transport: sum over gloo."""
-
-    def alive_count(self, global_sum=False):
-        c, t = super().alive_count()
-        if global_sum:
-            x = torch.tensor([c], dtype=torch.int64)
-            dist.all_reduce(x)
-            c = int(x.item())
-        return c, t
 
 
 class HostRingEnv(bench.RankEnv):
-    """bench.RankEnv on one shared GPU: gloo collectives on CPU tensors and
-    the library's test transport for the halo ring."""
-
-    def __init__(self, a, world, rank, local):
-        self.a, self.world, self.rank, self.local = a, world, rank, 0
-        self.wd = bench.Watchdog(a, rank)
-        self.torch = torch
-        torch.cuda.set_device(0)
-        dist.init_process_group("gloo")
-        self.dist = dist
-
-    def board(self, W, H, row0, rows):
-        return HostBoard(W, H, device=0, row0=row0, rows=rows)
+    """bench.RankEnv exactly as the driver's ranks run it (gloo control
+    plane, the library's ring schedule, golhip_alive_count_global), except
+    that the halo ring joins through the test transport instead of RCCL (two
+    ranks cannot share one GPU in RCCL)."""
 
     def ring_init(self, board, tag=""):
         self.stage(tag + "golhip_test_ring_init (host transport over gloo)")
@@ -75,29 +53,16 @@ class HostRingEnv(bench.RankEnv):
                 r.wait()
             return top.numpy().tobytes(), bottom.numpy().tobytes()
 
-        board.test_ring_init(self.world, self.rank, min(rows), exchange)
+        def allreduce(x):  # golhip_alive_count_global's sum
+            t = torch.tensor([x], dtype=torch.int64)
+            dist.all_reduce(t)
+            return int(t.item())
 
-    def barrier(self, board):
-        dist.barrier()
-        board.sync()
-        torch.cuda.synchronize()
-
-    def gsum(self, x):
-        t = torch.tensor([x - (1 << 64) if x >= (1 << 63) else x], dtype=torch.int64)
-        dist.all_reduce(t)
-        return int(t.item()) % (1 << 64)
-
-    def gmax(self, x):
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def bcast(self, x):
-        t = torch.tensor([x], dtype=torch.int64)
-        dist.broadcast(t, src=0)
-        return int(t.item())
+        board.test_ring_init(self.world, self.rank, min(rows), exchange, allreduce)
 
 
+# the tested env differs from the production one in ring_init alone
+assert sorted(k for k in vars(HostRingEnv) if not k.startswith("__")) == ["ring_init"]
 bench.main(env_factory=HostRingEnv)
 '''
 
@@ -145,3 +110,29 @@ def test_bench_two_ranks_host_ring(tmp_path):
         assert [r["rank"] for r in ranks] == list(range(world)), ranks
         assert blk["config"]["comm"]["nranks"] == world
         assert blk["value"] > 0 and blk["ms_per_step"] > 0
+
+
+@pytest.mark.timeout(300)
+def test_bench_one_rank_rccl_ring_production_path(tmp_path):
+    """`bench.py --ring`: the production RankEnv unchanged (gloo control
+    plane of one rank, rank 0's RCCL unique id over it, golhip_comm_init's
+    ncclCommInitRank and strip-row allreduce), the whole configs[2] board as
+    a one-rank RCCL ring (force_halo: the ncclSend / ncclRecv group of every
+    exchange), and the parity step's alive count from
+    golhip_alive_count_global's ncclAllReduce -- against the c2 fixture at
+    turn 1000."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "GOLHIP_TEST_HOOKS"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--ring", "--steps", "1", "--warmup", "1",
+                        "--warmup-seconds", "0", "--no-cpu-baseline", "--no-configs3", "--stage-timeout", "200"],
+                       env=env, capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stderr[-3000:]
+    (line,) = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert line["parity"] is True, line["parity_check"]
+    assert line["parity_check"]["fixture"] == "tests/golden/fullsize.json c2 turn 1000"
+    cfg = line["config"]
+    assert cfg["comm"] == {"nranks": 1, "rank": 0, "ring_rows": 65536}
+    assert cfg["parallelism"] == "one-rank RCCL ring (force_halo)" and cfg["halo_exchanges"] > 0
+    assert cfg["control_plane"].startswith("gloo")
+    assert line["final_turn"] == 2000

@@ -687,3 +687,73 @@ def test_wrong_result_options_need_measurement_consent(monkeypatch):
         monkeypatch.setenv("GOLHIP_MEASUREMENT", "1")
         b.set_option("halo_skip", 1)
         b.set_option("halo_skip", 0)
+
+
+TUNING_KEYS = {"persist_depth": 8, "persist_waves": 8, "dummy_rows": 1, "paired_bands": 0, "persist_half": 0,
+               "persist_wg_tx": 1, "trace": 0, "cu_count": 0, "fill_skip": 1, "skew_young": 60, "skew_hcap": 10,
+               "skew_prio": 0, "skew_half": 0, "skew_tx": 1, "lds_depth": 8, "lds_waves": 8, "lds_wg_cu": 1,
+               "lds_age": 70, "lds_pre": 2, "lds_stride": 1, "lds_xcd": 1}
+PRODUCT_OPTIONS = {"wpl": 0, "persistent": -1, "lds_band": -1, "skew": 1, "timing": 0, "persist_timeout_us": 1000000,
+                   "force_halo": 0}
+
+
+def test_tuning_knobs_need_consent(monkeypatch):
+    """the plan's A/B knobs are refused without
+    GOLHIP_TUNING=1 (or GOLHIP_MEASUREMENT=1); the product options are not;
+    the resident-launch cap is a test hook.  Same lists as
+    golhip_build_info() (tests/test_abi_cpu.py::test_product_build_macros)."""
+    info = dict(kv.split("=", 1) for kv in golhip.load().golhip_build_info().decode().split())
+    assert set(info["CONSENT_TUNING"].split(",")) == set(TUNING_KEYS)
+    assert set(info["PRODUCT_OPTIONS"].split(",")) == set(PRODUCT_OPTIONS)
+    for var in ("GOLHIP_TUNING", "GOLHIP_MEASUREMENT", "GOLHIP_TEST_HOOKS"):
+        monkeypatch.delenv(var, raising=False)
+    with golhip.Board(64, 64) as b:
+        for k, v in TUNING_KEYS.items():
+            with pytest.raises(golhip.GolHipError, match="GOLHIP_TUNING"):
+                b.set_option(k, v)
+        for k, v in PRODUCT_OPTIONS.items():
+            b.set_option(k, v)
+        with pytest.raises(golhip.GolHipError, match="GOLHIP_TEST_HOOKS"):
+            b.set_option("resident_max_turns", 100)
+        monkeypatch.setenv("GOLHIP_TUNING", "1")
+        for k, v in TUNING_KEYS.items():
+            b.set_option(k, v)
+        monkeypatch.setenv("GOLHIP_TUNING", "0")
+        monkeypatch.setenv("GOLHIP_MEASUREMENT", "1")
+        b.set_option("skew_young", 0)
+
+
+@pytest.mark.parametrize("n,lds,fault", [(1024, 1, 0), (1024, 1, 1), (1024, 1, 2), (1024, 0, 0), (1024, 0, 1),
+                                         (1024, 0, 2)])
+def test_resident_launches_past_the_cap(test_hooks, n, lds, fault):
+    """a step of more turns than one resident launch takes
+    runs several (here the test hook lowers golk::kResidentMaxTurns to 48 and
+    40 turns).  With resident_fault 2 only the step's first launch times out
+    (a transient starvation) and the later ones are healthy: the error word
+    must survive them (each used to clear it, and the step returned OK on a
+    drained board), so the step is restored and re-run on the per-launch
+    kernels; fault 1 times out every launch.  Bit-exact either way, and the
+    fallback is counted."""
+    from oracle.oracle import COracle
+    board = COracle().fill_random(n, n, 0x5EED0042)
+    turns = 200
+    want = COracle().run(board, turns)
+    with golhip.Board(n, n) as b:
+        b.set_option("persistent", 1)
+        b.set_option("lds_band", lds)
+        b.set_option("persist_timeout_us", 2000)
+        b.set_option("resident_max_turns", 48 if lds else 40)
+        b.set_option("resident_fault", fault)
+        b.load_bytes(board)
+        b.step(turns)
+        b.sync()
+        p = b.perf()
+        got = b.snapshot_bytes()
+        cnt, at = b.alive_count()
+    assert np.array_equal(got, want)
+    assert (cnt, at) == (int((want == 255).sum()), turns)
+    if fault:
+        assert p["persist_fallbacks"] == 1 and p["persist_launches"] == 0, p
+    else:
+        assert p["persist_fallbacks"] == 0 and p["persist_launches"] >= 4, p
+        assert (p["lds_launches"] > 0) == bool(lds), p

@@ -41,15 +41,17 @@ def _rank_main(rank, nranks, W, H, turns, board_key, seed, sample_rows, inboxes,
         bounds = [H * i // nranks for i in range(nranks + 1)]
         row0, rows = bounds[rank], bounds[rank + 1] - bounds[rank]
         ring_rows = min(bounds[i + 1] - bounds[i] for i in range(nranks))
-        inbox = inboxes[rank]
 
         def exchange(prev, nxt, up, down):
             # as the RCCL group: our first rows go up (prev's bottom halo), our
-            # last rows down (next's top halo); theirs come back the same way
-            inboxes[prev].put(("up", up))
-            inboxes[nxt].put(("down", down))
-            got = dict(inbox.get(timeout=60) for _ in range(2))
-            return got["down"], got["up"]
+            # last rows down (next's top halo); theirs come back the same way.
+            # One queue per directed edge: inboxes[2 r] holds what
+            # r's next rank sent up, inboxes[2 r + 1] what its prev sent down,
+            # each in exchange order, so a neighbour that runs a round ahead
+            # can never pair its halo with another neighbour's older one
+            inboxes[2 * prev].put(up)
+            inboxes[2 * nxt + 1].put(down)
+            return inboxes[2 * rank + 1].get(timeout=60), inboxes[2 * rank].get(timeout=60)
 
         with g.Board(W, H, row0=row0, rows=rows) as b:
             for k, v in opts.items():
@@ -80,7 +82,7 @@ def _rank_main(rank, nranks, W, H, turns, board_key, seed, sample_rows, inboxes,
 
 def run_ring(nranks, W, H, turns, board_key=None, seed=0, sample_rows=(), timeout=300, **opts):
     ctx = mp.get_context("spawn")
-    inboxes = [ctx.Queue() for _ in range(nranks)]
+    inboxes = [ctx.Queue() for _ in range(2 * nranks)]  # per directed edge: [2 r] from below, [2 r + 1] from above
     out_q = ctx.Queue()
     procs = [ctx.Process(target=_rank_main, args=(r, nranks, W, H, turns, board_key, seed, list(sample_rows), inboxes,
                                                         out_q, opts))
