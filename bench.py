@@ -420,7 +420,9 @@ def events_main(a) -> None:
     p = res["perf"]
     turns = tps * a.steps
     kus = p["flip_kernel_ms"] * 1e3 / max(1, p["flip_launches"])
-    alg = 2 * N * N / 8 + res["flips_timed"] / max(1, turns) * 4  # board in + out + entries, per launch
+    host_b = res["flips_timed"] / max(1, turns) * 4  # K5's entries per launch (4-byte indices, host memory)
+    alg = 2 * N * N / 8 + host_b  # board in + out + entries, per launch
+    link = golhip.host_link_probe(0)  # the link's ceiling for those stores, measured here
     out = {
         "metric": METRIC, "value": round(N * N * turns / res["dt"] / 1e9, 3), "unit": "GCUPS", "n_gpus": 1,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(res["dt"] / a.steps * 1e3, 4),
@@ -435,13 +437,24 @@ def events_main(a) -> None:
                       "flips": res["flips"]},
         "events_off": {"gcups": round(N * N * turns / res["dt_off"] / 1e9, 3),
                        "turns_per_s": round(turns / res["dt_off"], 1)},
-        "roofline": {"bound": "hbm", "achieved": round(alg / (kus * 1e-6) / 1e9, 1) if kus > 0 else None,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(alg / (kus * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
-                     if kus > 0 else None, "traffic": None, "kernel": "gol_flip_turn_kernel (K5)",
+        "roofline": {"bound": "host-link", "achieved": round(host_b / (kus * 1e-6) / 1e9, 2) if kus > 0 else None,
+                     "peak": link["kernel_write_GBps"], "unit": "GB/s",
+                     "frac": round(host_b / (kus * 1e-6) / 1e9 / link["kernel_write_GBps"], 4)
+                     if kus > 0 and link["kernel_write_GBps"] > 0 else None,
+                     "traffic": None, "kernel": "gol_flip_turn_kernel (K5)",
                      "avg_launch_ms": round(kus / 1e3, 5), "launches": p["flip_launches"],
-                     "alg_bytes_per_launch": alg,
-                     "note": "one turn + its list per launch; the 5120^2 board is cache-resident and the launch is "
-                             "bound by its grid-wide predecessor sum, not by bandwidth (DESIGN 7.3)"},
+                     "host_bytes_per_launch": host_b,
+                     "peak_source": "golhip_host_link_probe on this box, this run: a kernel's coalesced 16-byte "
+                                    "stores into golhip_host_alloc memory (K5's store path)",
+                     "link_probe": link,
+                     "stream_GBps": round(host_b * turns / res["dt"] / 1e9, 2),
+                     "hbm_side": {"alg_bytes_per_launch": alg,
+                                  "achieved_GBps": round(alg / (kus * 1e-6) / 1e9, 1) if kus > 0 else None,
+                                  "peak_GBps": HBM_PEAK_GBS,
+                                  "note": "board in + board out + entries; the 5120^2 board is cache-resident"},
+                     "note": "one turn + its list per launch: the entries cross the host link into page-locked "
+                             "memory; achieved = entry bytes per launch / the launch's device time (HIP events), "
+                             "stream_GBps the same bytes over the timed wall clock (host syncs included)"},
     }
     try:  # HBM bytes of K5 from the PMC passes of this command (scripts/pmc_bench.sh ... 5120)
         with open(a.pmc) as f:
@@ -449,10 +462,10 @@ def events_main(a) -> None:
     except (OSError, ValueError):
         rec = None
     if rec and rec.get("hbm_bytes_per_launch") and kus > 0:
-        out["roofline"]["traffic"] = rec["hbm_bytes_per_launch"]
-        out["roofline"]["hbm"] = {"achieved_GBps": round(rec["hbm_bytes_per_launch"] / (kus * 1e-6) / 1e9, 1),
-                                  "peak_GBps": HBM_PEAK_GBS, "source": os.path.relpath(a.pmc, ROOT),
-                                  "note": "FETCH_SIZE x2 + WRITE_SIZE; the entries go to page-locked host memory"}
+        out["roofline"]["hbm_side"].update(
+            pmc_bytes_per_launch=rec["hbm_bytes_per_launch"],
+            pmc_GBps=round(rec["hbm_bytes_per_launch"] / (kus * 1e-6) / 1e9, 1), source=os.path.relpath(a.pmc, ROOT),
+            pmc_note="FETCH_SIZE x2 + WRITE_SIZE; the entries go to page-locked host memory")
     if a.e2e_turns > 0:
         out["end_to_end"] = events_end_to_end(c4, a.e2e_turns)
         parity["ok"] = parity["ok"] and out["end_to_end"]["parity"]

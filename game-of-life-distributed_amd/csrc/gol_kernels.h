@@ -209,6 +209,9 @@ struct FlipTurnArgs {
 int64_t flip_turn_blocks(int64_t nwords);
 hipError_t launch_flip_turn(const FlipTurnArgs &a, hipStream_t s);
 int flip_turn_blocks_per_cu(bool contig);
+// gol_probe.hip: coalesced 16-byte stores over `bytes` (a multiple of 16) of
+// device-visible memory, e.g. page-locked host memory (the host-link probe)
+hipError_t launch_host_write_probe(void *dst, uint64_t bytes, int blocks, uint32_t tag, hipStream_t s);
 
 // "NAME=value ..." of the build's tuning macros (golhip_build_info).
 const char *build_info();

@@ -1631,6 +1631,59 @@ int golhip_host_free(void *p) {
     return GOLHIP_OK;
 }
 
+int golhip_host_link_probe(int32_t device, uint64_t bytes, int32_t reps, double *kernel_write_gbps,
+                           double *dma_d2h_gbps) {
+    if (!kernel_write_gbps || !dma_d2h_gbps || bytes < 4096 || bytes % 16 || reps < 1 || reps > 1000)
+        return fail(GOLHIP_EINVAL, "host link probe: bytes >= 4096, a multiple of 16; 1 <= reps <= 1000");
+    *kernel_write_gbps = *dma_d2h_gbps = 0;
+    HIP_OR_FAIL(hipSetDevice(device));
+    int cus = 0;
+    HIP_OR_FAIL(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    // the buffer K5 writes into: golhip_host_alloc's kind (hipHostMalloc, device-mapped)
+    void *host = nullptr, *host_dev = nullptr, *dev = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipError_t e = hipHostMalloc(&host, (size_t)bytes, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&host_dev, host, 0);
+    if (e == hipSuccess) e = hipMalloc(&dev, (size_t)bytes);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    if (e == hipSuccess) e = hipMemsetAsync(dev, 0x5a, (size_t)bytes, st);
+    // K5's own shape: 256-thread blocks, a few per CU, 16-byte stores
+    const int blocks = 4 * cus;
+    float kms = 0, dms = 0;
+    if (e == hipSuccess) e = golk::launch_host_write_probe(host_dev, bytes, blocks, 0, st);  // warm (page mapping)
+    if (e == hipSuccess) e = hipMemcpyAsync(host, dev, (size_t)bytes, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = hipEventRecord(e0, st);
+    for (int r = 0; e == hipSuccess && r < reps; ++r) e = golk::launch_host_write_probe(host_dev, bytes, blocks, r + 1, st);
+    if (e == hipSuccess) e = hipEventRecord(e1, st);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    if (e == hipSuccess) e = hipEventElapsedTime(&kms, e0, e1);
+    if (e == hipSuccess) e = hipEventRecord(e0, st);
+    for (int r = 0; e == hipSuccess && r < reps; ++r)
+        e = hipMemcpyAsync(host, dev, (size_t)bytes, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipEventRecord(e1, st);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    if (e == hipSuccess) e = hipEventElapsedTime(&dms, e0, e1);
+    // the last kernel pass's pattern must be in host memory (tag reps: word 0 == reps)
+    if (e == hipSuccess && reps >= 1) {
+        // (the DMA passes overwrote it with 0x5a bytes: check those instead)
+        const uint32_t w = static_cast<const uint32_t *>(host)[bytes / 4 - 1];
+        if (w != 0x5a5a5a5au) e = hipErrorUnknown;
+    }
+    if (e1) (void)hipEventDestroy(e1);
+    if (e0) (void)hipEventDestroy(e0);
+    if (st) (void)hipStreamDestroy(st);
+    if (dev) (void)hipFree(dev);
+    if (host) (void)hipHostFree(host);
+    if (e != hipSuccess) return fail(GOLHIP_EHIP, "host link probe: %s", hipGetErrorString(e));
+    *kernel_write_gbps = kms > 0 ? (double)bytes * reps / (kms * 1e-3) / 1e9 : 0;
+    *dma_d2h_gbps = dms > 0 ? (double)bytes * reps / (dms * 1e-3) / 1e9 : 0;
+    return GOLHIP_OK;
+}
+
 int golhip_create(int32_t width, int32_t height, int32_t device, uint32_t flags, golhip_t *out) {
     return create_common(width, height, 0, height, device, flags, false, out);
 }

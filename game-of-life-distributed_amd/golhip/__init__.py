@@ -109,6 +109,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "golhip_device_count": ([P(i32)], ctypes.c_int),
         "golhip_host_alloc": ([u64, P(ctypes.c_void_p)], ctypes.c_int),
         "golhip_host_free": ([ctypes.c_void_p], ctypes.c_int),
+        "golhip_host_link_probe": ([i32, u64, i32, P(ctypes.c_double), P(ctypes.c_double)], ctypes.c_int),
         "golhip_create": ([i32, i32, i32, u32, P(H)], ctypes.c_int),
         "golhip_create_strip": ([i32, i32, i32, i32, i32, u32, P(H)], ctypes.c_int),
         "golhip_destroy": ([H], ctypes.c_int),
@@ -202,6 +203,15 @@ def host_array(shape, dtype) -> np.ndarray:
     a = np.frombuffer(buf, dtype=dt).reshape(shape).view(HostArray)
     a._golhip_ptr = p.value
     return a
+
+
+def host_link_probe(device: int = 0, nbytes: int = 256 << 20, reps: int = 5) -> dict:
+    """The host link into golhip_host_alloc memory (golhip_host_link_probe):
+    a kernel's coalesced 16-byte stores (how the event-stream kernel writes
+    its entries) and the DMA engine's device-to-host copy, GB/s."""
+    k, d = ctypes.c_double(), ctypes.c_double()
+    _check(load().golhip_host_link_probe(device, nbytes, reps, ctypes.byref(k), ctypes.byref(d)))
+    return {"kernel_write_GBps": round(k.value, 2), "dma_d2h_GBps": round(d.value, 2), "bytes": nbytes, "reps": reps}
 
 
 def unique_id() -> bytes:

@@ -107,6 +107,13 @@ int golhip_device_count(int32_t *n);
  * copy after the batch.  Go callers use it as C memory (unsafe.Slice). */
 int golhip_host_alloc(uint64_t bytes, void **out);
 int golhip_host_free(void *p);
+/* Measurement (no reference counterpart): the host link's rates into a
+ * buffer of golhip_host_alloc's kind -- a kernel streaming coalesced 16-byte
+ * stores into it (what the event-stream kernel's entries ride) and the DMA
+ * engine's device-to-host copy -- over `bytes` (>= 4096, a multiple of 16),
+ * `reps` passes each after one warm pass, in GB/s (1e9 B/s). */
+int golhip_host_link_probe(int32_t device, uint64_t bytes, int32_t reps, double *kernel_write_gbps,
+                           double *dma_d2h_gbps);
 
 /* ---- handles ---------------------------------------------------------- */
 /* Whole width x height torus on one device.  Replaces the world allocation

@@ -288,3 +288,14 @@ def test_persistent_timeout_one_rank_ring(coracle, timeout_us):  # 1: workgroup 
         assert b.alive_count() == (int((want == 255).sum()), turns)
         b.step(10)
         assert np.array_equal(b.snapshot_bytes(), coracle.run(want, 10))
+
+
+def test_host_link_probe():
+    """golhip_host_link_probe: K5's ceiling, the rate a
+    kernel's coalesced 16-byte stores reach page-locked host memory, and the
+    DMA copy rate beside it; bad arguments are refused."""
+    r = golhip.host_link_probe(0, 16 << 20, 2)
+    assert 1.0 < r["kernel_write_GBps"] < 1000.0 and 1.0 < r["dma_d2h_GBps"] < 1000.0, r
+    for nbytes, reps in ((100, 1), (4097, 1), (1 << 20, 0)):
+        with pytest.raises(golhip.GolHipError):
+            golhip.host_link_probe(0, nbytes, reps)
