@@ -37,9 +37,62 @@ constexpr unsigned kNext = tt3([](int u0, int g1, int g2) { return u0 ? (!g1 && 
 static_assert(kG1 == 0x43 && kG2 == 0x35 && kNext == 0x24, "rule LUTs");
 static_assert(kXor3 == 0x96 && kMaj == 0xE8, "bitop3 table order");
 
+// Pair rule (round 6, K1w's main loop with `PR`): the two output rows 2m and
+// 2m + 1 share the middle pair of their input rows, so they share that
+// pair's vertical sum P = S(2m) + S(2m + 1) of the row sums S = s0 + 2 s1:
+// P in 0..6 as three bits from four LUTs (a half adder on the s0 bits, a
+// full adder on the s1 bits and its carry), two LUTs a row.  Each output row
+// is then a 4-LUT circuit of the other input row's sum A (a0 + 2 a1, the row
+// above for 2m, below for 2m + 1), P and its centre c: sum9 = A + P and
+// next = (sum9 == 3) | (c & sum9 == 4).  Found by exhaustive search over
+// 4-gate circuits (none with 3 exists); it leans on the unreachable input
+// c & P == 0 and is checked on all 4096 four-row neighbourhoods in
+// tests/test_rule_circuit.py:
+//   s6   = [exactly one of a0, p0, c]
+//   s7   = [(a1, p1, p2) in {000, 001, 110}]
+//   s8   = [(c, s6, s7) in {010, 100, 111}]
+//   next = s8 & (s7 | !p2)
+// 2 (row sum) + 2 (pair) + 4 = 8 LUTs a word-turn instead of 9.
+constexpr unsigned kXor2 = tt3([](int a, int b, int) { return (a ^ b) != 0; });   // 0x3C
+constexpr unsigned kAnd2 = tt3([](int a, int b, int) { return a && b; });         // 0xC0
+constexpr unsigned kBorrow = tt3([](int a, int b, int) { return !a && b; });      // 0x0C: a - b borrows
+constexpr unsigned kPrA = tt3([](int a0, int p0, int c) { return a0 + p0 + c == 1; });
+constexpr unsigned kPrB = tt3([](int a1, int p1, int p2) {
+    return (!a1 && !p1) || (a1 && p1 && !p2);
+});
+constexpr unsigned kPrC = tt3([](int c, int s6, int s7) { return (!c && s6 && !s7) || (c && !s6 && !s7) || (c && s6 && s7); });
+constexpr unsigned kPrNext = tt3([](int p2, int s7, int s8) { return s8 && (s7 || !p2); });
+static_assert(kPrA == 0x16 && kPrB == 0x43 && kPrC == 0x94 && kPrNext == 0x8a, "pair rule LUTs");
+static_assert(kXor2 == 0x3C && kAnd2 == 0xC0 && kBorrow == 0x0C, "pair adder LUTs");
+
 template <unsigned IMM>
 __device__ __forceinline__ uint32_t bop(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, IMM);
+}
+
+// P = B + C of two row sums (b0 + 2 b1, c0 + 2 c1): p0 + 2 p1 + 4 p2.  The
+// two-input LUTs repeat an operand (8-byte bitop3 keeps the step kernels'
+// instruction stream on its code parity; a VOP2 v_xor would not).
+__device__ __forceinline__ void pair_sum(uint32_t b0, uint32_t b1, uint32_t c0, uint32_t c1, uint32_t &p0,
+                                         uint32_t &p1, uint32_t &p2) {
+    p0 = bop<kXor2>(b0, c0, c0);
+    const uint32_t k = bop<kAnd2>(b0, c0, c0);
+    p1 = bop<kXor3>(b1, c1, k);
+    p2 = bop<kMaj>(b1, c1, k);
+}
+// B = P - C (the inverse, for a pipeline leaving the pair layout; B <= 3)
+__device__ __forceinline__ void pair_unsum(uint32_t p0, uint32_t p1, uint32_t c0, uint32_t c1, uint32_t &b0,
+                                           uint32_t &b1) {
+    b0 = bop<kXor2>(p0, c0, c0);
+    const uint32_t br = bop<kBorrow>(p0, c0, c0);
+    b1 = bop<kXor3>(p1, c1, br);
+}
+__device__ __forceinline__ uint32_t pair_rule(uint32_t a0, uint32_t a1, uint32_t p0, uint32_t p1, uint32_t p2,
+                                              uint32_t c) {
+    const uint32_t s6 = bop<kPrA>(a0, p0, c);
+    const uint32_t s7 = bop<kPrB>(a1, p1, p2);
+    const uint32_t s8 = bop<kPrC>(c, s6, s7);
+    return bop<kPrNext>(p2, s7, s8);
 }
 // Whole-wavefront lane shifts (DPP wave_shr:1 / wave_shl:1): lane i receives
 // lane i-1 / i+1; bound_ctrl zero-fills the edge lane (no `old` operand, so

@@ -205,6 +205,15 @@ struct FlipTurnArgs {
                                     //    blockIdx and each block sums ALL its predecessors' aggregates;
                                     // 0: virtual ids from `ticket` and a decoupled look-back
     unsigned long long *alive;      // nullable: += popcount of the new board
+    // Host copy of the PREVIOUS turn's list, overlapped with this turn (round
+    // 6): cp_blocks extra blocks after the turn's own (every block when the
+    // launch is copy-only, ncompute 0) copy entries [cp_run[0], cp_run[1])
+    // (cut at cap; none when stop_on_overflow and that turn overflowed) from
+    // the device list `out` to the host list cp_dst (golhip_host_alloc memory).
+    const unsigned long long *cp_run;  // nullable: no previous turn to copy
+    void *cp_dst;
+    int cp_blocks;
+    int ncompute;                   // the turn's own blocks (flip_turn_blocks; 0: copy only)
 };
 int64_t flip_turn_blocks(int64_t nwords);
 hipError_t launch_flip_turn(const FlipTurnArgs &a, hipStream_t s);

@@ -2140,11 +2140,44 @@ __device__ __forceinline__ uint32_t ft_rule(const uint32_t (&w)[3], const uint32
     return bop<kNext>(u0, g1, g2);
 }
 
+// The copy blocks of a K5 launch: the previous turn's entries, device list
+// -> host list, in 16-byte stores to the destination's 16-byte boundaries
+// (4-byte heads and tails), spread over the copy blocks.  They never wait on
+// anything, so the turn's own blocks keep their co-residency, and their host
+// stores are in their own waves: the turn's loads never wait behind them
+// (vmcnt is per wave).  Whether the previous turn is delivered follows from
+// its run bounds alone (a stop flag set by this launch's own blocks must not
+// cancel the copy of a turn that did fit).
+__device__ void flip_copy_prev(const FlipTurnArgs &a, unsigned cb, unsigned ncb) {
+    const unsigned long long s = a.cp_run[0], e0 = a.cp_run[1];
+    if (a.stop_on_overflow && e0 > a.cap) return;  // that turn did not fit: the host rolls back to it
+    const unsigned long long e = e0 < a.cap ? e0 : a.cap;
+    if (e <= s) return;
+    const unsigned wpe = a.format == kFlipFormatXY ? 2u : 1u;  // 32-bit words per entry
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(a.out) + s * wpe;
+    uint32_t *d = reinterpret_cast<uint32_t *>(a.cp_dst) + s * wpe;
+    const unsigned long long nw = (e - s) * wpe;
+    const unsigned long long head = min(nw, (unsigned long long)((4u - (unsigned)(((uintptr_t)d >> 2) & 3u)) & 3u));
+    const unsigned long long nq = (nw - head) / 4;
+    const unsigned long long gt = (unsigned long long)cb * kFtThreads + threadIdx.x, gn = (unsigned long long)ncb * kFtThreads;
+    if (gt < head) d[gt] = src[gt];
+    for (unsigned long long q = gt; q < nq; q += gn) {
+        const unsigned long long w = head + 4 * q;
+        *reinterpret_cast<uint4 *>(d + w) = make_uint4(src[w], src[w + 1], src[w + 2], src[w + 3]);
+    }
+    const unsigned long long t0 = head + 4 * nq;
+    if (t0 + gt < nw) d[t0 + gt] = src[t0 + gt];
+}
+
 // CONTIG (Ww % 4 == 0): thread tid of the block owns the 4 consecutive words
 // base + 4 tid .. + 3 of one row (16-byte loads and stores); otherwise word
 // base + k * 256 + tid for k = 0..3 (4-byte accesses, any Ww).
 template <bool CONTIG>
 __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
+    if (blockIdx.x >= (unsigned)a.ncompute) {  // a copy block (after the turn's own, so dispatched last)
+        if (a.cp_run) flip_copy_prev(a, blockIdx.x - (unsigned)a.ncompute, gridDim.x - (unsigned)a.ncompute);
+        return;
+    }
     if (a.ctl[0]) return;  // an earlier turn of the batch overflowed: the host rolls back to it
     __shared__ unsigned s_vid;
     __shared__ unsigned long long s_wsum[4], s_part[4];
@@ -2285,7 +2318,7 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
     if (a.dbg & 1) {  // measurement only: no look-back (entries overlap)
         if (tid == 0) {
             s_excl = a.run[0];
-            if (vid == gridDim.x - 1) a.run[1] = a.run[0];
+            if (vid == (unsigned)a.ncompute - 1) a.run[1] = a.run[0];
         }
     } else if (a.coresident) {
         // publish the aggregate, then every thread sums its share of ALL
@@ -2318,7 +2351,7 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
         if (tid == 0) {
             const unsigned long long excl = a.run[0] + s_part[0] + s_part[1] + s_part[2] + s_part[3];
             s_excl = excl;
-            if (vid == gridDim.x - 1) {
+            if (vid == (unsigned)a.ncompute - 1) {
                 const unsigned long long end = excl + T;
                 a.run[1] = end;
                 if (a.stop_on_overflow && end > a.cap) atomicOr(&a.ctl[0], 1u);
@@ -2371,7 +2404,7 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
         }
         if (lane == 0) {
             s_excl = excl;
-            if (vid == gridDim.x - 1) {  // the last block's inclusive prefix closes the turn
+            if (vid == (unsigned)a.ncompute - 1) {  // the last block's inclusive prefix closes the turn
                 const unsigned long long end = excl + T;
                 a.run[1] = end;
                 if (a.stop_on_overflow && end > a.cap) atomicOr(&a.ctl[0], 1u);
@@ -2445,12 +2478,12 @@ int flip_turn_blocks_per_cu(bool contig) {
 }
 
 hipError_t launch_flip_turn(const FlipTurnArgs &a, hipStream_t s) {
-    const int64_t nb = flip_turn_blocks((int64_t)a.rows * a.Ww);
-    if (nb == 0) return hipSuccess;
+    const int64_t grid = (int64_t)a.ncompute + (a.cp_run ? a.cp_blocks : 0);
+    if (grid == 0) return hipSuccess;
     if (a.Ww % 4 == 0)
-        hipLaunchKernelGGL(gol_flip_turn_kernel<true>, dim3((unsigned)nb), dim3(kFtThreads), 0, s, a);
+        hipLaunchKernelGGL(gol_flip_turn_kernel<true>, dim3((unsigned)grid), dim3(kFtThreads), 0, s, a);
     else
-        hipLaunchKernelGGL(gol_flip_turn_kernel<false>, dim3((unsigned)nb), dim3(kFtThreads), 0, s, a);
+        hipLaunchKernelGGL(gol_flip_turn_kernel<false>, dim3((unsigned)grid), dim3(kFtThreads), 0, s, a);
     return hipGetLastError();
 }
 

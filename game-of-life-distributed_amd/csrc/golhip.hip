@@ -193,6 +193,7 @@ struct golhip {
     int64_t ev_cap_bytes = 0;
     unsigned flip_epoch = 0;
     int flip_debug = 0;  // option "flip_debug" (measurement only: wrong lists)
+    int flip_overlap = 1;  // option "flip_overlap": host lists copied by the next launch's copy blocks
     bool ft_ticket = false;       // K5 block order by ticket (set after a co-residency failure)
     uint64_t ft_est = 0;          // most entries of one turn in the last batch (launch sizing)
     int64_t flip_fallbacks = 0;
@@ -904,7 +905,7 @@ bool test_hooks_env() {
 constexpr const char *kTuningKeys[] = {
     "persist_depth", "persist_waves", "dummy_rows", "paired_bands", "persist_half", "persist_wg_tx", "trace",
     "cu_count", "fill_skip", "skew_young", "skew_hcap", "skew_prio", "skew_half", "skew_tx", "lds_depth",
-    "lds_waves", "lds_wg_cu", "lds_age", "lds_pre", "lds_stride", "lds_xcd"};
+    "lds_waves", "lds_wg_cu", "lds_age", "lds_pre", "lds_stride", "lds_xcd", "flip_overlap"};
 bool tuning_env() {
     const char *v = getenv("GOLHIP_TUNING");
     return (v && !strcmp(v, "1")) || measurement_env();
@@ -916,7 +917,7 @@ constexpr const char *kConsentInfo =
     " CONSENT_TEST_HOOKS=resident_fault,resident_max_turns,flip_debug:4,golhip_test_ring_init"
     " CONSENT_TUNING=persist_depth,persist_waves,dummy_rows,paired_bands,persist_half,persist_wg_tx,trace,cu_count,"
     "fill_skip,skew_young,skew_hcap,skew_prio,skew_half,skew_tx,lds_depth,lds_waves,lds_wg_cu,lds_age,lds_pre,"
-    "lds_stride,lds_xcd"
+    "lds_stride,lds_xcd,flip_overlap"
     " PRODUCT_OPTIONS=wpl,persistent,lds_band,skew,timing,persist_timeout_us,force_halo";
 
 // After the stream has synchronised: the K1w spin-bound flag of the launches
@@ -1447,9 +1448,13 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
     }
 
     // fused turn + list (K5) on the canonical layout; into a golhip_host_alloc
-    // buffer the kernel writes the entries itself (no device list, no copy)
+    // buffer the entries go without a host-side copy: each launch's copy
+    // blocks move the previous turn's list from the device list while the
+    // turn itself computes (option "flip_overlap", round 6), or (off) the
+    // turn's own blocks store their entries there directly
     if (int rc = set_layout(h, 0)) return rc;
     void *direct = mapped_device_ptr(out, (size_t)dcap * esz);
+    const bool overlap = direct && h->flip_overlap;
     const int64_t nb = golk::flip_turn_blocks(nw);
     const bool contig = h->Ww % 4 == 0;
     const int bpc = std::min(golk::flip_turn_blocks_per_cu(contig), 4);
@@ -1466,7 +1471,7 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
     if (int rc = ensure_dev(h, &h->d_ftticket, &h->ftticket_cap, nlaunch)) return rc;
     int64_t ctl_cap = h->d_ftctl ? 2 : 0;
     if (int rc = ensure_dev(h, &h->d_ftctl, &ctl_cap, 2)) return rc;
-    if (!direct) {
+    if (!direct || overlap) {
         int64_t bytes_cap = h->ev_cap_bytes;
         unsigned char *p = static_cast<unsigned char *>(h->d_ev);
         if (int rc = ensure_dev(h, &p, &bytes_cap, (int64_t)std::max<uint64_t>(dcap, 1) * esz)) return rc;
@@ -1479,7 +1484,13 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
         if (int rc = ensure_dev(h, &h->backup, &bcap, h->local_words())) return rc;
         HIP_OR_FAIL(hipMemcpyAsync(h->backup, h->cur_rows(), bytes, hipMemcpyDeviceToDevice, h->stream));
     }
-    HIP_OR_FAIL(hipMemsetAsync(h->d_run, 0, sizeof(unsigned long long), h->stream));
+    // every run bound zeroed: a turn that never ran (after a stop) reads as an
+    // empty list to the next launch's copy blocks
+    HIP_OR_FAIL(hipMemsetAsync(h->d_run, 0, (size_t)(nlaunch + 1) * sizeof(unsigned long long), h->stream));
+    // copy blocks: the slots the turn's blocks leave free (they come after
+    // them in the grid, so the turn's blocks stay co-resident), 32..256
+    const int cpb = overlap ? (int)std::max<int64_t>(32, std::min<int64_t>(256, (int64_t)h->cu_count * std::max(bpc, 1) - nb))
+                            : 0;
     HIP_OR_FAIL(hipMemsetAsync(h->d_ftticket, 0, (size_t)nlaunch * sizeof(unsigned), h->stream));
     HIP_OR_FAIL(hipMemsetAsync(h->d_ftctl, 0, 2 * sizeof(unsigned), h->stream));
     golk::StepArgs sa = step_args(h, nullptr, halo);
@@ -1498,7 +1509,11 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
         a.in = sa.in;
         a.row0 = h->row0;
         a.format = format == GOLHIP_FLIPS_XY ? golk::kFlipFormatXY : golk::kFlipFormatIdx;
-        a.out = direct ? direct : h->d_ev;
+        a.out = direct && !overlap ? direct : h->d_ev;
+        a.ncompute = (int)nb;
+        a.cp_run = overlap && t > 0 ? h->d_run + t - 1 : nullptr;
+        a.cp_dst = direct;
+        a.cp_blocks = cpb;
         a.cap = dcap;
         a.run = h->d_run + t;
         a.ticket = h->d_ftticket + t;
@@ -1526,6 +1541,31 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
         h->flip_launches++;
         h->cur ^= 1;
         h->turns += 1;
+    }
+    if (overlap && nlaunch > 0) {  // the last turn's list: a copy-only launch
+        golk::FlipTurnArgs a{};
+        a.Ww = h->Ww;
+        a.format = format == GOLHIP_FLIPS_XY ? golk::kFlipFormatXY : golk::kFlipFormatIdx;
+        a.out = h->d_ev;
+        a.cap = dcap;
+        a.ctl = h->d_ftctl;
+        a.stop_on_overflow = stop ? 1 : 0;
+        a.ncompute = 0;
+        a.cp_run = h->d_run + nlaunch - 1;
+        a.cp_dst = direct;
+        a.cp_blocks = 256;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (h->flags & GOLHIP_FLAG_TIMING) {
+            e0 = take_event(h);
+            e1 = take_event(h);
+            if (!e0 || !e1) return fail(GOLHIP_EHIP, "hipEventCreate failed");
+            HIP_OR_FAIL(hipEventRecord(e0, h->stream));
+        }
+        HIP_OR_FAIL(golk::launch_flip_turn(a, h->stream));
+        if (e1) {
+            HIP_OR_FAIL(hipEventRecord(e1, h->stream));
+            h->ev_pending.push_back({e0, e1, 2});
+        }
     }
     HIP_OR_FAIL(hipMemcpyAsync(run.data(), h->d_run, (size_t)(nlaunch + 1) * sizeof(unsigned long long),
                                hipMemcpyDeviceToHost, h->stream));
@@ -1841,6 +1881,11 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         if ((value & 4) && !test_hooks_env())
             return fail(GOLHIP_EINVAL, "flip_debug 4 is a test hook (GOLHIP_TEST_HOOKS=1)");
         h->flip_debug = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "flip_overlap")) {
+        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "flip_overlap %lld", (long long)value);
+        h->flip_overlap = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "force_halo")) {

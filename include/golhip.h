@@ -103,7 +103,8 @@ int golhip_device_count(int32_t *n);
 
 /* Page-locked host memory that the device writes directly (hipHostMalloc,
  * mapped).  A golhip_flip_stream whose `out` lies inside such a buffer gets
- * its entries written by the kernel itself over PCIe: no device list and no
+ * its entries written by the kernels themselves over PCIe (each turn's list
+ * by the next launch's copy blocks while that turn computes): no host-side
  * copy after the batch.  Go callers use it as C memory (unsafe.Slice). */
 int golhip_host_alloc(uint64_t bytes, void **out);
 int golhip_host_free(void *p);
@@ -163,7 +164,9 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * persist_depth, persist_waves, persist_half, persist_wg_tx, paired_bands,
  * dummy_rows, trace (golhip_persist_trace), cu_count, fill_skip, skew_young,
  * skew_hcap, skew_prio, skew_half, skew_tx, lds_depth, lds_waves, lds_wg_cu,
- * lds_age, lds_pre, lds_stride, lds_xcd.
+ * lds_age, lds_pre, lds_stride, lds_xcd, flip_overlap (1: a golhip_flip_stream
+ * into golhip_host_alloc memory copies each turn's list to the host while the
+ * next turn computes; 0: the turn's blocks store their entries there).
  *
  * Measurement only, refused without GOLHIP_MEASUREMENT=1 (WRONG results by
  * design): "halo_skip" (post no halo exchange), "flip_debug" 1-3.

@@ -92,10 +92,14 @@ def test_flip_stream_stops_without_loss(fixtures, coracle, W, H, fmt):
         assert np.array_equal(got[t], want[t]), t
 
 
-@pytest.mark.parametrize("fmt", [0, 1])
-def test_flip_stream_into_pinned_host_buffer(fixtures, coracle, fmt):
-    """out inside a golhip_host_alloc buffer: the kernel writes the entries
-    over PCIe itself; same lists, same early stop."""
+@pytest.mark.parametrize("fmt,overlap,shift", [(0, 1, 0), (1, 1, 0), (0, 1, 1), (1, 1, 3), (0, 0, 0), (1, 0, 1)])
+def test_flip_stream_into_pinned_host_buffer(fixtures, coracle, fmt, overlap, shift):
+    """out inside a golhip_host_alloc buffer: the kernels write the entries
+    over PCIe themselves -- with flip_overlap (default) each launch's copy
+    blocks move the previous turn's list while the turn computes, a last
+    copy-only launch the final turn's -- same lists, same early stop; `shift`
+    entries into the buffer the destination is not 16-byte aligned (the copy
+    blocks' 4-byte heads and tails)."""
     W = H = 512
     board = unpack_bits(fixtures["image_512"], 512)
     want, cur = [], board
@@ -104,9 +108,11 @@ def test_flip_stream_into_pinned_host_buffer(fixtures, coracle, fmt):
         want.append(flips_np(cur, nxt))
         cur = nxt
     cap = max(len(w) for w in want) * 4
-    out = golhip.host_array((cap, 2) if fmt == 0 else (cap,), np.int32 if fmt == 0 else np.uint32)
+    buf = golhip.host_array((cap + shift, 2) if fmt == 0 else (cap + shift,), np.int32 if fmt == 0 else np.uint32)
+    out = buf[shift:]
     got = []
     with golhip.Board(W, H) as b:
+        b.set_option("flip_overlap", overlap)
         b.load_bytes(board)
         while len(got) < 30:
             ent, counts, done = b.flip_stream(30 - len(got), cap=cap, fmt=fmt, out=out)
@@ -119,7 +125,7 @@ def test_flip_stream_into_pinned_host_buffer(fixtures, coracle, fmt):
         assert np.array_equal(b.snapshot_bytes(), cur)
     for t in range(30):
         assert np.array_equal(got[t], want[t]), t
-    del out
+    del out, buf
 
 
 def test_flip_stream_first_turn_too_big(fixtures):

@@ -243,3 +243,35 @@ def test_config4_5120_flip_stream_index(full):
         assert counts_all == rec["flip_counts"]
         assert sha.hexdigest() == rec["flips_sha256"]
         assert (f"{b.board_hash():016x}", b.alive_count()) == (rec["final"]["hash"], (rec["final"]["alive"], 50))
+
+
+@pytest.mark.parametrize("overlap", [1, 0])
+def test_config4_5120_flip_stream_pinned(full, overlap):
+    """configs[4] as bench.py streams it: 4-byte indices into golhip_host_alloc
+    memory, the host lists written by the copy blocks of the next launch while
+    each turn computes (flip_overlap 1, round 6) or by the turn's own blocks
+    (0); a 12 M-entry buffer makes calls stop before a turn that would not fit
+    and resume.  The stream hashes to the fixture."""
+    js, _ = full
+    rec = js["c4"]
+    N = rec["width"]
+    sha, counts_all = hashlib.sha256(), []
+    cap = 12 << 20
+    out = golhip.host_array((cap,), np.uint32)
+    with golhip.Board(N, N) as b:
+        b.set_option("flip_overlap", overlap)
+        b.fill_random(rec["seed"])
+        calls = 0
+        while len(counts_all) < rec["turns"]:
+            ent, counts, done = b.flip_stream(rec["turns"] - len(counts_all), cap=cap, fmt=golhip.FLIPS_INDEX,
+                                              out=out)
+            assert done >= 1
+            idx = ent.astype(np.int64)
+            sha.update(np.stack([idx % N, idx // N], axis=1).astype(np.int32).tobytes())
+            counts_all += [int(c) for c in counts]
+            calls += 1
+        assert calls > 10
+        assert counts_all == rec["flip_counts"]
+        assert sha.hexdigest() == rec["flips_sha256"]
+        assert (f"{b.board_hash():016x}", b.alive_count()) == (rec["final"]["hash"], (rec["final"]["alive"], 50))
+    del out
