@@ -79,9 +79,10 @@ struct SkewArgs {
     unsigned *error;  // nullable, host-mapped: set if a band's imports never arrived (spin bound)
     unsigned long long *trace;  // nullable diagnostics: per wave (start, end) s_memrealtime at 8 + 2 (block * 64 + wave),
                                 // (fill done, main loop done) at 8 + 2 (block * 64 + 8 + wave)
+    int pairs;        // 1: the pair rule in the main loop (8 LUTs a word-turn; bands in multiples of 6 rows)
 };
-bool skew_supported(int depth, int wpl, bool half = false);
-int skew_blocks_per_cu(int depth, int wpl, bool half = false);
+bool skew_supported(int depth, int wpl, bool half = false, bool pr = false);
+int skew_blocks_per_cu(int depth, int wpl, bool half = false, bool pr = false);
 hipError_t launch_skew(const SkewArgs &p, int depth, int wpl, hipStream_t s);
 
 // Persistent multi-super-step step kernel (torus, or a strip's extended rows

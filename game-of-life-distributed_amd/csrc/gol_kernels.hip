@@ -865,6 +865,146 @@ struct SkewPlan {
 };
 
 
+// ---------------------------------------------------------------------------
+// The pair rule in K1w's main loop (round 6; gol_bits.h pair_sum / pair_rule).
+// Generation-t rows pair up as (2m, 2m + 1) by the parity of their index in
+// the band's input frame (push j brings row j - t to stage t, so a row's
+// parity is that of j + t).  Per stage the state alternates:
+//  * before an odd row 2m + 1 arrives: a = S(2m - 1), b = S(2m), c = row 2m;
+//    the odd row completes the pair: p = b + S(2m + 1), out row 2m =
+//    pair_rule(a, p, c); then a = S(2m + 1), c = row 2m + 1 (b is dead);
+//  * before an even row 2m + 2 arrives: p, a = S(2m + 1), c = row 2m + 1;
+//    out row 2m + 1 = pair_rule(S(2m + 2), p, c); then b = S(2m + 2),
+//    c = row 2m + 2 (p is dead).
+// So a stage's live state is 5 words (a, b, c) or 6 (p, a, c) per word of a
+// lane, where the 9-LUT stage keeps 5: half the stages are in each phase, so
+// the pipeline costs 10 % more VGPRs and runs at most 18 turns a launch at two
+// words per lane (242 VGPRs at 20 with the 9-LUT stage).  Groups still hold 3
+// rows, so the phase of (group row q, stage t) flips from group to group: the
+// main loop takes two groups a body (KQ = parity of the group's first push).
+// The fill and drain keep the 9-LUT stages; pr_enter / pr_leave convert the
+// state between the two layouts (b from p and a: pair_unsum).
+// ---------------------------------------------------------------------------
+template <int D, int WPL>
+struct PairSt {
+    uint32_t a0[D][WPL], a1[D][WPL];
+    uint32_t b0[D][WPL], b1[D][WPL];
+    uint32_t p0[D][WPL], p1[D][WPL], p2[D][WPL];
+    uint32_t c[D][WPL];
+};
+
+// One stage (turn t) of a row of phase PH (1: odd row, completes its pair).
+template <int D, int PH, int WPL>
+__device__ __forceinline__ void stage_pr(int t, Lanes<WPL> &x, PairSt<D, WPL> &st) {
+    uint32_t west[WPL], east[WPL];
+    if constexpr (WPL == 1) {
+        const uint32_t l = from_left_lane(x.w[0]);
+        const uint32_t r = from_right_lane(x.w[0]);
+        west[0] = __builtin_amdgcn_alignbit(x.w[0], l, 31);
+        east[0] = __builtin_amdgcn_alignbit(r, x.w[0], 1);
+    } else if constexpr (WPL == 4) {
+        const uint32_t l3 = from_left_lane(x.w[3]);
+        const uint32_t r0 = from_right_lane(x.w[0]);
+        west[0] = __builtin_amdgcn_alignbit(x.w[3], l3, 31);
+        west[1] = x.w[0];
+        west[2] = x.w[1];
+        west[3] = x.w[2];
+        east[0] = x.w[1];
+        east[1] = x.w[2];
+        east[2] = x.w[3];
+        east[3] = __builtin_amdgcn_alignbit(r0, x.w[0], 1);
+    } else {
+        const uint32_t l1 = from_left_lane(x.w[1]);
+        const uint32_t r0 = from_right_lane(x.w[0]);
+        west[0] = __builtin_amdgcn_alignbit(x.w[1], l1, 31);
+        east[0] = x.w[1];
+        west[1] = x.w[0];
+        east[1] = __builtin_amdgcn_alignbit(r0, x.w[0], 1);
+    }
+    uint32_t nx[WPL];
+#pragma unroll
+    for (int k = 0; k < WPL; ++k) {
+        const uint32_t n0 = bop<kXor3>(west[k], x.w[k], east[k]);
+        const uint32_t n1 = bop<kMaj>(west[k], x.w[k], east[k]);
+        if constexpr (PH == 1) {
+            uint32_t p0, p1, p2;
+            pair_sum(st.b0[t][k], st.b1[t][k], n0, n1, p0, p1, p2);
+            nx[k] = pair_rule(st.a0[t][k], st.a1[t][k], p0, p1, p2, st.c[t][k]);
+            st.p0[t][k] = p0;
+            st.p1[t][k] = p1;
+            st.p2[t][k] = p2;
+            st.a0[t][k] = n0;
+            st.a1[t][k] = n1;
+        } else {
+            nx[k] = pair_rule(n0, n1, st.p0[t][k], st.p1[t][k], st.p2[t][k], st.c[t][k]);
+            st.b0[t][k] = n0;
+            st.b1[t][k] = n1;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < WPL; ++k) {
+        st.c[t][k] = x.w[k];
+        x.w[k] = nx[k];
+    }
+}
+
+// push_group on the pair state: rows of pushes KQ + 0, 1, 2 (mod 2).
+template <int D, int KQ, int WPL>
+__device__ __forceinline__ void push_group_pr(Lanes<WPL> &x0, Lanes<WPL> &x1, Lanes<WPL> &x2,
+                                              PairSt<D, WPL> &st) {
+    parity_fix<1>();
+    static_for<D + 2>([&](auto s_tag) {
+        constexpr int s = decltype(s_tag)::value;
+        parity_fix<2>();
+        if constexpr (s < D) stage_pr<D, (KQ + 0 + s) & 1, WPL>(s, x0, st);
+        if constexpr (s >= 1 && s - 1 < D) stage_pr<D, (KQ + 1 + s - 1) & 1, WPL>(s - 1, x1, st);
+        if constexpr (s >= 2) stage_pr<D, (KQ + 2 + s - 2) & 1, WPL>(s - 2, x2, st);
+    });
+}
+
+// 9-LUT stage state (slots 1, 2 = pushes k - 2, k - 1 of a push k = 0 mod 3)
+// -> pair state before push k (parity KQ); pr_leave the inverse.
+template <int D, int KQ, int WPL>
+__device__ __forceinline__ void pr_enter(const uint32_t (&h0)[3][D][WPL], const uint32_t (&h1)[3][D][WPL],
+                                         const uint32_t (&cc)[3][D][WPL], PairSt<D, WPL> &st) {
+#pragma unroll
+    for (int t = 0; t < D; ++t)
+#pragma unroll
+        for (int k = 0; k < WPL; ++k) {
+            st.c[t][k] = cc[2][t][k];
+            if (((KQ + t) & 1) == 1) {  // the next row completes a pair
+                st.a0[t][k] = h0[1][t][k];
+                st.a1[t][k] = h1[1][t][k];
+                st.b0[t][k] = h0[2][t][k];
+                st.b1[t][k] = h1[2][t][k];
+            } else {
+                pair_sum(h0[1][t][k], h1[1][t][k], h0[2][t][k], h1[2][t][k], st.p0[t][k], st.p1[t][k], st.p2[t][k]);
+                st.a0[t][k] = h0[2][t][k];
+                st.a1[t][k] = h1[2][t][k];
+            }
+        }
+}
+template <int D, int KQ, int WPL>
+__device__ __forceinline__ void pr_leave(const PairSt<D, WPL> &st, uint32_t (&h0)[3][D][WPL],
+                                         uint32_t (&h1)[3][D][WPL], uint32_t (&cc)[3][D][WPL]) {
+#pragma unroll
+    for (int t = 0; t < D; ++t)
+#pragma unroll
+        for (int k = 0; k < WPL; ++k) {
+            cc[2][t][k] = st.c[t][k];
+            if (((KQ + t) & 1) == 1) {
+                h0[1][t][k] = st.a0[t][k];
+                h1[1][t][k] = st.a1[t][k];
+                h0[2][t][k] = st.b0[t][k];
+                h1[2][t][k] = st.b1[t][k];
+            } else {
+                h0[2][t][k] = st.a0[t][k];
+                h1[2][t][k] = st.a1[t][k];
+                pair_unsum(st.p0[t][k], st.p1[t][k], st.a0[t][k], st.a1[t][k], h0[1][t][k], h1[1][t][k]);
+            }
+        }
+}
+
 // push_group for the last stages only: the group's rows enter stage LO.
 template <int D, int LO, int WPL>
 __device__ __forceinline__ void push_group_hi(Lanes<WPL> &x0, Lanes<WPL> &x1, Lanes<WPL> &x2,
@@ -889,7 +1029,7 @@ __device__ __forceinline__ void push_group_hi(Lanes<WPL> &x0, Lanes<WPL> &x1, La
 // of a wave on padding (16384^2: nine 60-word tiles for 512 words instead of
 // five 124-word ones).  Everything lane-wise (loads, stores, LDS hand-offs)
 // just takes the upper half's rows `dr` further down.
-template <int D, int WPL, bool HALF = false>
+template <int D, int WPL, bool HALF = false, bool PR = false>
 __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int eb, int tile, bool self,
                                                 uint32_t *exp_mine, const uint32_t *exp_next, int *flag_mine,
                                                 int *flag_next, unsigned *error, unsigned long long *phase_tr,
@@ -1006,7 +1146,58 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
     // main: every stage on board rows (the bottom band of a stack to the end)
     const int kmain = S + (self ? 2 * D : 2 * SP::P(0));
     for (int i = 0; i < GOL_LOOP_PAD; ++i) asm volatile("s_nop 0");
-    for (; k < kmain; k += 3) {
+    if constexpr (PR) {
+        // the pair rule, two groups a body: the fill leaves k at KSTART (= 0
+        // mod 6), other bands are multiples of 6 rows (gol_skew_kernel), so
+        // the loop ends exactly at kmain where a drain follows; a stack's
+        // bottom band may run up to 5 rows past its end (masked stores)
+        constexpr int KSTART = 3 * ((2 * D + 2) / 3);
+        static_assert(KSTART % 6 == 0, "the pair main loop starts at an even push");
+        if (k < kmain) {
+            PairSt<D, WPL> st;
+            pr_enter<D, 0, WPL>(h0, h1, cc, st);
+            for (; k < kmain; k += 6) {
+                {
+                    const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
+                    emit(q0, qoi);
+                    emit(q1, qoi + 1);
+                    emit(q2, qoi + 2);
+                    __builtin_amdgcn_sched_barrier(0);
+                    Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
+                    push_group_pr<D, 0, WPL>(y0, y1, y2, st);
+                    q0 = y0;
+                    q1 = y1;
+                    q2 = y2;
+                    qoi = k - 2 * D;
+                    __builtin_amdgcn_sched_barrier(0);
+                    x0 = vmov(n0);
+                    x1 = vmov(n1);
+                    x2 = vmov(n2);
+                }
+                {
+                    const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
+                    emit(q0, qoi);
+                    emit(q1, qoi + 1);
+                    emit(q2, qoi + 2);
+                    __builtin_amdgcn_sched_barrier(0);
+                    Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
+                    push_group_pr<D, 1, WPL>(y0, y1, y2, st);
+                    q0 = y0;
+                    q1 = y1;
+                    q2 = y2;
+                    qoi = k + 3 - 2 * D;
+                    __builtin_amdgcn_sched_barrier(0);
+                    x0 = vmov(n0);
+                    x1 = vmov(n1);
+                    x2 = vmov(n2);
+                }
+            }
+            // (unconditional, though only the drain reads it: the fill's state
+            // must not stay live across the loop for the bottom band's path)
+            pr_leave<D, 0, WPL>(st, h0, h1, cc);
+        }
+    }
+    for (; !PR && k < kmain; k += 3) {
         const Lanes<WPL> n0 = load_next(), n1 = load_next(), n2 = load_next();
         emit(q0, qoi);
         emit(q1, qoi + 1);
@@ -1110,7 +1301,7 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
 
 // K1w: one workgroup = one stack = tx tiles x (8 / tx) bands; wave w takes
 // tile w % tx and stack position w / tx (top to bottom).
-template <int D, int WPL, bool HALF = false>
+template <int D, int WPL, bool HALF = false, bool PR = false>
 __global__ __launch_bounds__(512) void gol_skew_kernel(SkewArgs p) {
     using SP = SkewPlan<D>;
     constexpr int ROW = 64 * WPL;
@@ -1140,11 +1331,13 @@ __global__ __launch_bounds__(512) void gol_skew_kernel(SkewArgs p) {
     }
     const bool bottom = pos == sy - 1;
     // band boundaries at multiples of 3 rows from the stack start (drain
-    // groups aligned with the drain phases, SkewPlan); the bottom band takes the rest
-    const int ab = A0 + (int)(Ls * cum / tot) / 3 * 3;
-    const int eb = bottom ? E0 : A0 + (int)(Ls * (cum + p.wgt[pos]) / tot) / 3 * 3;
+    // groups aligned with the drain phases, SkewPlan; 6 for the pair rule's
+    // two-group main-loop body); the bottom band takes the rest
+    constexpr int G = PR ? 6 : 3;
+    const int ab = A0 + (int)(Ls * cum / tot) / G * G;
+    const int eb = bottom ? E0 : A0 + (int)(Ls * (cum + p.wgt[pos]) / tot) / G * G;
     const long long t_start = p.trace ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
-    const uint32_t cnt = stream_skew<D, WPL, HALF>(p.base, ab, eb, tile, bottom, s_exp[w], bottom ? nullptr : s_exp[w + p.tx],
+    const uint32_t cnt = stream_skew<D, WPL, HALF, PR>(p.base, ab, eb, tile, bottom, s_exp[w], bottom ? nullptr : s_exp[w + p.tx],
                                              &s_flag[w], bottom ? nullptr : &s_flag[w + p.tx], p.error,
                                              (p.trace && blockIdx.x < 1024) ? p.trace + 8 + 2 * (blockIdx.x * 64 + 16 + w)
                                                                             : nullptr,
@@ -1906,26 +2099,30 @@ hipError_t launch_step_tb(const StepArgs &a, int depth, hipStream_t s, bool fill
 }
 
 template <typename F>
-static hipError_t dispatch_skew(int depth, int wpl, bool half, F &&f) {
+static hipError_t dispatch_skew(int depth, int wpl, bool half, bool pr, F &&f) {
 #define GOL_WCASE(D, WP) \
-    if (!half && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP>);
+    if (!pr && !half && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP>);
 #define GOL_HCASE(D, WP) \
-    if (half && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP, true>);
+    if (!pr && half && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP, true>);
+#define GOL_RCASE(D, WP, HF) \
+    if (pr && half == HF && depth == D && wpl == WP) return f(gol_skew_kernel<D, WP, HF, true>);
     GOL_WCASE(8, 2) GOL_WCASE(12, 2) GOL_WCASE(16, 2) GOL_WCASE(20, 2) GOL_WCASE(6, 4) GOL_WCASE(8, 4)
     GOL_WCASE(9, 4) GOL_WCASE(16, 1) GOL_WCASE(32, 1)
     GOL_HCASE(16, 2) GOL_HCASE(20, 2)
+    GOL_RCASE(18, 2, false) GOL_RCASE(18, 2, true)
 #undef GOL_WCASE
 #undef GOL_HCASE
+#undef GOL_RCASE
     return hipErrorInvalidValue;
 }
 
-bool skew_supported(int depth, int wpl, bool half) {
-    return dispatch_skew(depth, wpl, half, [](auto) { return hipSuccess; }) == hipSuccess;
+bool skew_supported(int depth, int wpl, bool half, bool pr) {
+    return dispatch_skew(depth, wpl, half, pr, [](auto) { return hipSuccess; }) == hipSuccess;
 }
 
-int skew_blocks_per_cu(int depth, int wpl, bool half) {
+int skew_blocks_per_cu(int depth, int wpl, bool half, bool pr) {
     int b = 0;
-    hipError_t e = dispatch_skew(depth, wpl, half, [&](auto kern) {
+    hipError_t e = dispatch_skew(depth, wpl, half, pr, [&](auto kern) {
         return hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 512, 0);
     });
     return e == hipSuccess ? b : 0;
@@ -1933,7 +2130,7 @@ int skew_blocks_per_cu(int depth, int wpl, bool half) {
 
 hipError_t launch_skew(const SkewArgs &p, int depth, int wpl, hipStream_t s) {
     const int tcols = (p.tiles_x + p.tx - 1) / p.tx;
-    return dispatch_skew(depth, wpl, p.half != 0, [&](auto kern) {
+    return dispatch_skew(depth, wpl, p.half != 0, p.pairs != 0, [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(tcols * p.nst), dim3(512), 0, s, p);
         return hipGetLastError();
     });

@@ -87,7 +87,7 @@ int fail(int code, const char *fmt, ...) {
 // Turns per launch with an instantiated step kernel (24: one word per lane
 // only, as 32; 9: four words per lane only, planned only under a cap of
 // exactly 9 (depth_cap); see max_depth_for).
-constexpr int kDepths[] = {32, 24, 20, 16, 12, 9, 8, 6, 4, 2, 1};
+constexpr int kDepths[] = {32, 24, 20, 18, 16, 12, 9, 8, 6, 4, 2, 1};
 constexpr int kNumDepths = sizeof(kDepths) / sizeof(kDepths[0]);
 // trace buffer: 8 totals + (start, end) per (workgroup < 1024, wave < 64)
 constexpr int64_t kTraceWords = 8 + 2 * 1024 * 64;
@@ -122,7 +122,8 @@ struct golhip {
     int lds_bpc[4] = {};               // K1r workgroups per CU by (wpl, 512 / 1024 threads) at lds_bpc_bytes of LDS
     int64_t lds_bpc_bytes[4] = {};
     int lds_bpc_stride[4] = {};
-    int skew_bpc[kNumDepths][6] = {};  // K1w workgroups per CU by (depth, wpl, half) (0: not queried)
+    int skew_bpc[kNumDepths][12] = {};  // K1w workgroups per CU by (depth, wpl, half, pairs) (0: not queried)
+    int skew_pairs = 0;             // option "skew_pairs": the pair rule (8 LUTs a word-turn) at depth 18
     unsigned *skew_err = nullptr;      // host-mapped spin-bound flag of the K1w kernels
     unsigned *skew_err_dev = nullptr;
     int64_t skew_launches = 0;
@@ -295,9 +296,12 @@ int64_t stage_rows(golhip_t h) {
 // the other word widths have no 9.
 int largest_depth(int64_t want) {
     for (int d : kDepths)
-        if (d <= want && d != 9) return d;
+        if (d <= want && d != 9 && d != 18) return d;
     return 1;
 }
+// Depths a plan capped at exactly them alone takes: 9 (quads) and 18 (the
+// pair-rule K1w, option "skew_pairs"); depth_cap.
+bool special_depth(int d) { return d == 9 || d == 18; }
 
 // The next run of launches for `left` turns of at most `cap` turns each:
 // depth d and how many launches of d come next.  The schedule has the fewest
@@ -313,7 +317,7 @@ struct DepthRun {
     int64_t n;
 };
 DepthRun depth_plan(int cap, int64_t left) {
-    const int M = cap == 9 ? 9 : largest_depth(std::max(1, cap));  // 9: quads (depth_cap)
+    const int M = special_depth(cap) ? cap : largest_depth(std::max(1, cap));  // 9: quads, 18: pairs (depth_cap)
     if (left <= 0) return {M, 0};
     const int64_t head = std::max<int64_t>(0, left / M - 12);  // launches of M before the planned tail
     const int t = (int)(left - head * M);                      // < 13 M <= 416
@@ -323,7 +327,7 @@ DepthRun depth_plan(int cap, int64_t left) {
     mn[0] = INT_MAX;
     for (int v = 1; v <= t; ++v)
         for (int d : kDepths) {  // descending: ties keep the larger depth
-            if (d > M || d > v || nl[v - d] == INT_MAX || (d == 9 && M != 9)) continue;
+            if (d > M || d > v || nl[v - d] == INT_MAX || (special_depth(d) && M != d)) continue;
             const int n = nl[v - d] + 1, m = std::min(mn[v - d], d);
             if (n < nl[v] || (n == nl[v] && m > mn[v])) {
                 nl[v] = n;
@@ -481,6 +485,13 @@ int depth_cap(golhip_t h, bool halo) {
         if (skew_dims(h, 20, 2, h->rows, &sk) && sk.half) cap = 16;
     }
     if (cap == 9 && (wpl != 4 || (halo && persist_on(h)))) cap = 8;  // only per-launch quads have 9
+    // the pair rule (option "skew_pairs"): K1w at 18 turns a launch, its
+    // state's VGPR bound at two words per lane, where a whole torus takes
+    // full-width tiles
+    if (h->skew_pairs && !halo && wpl == 2 && cap >= 18) {
+        golk::SkewArgs sk{};
+        if (skew_dims(h, 18, 2, h->rows, &sk) && !sk.half) cap = 18;
+    }
     return cap;
 }
 
@@ -649,10 +660,10 @@ void shift_rows(golk::StepArgs &a, int lo, int hi) {
 // band below's exports) and the stack's bottom band `hcap` rows shorter (it
 // computes its drain in full).  tx = 2 (stacks of 4
 // bands, two tiles a workgroup) when the tile count fits the CUs better.
-int skew_bpc(golhip_t h, int depth, int wpl, bool half) {
-    int &c = h->skew_bpc[depth_index(depth)][(wpl == 4 ? 2 : wpl - 1) + (half ? 3 : 0)];
+int skew_bpc(golhip_t h, int depth, int wpl, bool half, bool pr) {
+    int &c = h->skew_bpc[depth_index(depth)][(wpl == 4 ? 2 : wpl - 1) + (half ? 3 : 0) + (pr ? 6 : 0)];
     if (c == 0) {
-        const int b = golk::skew_blocks_per_cu(depth, wpl, half);
+        const int b = golk::skew_blocks_per_cu(depth, wpl, half, pr);
         c = b > 0 ? b : -1;
     }
     return c;
@@ -661,18 +672,19 @@ int skew_bpc(golhip_t h, int depth, int wpl, bool half) {
 // The stack plan of a K1w launch over L rows: tiles, workgroup shape, stacks
 // and tile kind (no side effects); false if K1w does not apply.
 bool skew_dims(golhip_t h, int depth, int wpl, int L, golk::SkewArgs *sk) {
-    if (!h->skew || h->W % 32 != 0 || !golk::skew_supported(depth, wpl)) return false;
+    const bool pr = depth == 18;  // only the pair-rule kernels run 18 turns (depth_cap)
+    if (!h->skew || h->W % 32 != 0 || !golk::skew_supported(depth, wpl, false, pr)) return false;
     const int hcap = h->skew_hcap >= 0 ? h->skew_hcap : 3 * depth / 4;
     const int smin = depth + 3;
     // half-wave tiles (30 stored lanes a tile, two tiles a wave, the upper one
     // L / 2 rows down): when they need fewer wave-rows than 62-lane tiles
     // (16384^2: 4.5 vs 5 waves a row), or when forced; L must be even
-    const bool half_ok = h->skew_half >= 0 && L % 2 == 0 && golk::skew_supported(depth, wpl, true);
+    const bool half_ok = h->skew_half >= 0 && L % 2 == 0 && golk::skew_supported(depth, wpl, true, pr);
     int best_tx = 0, best_nst = 0, best_half = 0, best_tiles = 0;
     double best = 1e300;
     for (int half = 0; half <= (half_ok ? 1 : 0); ++half) {
         if (!half && half_ok && h->skew_half > 0) continue;  // forced
-        const int bpc = skew_bpc(h, depth, wpl, half);
+        const int bpc = skew_bpc(h, depth, wpl, half, pr);
         if (bpc < 1) continue;
         const int tiles = half ? (h->Ww + golk::kHalfTileValid * wpl - 1) / (golk::kHalfTileValid * wpl)
                                : golk::tb_tiles(h->Ww, wpl);
@@ -704,6 +716,7 @@ bool skew_dims(golhip_t h, int depth, int wpl, int L, golk::SkewArgs *sk) {
     }
     if (!best_tx) return false;
     sk->tiles_x = best_tiles;
+    sk->pairs = pr ? 1 : 0;
     sk->tx = best_tx;
     sk->nst = best_nst;
     sk->half = best_half;
@@ -905,7 +918,7 @@ bool test_hooks_env() {
 constexpr const char *kTuningKeys[] = {
     "persist_depth", "persist_waves", "dummy_rows", "paired_bands", "persist_half", "persist_wg_tx", "trace",
     "cu_count", "fill_skip", "skew_young", "skew_hcap", "skew_prio", "skew_half", "skew_tx", "lds_depth",
-    "lds_waves", "lds_wg_cu", "lds_age", "lds_pre", "lds_stride", "lds_xcd", "flip_overlap"};
+    "lds_waves", "lds_wg_cu", "lds_age", "lds_pre", "lds_stride", "lds_xcd", "flip_overlap", "skew_pairs"};
 bool tuning_env() {
     const char *v = getenv("GOLHIP_TUNING");
     return (v && !strcmp(v, "1")) || measurement_env();
@@ -917,7 +930,7 @@ constexpr const char *kConsentInfo =
     " CONSENT_TEST_HOOKS=resident_fault,resident_max_turns,flip_debug:4,golhip_test_ring_init"
     " CONSENT_TUNING=persist_depth,persist_waves,dummy_rows,paired_bands,persist_half,persist_wg_tx,trace,cu_count,"
     "fill_skip,skew_young,skew_hcap,skew_prio,skew_half,skew_tx,lds_depth,lds_waves,lds_wg_cu,lds_age,lds_pre,"
-    "lds_stride,lds_xcd,flip_overlap"
+    "lds_stride,lds_xcd,flip_overlap,skew_pairs"
     " PRODUCT_OPTIONS=wpl,persistent,lds_band,skew,timing,persist_timeout_us,force_halo";
 
 // After the stream has synchronised: the K1w spin-bound flag of the launches
@@ -1881,6 +1894,11 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         if ((value & 4) && !test_hooks_env())
             return fail(GOLHIP_EINVAL, "flip_debug 4 is a test hook (GOLHIP_TEST_HOOKS=1)");
         h->flip_debug = (int)value;
+        return GOLHIP_OK;
+    }
+    if (!strcmp(key, "skew_pairs")) {
+        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "skew_pairs %lld", (long long)value);
+        h->skew_pairs = (int)value;
         return GOLHIP_OK;
     }
     if (!strcmp(key, "flip_overlap")) {

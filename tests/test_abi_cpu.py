@@ -135,7 +135,7 @@ def test_product_build_macros():
             # GOLHIP_TUNING=1; a product caller has the options below alone
             "CONSENT_TUNING": "persist_depth,persist_waves,dummy_rows,paired_bands,persist_half,persist_wg_tx,trace,"
                               "cu_count,fill_skip,skew_young,skew_hcap,skew_prio,skew_half,skew_tx,lds_depth,lds_waves,"
-                              "lds_wg_cu,lds_age,lds_pre,lds_stride,lds_xcd,flip_overlap",
+                              "lds_wg_cu,lds_age,lds_pre,lds_stride,lds_xcd,flip_overlap,skew_pairs",
             "PRODUCT_OPTIONS": "wpl,persistent,lds_band,skew,timing,persist_timeout_us,force_halo"}
     got = dict(kv.split("=", 1) for kv in info.split())
     assert got == want, info

@@ -74,6 +74,7 @@ def run_checkpoints(full, key, **options):
 
 # ---------------------------------------------------------------- configs[1]
 @pytest.mark.parametrize("opts", [{}, {"persistent": 1}, {"skew": 0, "persistent": 0}, {"wpl": 2},
+                                  {"persistent": 0, "skew_pairs": 1, "skew_half": -1},
                                   {"persistent": 0, "wpl": 4}, {"tb_depth": 32, "wpl": 1},
                                   {"persistent": 0, "tb_depth": 6}, {"tb_depth": 16}])
 def test_config1_16384_10k_turns(full, opts):
@@ -85,7 +86,7 @@ def test_config1_16384_10k_turns(full, opts):
 # ---------------------------------------------------------------- configs[2]
 @pytest.mark.parametrize("opts", [{}, {"skew": 0}, {"tb_depth": 16}, {"wpl": 4},
                                   {"persistent": 1}, {"wpl": 1, "tb_depth": 32}, {"skew_tx": 2},
-                                  {"skew_young": 70, "skew_prio": 1}])
+                                  {"skew_young": 70, "skew_prio": 1}, {"skew_pairs": 1}])
 def test_config2_65536_1k_turns(full, opts):
     """configs[2]: 65536^2, 1,000 turns (default: skewed band stacks, 20-turn launches;
     skew 0: the overlapped paired-band kernel)."""

@@ -692,7 +692,7 @@ def test_wrong_result_options_need_measurement_consent(monkeypatch):
 TUNING_KEYS = {"persist_depth": 8, "persist_waves": 8, "dummy_rows": 1, "paired_bands": 0, "persist_half": 0,
                "persist_wg_tx": 1, "trace": 0, "cu_count": 0, "fill_skip": 1, "skew_young": 60, "skew_hcap": 10,
                "skew_prio": 0, "skew_half": 0, "skew_tx": 1, "lds_depth": 8, "lds_waves": 8, "lds_wg_cu": 1,
-               "lds_age": 70, "lds_pre": 2, "lds_stride": 1, "lds_xcd": 1, "flip_overlap": 1}
+               "lds_age": 70, "lds_pre": 2, "lds_stride": 1, "lds_xcd": 1, "flip_overlap": 1, "skew_pairs": 0}
 PRODUCT_OPTIONS = {"wpl": 0, "persistent": -1, "lds_band": -1, "skew": 1, "timing": 0, "persist_timeout_us": 1000000,
                    "force_halo": 0}
 

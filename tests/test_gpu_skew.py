@@ -245,3 +245,29 @@ def test_default_plans_by_board_size():
         b.step(64)
         p = b.perf()
         assert p["persist_launches"] >= 1 and p["skew_launches"] == 0
+
+
+@pytest.mark.parametrize("W,H", [(2048, 1024), (4096, 777), (8192, 331), (3968, 2500), (16384, 1600), (7936, 4099)])
+@pytest.mark.parametrize("turns", [41, 18, 54, 17])
+def test_skew_pairs_matches_oracle(coracle, W, H, turns):
+    """The pair rule (option skew_pairs, gol_bits.h pair_sum / pair_rule):
+    K1w at 18 turns a launch on full-width tiles, its main loop in two-group
+    bodies on the pair state, the fill and drain on the 9-LUT stages with the
+    state converted between them (pr_enter / pr_leave), bands in multiples of
+    6 rows; remainders on 16 / 12 / ... -turn launches of the other kernels."""
+    board = coracle.fill_random(W, H, 0x5EED0071 + W + H)
+    want = coracle.run(board, turns)
+    got, p = run_skew(board, turns, 20, 2, skew_pairs=1, skew_half=-1)
+    if turns >= 18:
+        assert p["tb_depth"] == 18 and p["skew_launches"] >= turns // 18, p
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("young,tx", [(60, 1), (100, 2), (150, 1)])
+def test_skew_pairs_band_shapes(coracle, young, tx):
+    """Pair-rule bands of other heights and stacks of 4 bands."""
+    board = coracle.fill_random(6080, 3000, 0x5EED0077 + young + tx)
+    want = coracle.run(board, 40)
+    got, p = run_skew(board, 40, 20, 2, skew_pairs=1, skew_half=-1, skew_young=young, skew_tx=tx)
+    assert p["skew_launches"] >= 2
+    assert np.array_equal(got, want)
