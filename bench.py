@@ -274,9 +274,10 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str, 
     The kernels are VALU-issue-bound: a launch fuses 8-16
     turns per board pass, so HBM moves ~1/D of the single-pass bytes.  `frac`
     is therefore the VALU issue fraction: algorithmic issue slots per launch
-    (output words x turns / 64 lanes x slots per word-turn: 9 bitop3 LUTs + 2
-    half-rate shifts per `words_per_lane` words, i.e. 9 + 8/wpl; tile-halo
-    lanes and pipeline fill are overhead, not counted) / launch time / peak.
+    (output words x turns / 64 lanes x slots per word-turn: 9 bitop3 LUTs, 8
+    on the pair rule's launches, + 2 half-rate shifts per `words_per_lane`
+    words, i.e. 9 + 8/wpl or 8 + 8/wpl; tile-halo lanes and pipeline fill are
+    overhead, not counted) / launch time / peak.
     The HBM side comes from the rocprofv3 PMC passes of this same bench
     command (scripts/pmc_bench.sh -> profiles/pmc_bench.json): measured bytes
     (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) per launch of the same
@@ -294,7 +295,10 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str, 
     launches = max(1, launches)
     avg_s = kms / launches * 1e-3
     wpl = max(1, perf["words_per_lane"])
-    spw = 9.0 + 8.0 / wpl
+    # 9 LUTs a word-turn, 8 on the pair rule's launches (round 6, DESIGN.md
+    # §5.13), + the two half-rate shifts per wpl words; weighted by turns
+    pt = min(perf.get("pair_turns", 0), kturns) if kname == "gol_skew_kernel" else 0
+    spw = 9.0 + 8.0 / wpl - (pt / kturns if kturns else 0.0)
     words = rows * ((W + 31) // 32)
     tpl = kturns / launches
     if depth is None and abs(tpl - round(tpl)) < 1e-9:
@@ -318,7 +322,8 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str, 
         "launches": launches,
         "skew_launches": perf.get("skew_launches", 0),
         "turns_per_launch": tpl,
-        "slots_per_word_turn": spw,
+        "slots_per_word_turn": round(spw, 4),
+        "pair_rule_turns": pt,
         "alg_bytes_per_launch": alg_bytes,
         "temporal_blocking": {"alg_bytes_GBps": round(alg_bytes / avg_s / 1e9, 1) if avg_s > 0 else None,
                               "note": "0.25 B/cell-update (SURVEY 8d) over the launch time: the single-pass "

@@ -207,7 +207,7 @@ struct FlipTurnArgs {
                                     // 0: virtual ids from `ticket` and a decoupled look-back
     unsigned long long *alive;      // nullable: += popcount of the new board
     // Host copy of the PREVIOUS turn's list, overlapped with this turn (round
-    // 6): cp_blocks extra blocks after the turn's own (every block when the
+    // 6): cp_blocks extra blocks ahead of the turn's own (every block when the
     // launch is copy-only, ncompute 0) copy entries [cp_run[0], cp_run[1])
     // (cut at cap; none when stop_on_overflow and that turn overflowed) from
     // the device list `out` to the host list cp_dst (golhip_host_alloc memory).

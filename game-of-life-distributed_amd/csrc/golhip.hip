@@ -123,7 +123,8 @@ struct golhip {
     int64_t lds_bpc_bytes[4] = {};
     int lds_bpc_stride[4] = {};
     int skew_bpc[kNumDepths][12] = {};  // K1w workgroups per CU by (depth, wpl, half, pairs) (0: not queried)
-    int skew_pairs = 0;             // option "skew_pairs": the pair rule (8 LUTs a word-turn) at depth 18
+    int skew_pairs = 1;             // option "skew_pairs": the pair rule (8 LUTs a word-turn) at depth 18
+    int64_t pair_launches = 0, pair_turns = 0;
     unsigned *skew_err = nullptr;      // host-mapped spin-bound flag of the K1w kernels
     unsigned *skew_err_dev = nullptr;
     int64_t skew_launches = 0;
@@ -485,12 +486,15 @@ int depth_cap(golhip_t h, bool halo) {
         if (skew_dims(h, 20, 2, h->rows, &sk) && sk.half) cap = 16;
     }
     if (cap == 9 && (wpl != 4 || (halo && persist_on(h)))) cap = 8;  // only per-launch quads have 9
-    // the pair rule (option "skew_pairs"): K1w at 18 turns a launch, its
-    // state's VGPR bound at two words per lane, where a whole torus takes
-    // full-width tiles
-    if (h->skew_pairs && !halo && wpl == 2 && cap >= 18) {
+    // the pair rule (option "skew_pairs", round 6): K1w at 18 turns a launch
+    // (the pair state's VGPR bound at two words per lane) wherever its stacks
+    // plan on full-width tiles: whole tori, and ring strips (every rank
+    // decides from the ring's smallest strip; the extended rows of a strip's
+    // launches only make the stacks easier to plan).  Half-tile tori stay at
+    // 16 (their launches are mostly ramps, which the pair rule leaves alone).
+    if (h->skew_pairs && wpl == 2 && cap >= 18) {
         golk::SkewArgs sk{};
-        if (skew_dims(h, 18, 2, h->rows, &sk) && !sk.half) cap = 18;
+        if (skew_dims(h, 18, 2, halo ? sched_rows(h) : h->rows, &sk) && !sk.half) cap = 18;
     }
     return cap;
 }
@@ -821,6 +825,10 @@ int launch_rows(golhip_t h, int depth, unsigned long long *alive, bool halo, int
     h->step_launches++;
     h->skew_launches += skew;
     h->skew_half_launches += skew && sk.half;
+    if (skew && sk.pairs) {
+        h->pair_launches++;
+        h->pair_turns += depth;
+    }
     return GOLHIP_OK;
 }
 
@@ -2226,6 +2234,7 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     const int64_t step_launches0 = h->step_launches, step_turns0 = h->step_turns;
     const int64_t skew_launches0 = h->skew_launches;
     const int64_t skew_half_launches0 = h->skew_half_launches, lds_launches0 = h->lds_launches;
+    const int64_t pair_launches0 = h->pair_launches, pair_turns0 = h->pair_turns;
     const size_t ev0 = h->ev_pending.size();
     const int64_t halo_exchanges0 = h->halo_exchanges, halo_bytes0 = h->halo_bytes;
     int rc = step_locked(h, nturns, want_flips);
@@ -2255,6 +2264,8 @@ int golhip_step(golhip_t h, int64_t nturns, int32_t want_flips) {
     h->skew_launches = skew_launches0;
     h->skew_half_launches = skew_half_launches0;
     h->lds_launches = lds_launches0;
+    h->pair_launches = pair_launches0;
+    h->pair_turns = pair_turns0;
     h->halo_exchanges = halo_exchanges0;
     h->halo_bytes = halo_bytes0;
     if (h->ev_pending.size() >= ev0) {  // the abandoned attempt's launch timings (unless drained meanwhile)
@@ -2615,6 +2626,8 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     out->reserved2 = 0;
     out->skew_half_launches = h->skew_half_launches;
     out->lds_launches = h->lds_launches;
+    out->pair_launches = h->pair_launches;
+    out->pair_turns = h->pair_turns;
     out->words_per_lane = h->W % 32 == 0 ? wpl_for(h) : 0;
     out->persist_depth = h->W % 32 == 0 ? persist_depth_for(h, wpl_for(h)) : 0;
     return GOLHIP_OK;
@@ -2658,6 +2671,8 @@ int golhip_perf_reset(golhip_t h) {
     h->halo_ms = 0;
     h->skew_half_launches = 0;
     h->lds_launches = 0;
+    h->pair_launches = 0;
+    h->pair_turns = 0;
     return GOLHIP_OK;
 }
 

@@ -61,6 +61,8 @@ class Perf(ctypes.Structure):
         ("reserved2", ctypes.c_int64),
         ("skew_half_launches", ctypes.c_int64),
         ("lds_launches", ctypes.c_int64),
+        ("pair_launches", ctypes.c_int64),
+        ("pair_turns", ctypes.c_int64),
     ]
 
     def as_dict(self) -> dict:

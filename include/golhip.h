@@ -91,6 +91,9 @@ typedef struct golhip_perf {
     int64_t skew_half_launches; /* of skew_launches, those on half-wave tiles    */
     int64_t lds_launches;     /* of persist_launches, those that ran resident LDS
                                  bands (gol_lds_band_kernel, kernel_variant 4)  */
+    int64_t pair_launches;    /* of skew_launches, those on the pair rule (option
+                                 "skew_pairs": 8 LUTs a word-turn; round 6)     */
+    int64_t pair_turns;       /* turns run by those                              */
 } golhip_perf_t;
 
 /* ---- library ---------------------------------------------------------- */
