@@ -2044,6 +2044,7 @@ static hipError_t dispatch(int depth, bool skip, int wpl, F &&f) {
     GOL_CASE(1, true, 2) GOL_CASE(2, true, 2) GOL_CASE(4, true, 2) GOL_CASE(8, true, 2) GOL_CASE(16, true, 2)
     GOL_CASE(1, false, 2) GOL_CASE(2, false, 2) GOL_CASE(4, false, 2) GOL_CASE(8, false, 2) GOL_CASE(16, false, 2)
     GOL_CASE(20, true, 1) GOL_CASE(20, false, 1) GOL_CASE(20, true, 2) GOL_CASE(20, false, 2)
+    GOL_CASE(18, true, 2) GOL_CASE(18, false, 2)  // the pair rule's depth where a strip's K1w does not plan
 #undef GOL_CASE
     return hipErrorInvalidValue;
 }
@@ -2070,6 +2071,7 @@ static hipError_t dispatch_pair(int depth, int wpl, F &&f, bool cnt = false) {
     GOL_QCASE(1, 2) GOL_QCASE(2, 2) GOL_QCASE(4, 2) GOL_QCASE(8, 2) GOL_QCASE(16, 2)
     GOL_QCASE(12, 1) GOL_QCASE(24, 1) GOL_QCASE(12, 2) GOL_QCASE(1, 4) GOL_QCASE(2, 4) GOL_QCASE(4, 4) GOL_QCASE(8, 4)
     GOL_QCASE(6, 1) GOL_QCASE(6, 2) GOL_QCASE(6, 4) GOL_QCASE(9, 4) GOL_QCASE(20, 1) GOL_QCASE(20, 2)
+    GOL_QCASE(18, 2)
 #undef GOL_QCASE
     return hipErrorInvalidValue;
 }
@@ -2109,7 +2111,7 @@ static hipError_t dispatch_skew(int depth, int wpl, bool half, bool pr, F &&f) {
     GOL_WCASE(8, 2) GOL_WCASE(12, 2) GOL_WCASE(16, 2) GOL_WCASE(20, 2) GOL_WCASE(6, 4) GOL_WCASE(8, 4)
     GOL_WCASE(9, 4) GOL_WCASE(16, 1) GOL_WCASE(32, 1)
     GOL_HCASE(16, 2) GOL_HCASE(20, 2)
-    GOL_RCASE(18, 2, false) GOL_RCASE(18, 2, true)
+    GOL_RCASE(18, 2, false) GOL_RCASE(18, 2, true) GOL_RCASE(8, 4, false)
 #undef GOL_WCASE
 #undef GOL_HCASE
 #undef GOL_RCASE

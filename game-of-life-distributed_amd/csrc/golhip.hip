@@ -492,9 +492,14 @@ int depth_cap(golhip_t h, bool halo) {
     // decides from the ring's smallest strip; the extended rows of a strip's
     // launches only make the stacks easier to plan).  Half-tile tori stay at
     // 16 (their launches are mostly ramps, which the pair rule leaves alone).
-    if (h->skew_pairs && wpl == 2 && cap >= 18) {
+    if ((h->skew_pairs & 1) && wpl == 2 && cap >= 18) {
         golk::SkewArgs sk{};
         if (skew_dims(h, 18, 2, halo ? sched_rows(h) : h->rows, &sk) && !sk.half) cap = 18;
+    }
+    // quads (bit 2): 8 turns a launch on the pair rule instead of 9 on the 9-LUT stages
+    if ((h->skew_pairs & 2) && wpl == 4 && cap >= 8) {
+        golk::SkewArgs sk{};
+        if (skew_dims(h, 8, 4, halo ? sched_rows(h) : h->rows, &sk) && !sk.half) cap = 8;
     }
     return cap;
 }
@@ -676,7 +681,9 @@ int skew_bpc(golhip_t h, int depth, int wpl, bool half, bool pr) {
 // The stack plan of a K1w launch over L rows: tiles, workgroup shape, stacks
 // and tile kind (no side effects); false if K1w does not apply.
 bool skew_dims(golhip_t h, int depth, int wpl, int L, golk::SkewArgs *sk) {
-    const bool pr = depth == 18;  // only the pair-rule kernels run 18 turns (depth_cap)
+    // the pair rule: 18 turns at two words per lane (no other kernel runs 18,
+    // depth_cap), 8 at four (option "skew_pairs" bit 2)
+    const bool pr = depth == 18 || (wpl == 4 && depth == 8 && (h->skew_pairs & 2));
     if (!h->skew || h->W % 32 != 0 || !golk::skew_supported(depth, wpl, false, pr)) return false;
     const int hcap = h->skew_hcap >= 0 ? h->skew_hcap : 3 * depth / 4;
     const int smin = depth + 3;
@@ -1905,7 +1912,7 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         return GOLHIP_OK;
     }
     if (!strcmp(key, "skew_pairs")) {
-        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "skew_pairs %lld", (long long)value);
+        if (value < 0 || value > 3) return fail(GOLHIP_EINVAL, "skew_pairs %lld", (long long)value);
         h->skew_pairs = (int)value;
         return GOLHIP_OK;
     }

@@ -35,6 +35,7 @@ def run_skew(board, turns, depth, wpl, **opts):
         b.set_option("persistent", 0)
         b.set_option("skew", 2)  # whenever a plan exists (the default also wants the CUs filled)
         b.set_option("wpl", wpl)
+        b.set_option("skew_pairs", 0)  # the instantiation under test, not the pair rule's 18 (opts may set it)
         for k, v in opts.items():
             b.set_option(k, v)
         b.set_tb_depth(depth)
@@ -92,7 +93,7 @@ def test_skew_band_heights(coracle, depth, wpl, opts):
     assert np.array_equal(got, want)
 
 
-@pytest.mark.parametrize("depth,wpl", [(20, 2), (16, 2), (8, 4), (9, 4), (16, 1), (32, 1)])
+@pytest.mark.parametrize("depth,wpl", [(20, 2), (16, 2), (8, 4), (9, 4), (16, 1), (32, 1), (18, 2)])
 @pytest.mark.parametrize("W,H", [(4096, 1500), (8192, 700), (2048, 4096)])
 def test_skew_rccl_ring_one_rank(coracle, depth, wpl, W, H):
     """The multi-GPU path on K1w: deep-halo exchange, then launches over the
@@ -106,18 +107,22 @@ def test_skew_rccl_ring_one_rank(coracle, depth, wpl, W, H):
         b.set_option("persistent", 0)
         b.set_option("skew", 2)
         b.set_option("wpl", wpl)
-        b.set_tb_depth(depth)
+        b.set_option("skew_pairs", 3 if depth == 18 else 0)
+        if depth == 18:
+            b.set_option("skew_half", -1)  # (the pair rule plans on full-width tiles)
+        b.set_tb_depth(20 if depth == 18 else depth)
         b.load_bytes(board)
         b.step(turns)
         p = b.perf()
         assert p["halo_bytes"] > 0 and p["skew_launches"] >= 3
+        assert (p["pair_launches"] >= 3) == (depth == 18), p
         assert np.array_equal(b.snapshot_bytes(), want)
         assert b.alive_count() == (int((want == 255).sum()), turns)
 
 
 @pytest.mark.parametrize("nstrips", [2, 3, 5])
-@pytest.mark.parametrize("depth,wpl", [(20, 2), (9, 4)])
-def test_skew_group_strips(coracle, nstrips, depth, wpl):
+@pytest.mark.parametrize("depth,wpl,pairs", [(20, 2, 0), (9, 4, 0), (20, 2, 1), (9, 4, 2)])
+def test_skew_group_strips(coracle, nstrips, depth, wpl, pairs):
     """In-process row strips (halos by device copies) stepped on K1w."""
     W, H = 4096, 3001
     board = coracle.fill_random(W, H, 0x5EED0035 + nstrips)
@@ -129,6 +134,8 @@ def test_skew_group_strips(coracle, nstrips, depth, wpl):
         for i, s in enumerate(strips):
             s.set_option("wpl", wpl)
             s.set_option("skew", 2)
+            s.set_option("skew_pairs", pairs)
+            s.set_option("skew_half", -1 if pairs else 0)
             s.set_tb_depth(depth)
             s.load_bytes(board[bounds[i]:bounds[i + 1]])
         golhip.group_step(strips, turns)
@@ -155,6 +162,7 @@ def test_skew_every_launch_counts(coracle):
     with golhip.Board(8192, 1200) as b:
         b.set_option("persistent", 0)
         b.set_option("skew", 2)
+        b.set_option("skew_pairs", 0)
         b.set_tb_depth(20)
         b.load_bytes(board)
         cur = board
@@ -228,8 +236,9 @@ def test_skew_half_tiles_rccl_ring_and_strips(coracle, W, H):
 def test_default_plans_by_board_size():
     """The default plan: half-wave tiles at 16384^2 (configs[1]: 4.5 instead
     of 5 waves a row) with 16-turn launches (its bands are mostly ramp),
-    full tiles and 20-turn launches at 65536^2, and the resident kernel for
-    tori whose K1w stacks would not fill the CUs (8192^2)."""
+    full tiles and 18-turn launches on the pair rule at 65536^2 (round 6),
+    and the resident kernel for tori whose K1w stacks would not fill the CUs
+    (8192^2)."""
     with golhip.Board(16384, 16384) as b:
         b.fill_random(0x5EED0001)
         b.step(32)
@@ -237,9 +246,10 @@ def test_default_plans_by_board_size():
         assert p["skew_launches"] == 2 and p["skew_half_launches"] == 2 and p["step_turns"] == 32
     with golhip.Board(65536, 4096) as b:
         b.fill_random(0x5EED0002)
-        b.step(20)
+        b.step(18)
         p = b.perf()
-        assert p["skew_half_launches"] == 0 and p["skew_launches"] == 1
+        assert p["skew_half_launches"] == 0 and p["skew_launches"] == 1 and p["pair_launches"] == 1
+        assert p["tb_depth"] == 18
     with golhip.Board(8192, 8192) as b:
         b.fill_random(0x5EED0003)
         b.step(64)
