@@ -99,7 +99,8 @@ def test_skew_rccl_ring_one_rank(coracle, depth, wpl, W, H):
     """The multi-GPU path on K1w: deep-halo exchange, then launches over the
     extended row ranges [-e, rows + e) (one-rank RCCL ring, force_halo)."""
     board = coracle.fill_random(W, H, 0x5EED0034 + W)
-    turns = 7 * depth + 2
+    # (the pair rule: 7 launches of 18; 128 turns would plan as 8 x 16)
+    turns = 7 * depth + (0 if depth == 18 else 2)
     want = coracle.run(board, turns)
     with golhip.Board(W, H) as b:
         b.comm_init(golhip.unique_id(), 1, 0)
