@@ -334,6 +334,11 @@ def roofline_block(perf: dict, W: int, rows: int, workload: int, pmc_path: str, 
             rec = json.load(f).get(f"{workload}:{kname}")
     except (OSError, ValueError):
         rec = None
+    if rec and kname != "gol_persist_kernel" and abs(rec.get("turns_per_launch", 0) - tpl) > 1e-6:
+        # counters of another launch plan (an older tree): not this line's kernel
+        out["pmc_stale"] = {"source": os.path.relpath(pmc_path, ROOT), "bench_kernel": rec.get("bench_kernel"),
+                            "turns_per_launch": rec.get("turns_per_launch")}
+        rec = None
     if rec:
         traffic = rec["hbm_bytes_per_launch"] * (tpl / rec["turns_per_launch"] if kname == "gol_persist_kernel" else 1)
         out["traffic"] = traffic
@@ -1020,7 +1025,8 @@ def measure(a, env, workload: int, steps: int, warmup: int, warmup_seconds: floa
             "warmup": warmup, "warmup_extra_steps": extra, "ms_per_step": round(dt / steps * 1e3, 4),
             "parity": parity["ok"], "parity_check": parity,
             "config": {"workload": wl["desc"], "board": [H, W], "rows_per_rank": rows, "turns_per_step": tps,
-                       "tb_depth": a.tb_depth, "rows_per_wave": perf["rows_per_wave"],
+                       "tb_depth": a.tb_depth,  # the cap asked for; the plan's launches: roofline.turns_per_launch
+                       "rows_per_wave": perf["rows_per_wave"],
                        "words_per_lane": perf["words_per_lane"],
                        "parallelism": f"row strips x{world} (RCCL halo ring)" if world > 1 else
                        "one-rank RCCL ring (force_halo)" if ringed else "single GPU torus",
