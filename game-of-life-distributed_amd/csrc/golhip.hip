@@ -123,7 +123,7 @@ struct golhip {
     int64_t lds_bpc_bytes[4] = {};
     int lds_bpc_stride[4] = {};
     int skew_bpc[kNumDepths][12] = {};  // K1w workgroups per CU by (depth, wpl, half, pairs) (0: not queried)
-    int skew_pairs = 1;             // option "skew_pairs": the pair rule (8 LUTs a word-turn) at depth 18
+    int skew_pairs = 5;             // option "skew_pairs": the pair rule (8 LUTs a word-turn) at depth 18 (depth_cap)
     int64_t pair_launches = 0, pair_turns = 0;
     unsigned *skew_err = nullptr;      // host-mapped spin-bound flag of the K1w kernels
     unsigned *skew_err_dev = nullptr;
@@ -478,24 +478,28 @@ int depth_cap(golhip_t h, bool halo) {
     const int wpl = wpl_for(h);
     int cap = std::min(h->tb_depth, (halo && persist_on(h)) ? golk::persist_max_depth(wpl) : golk::max_depth_for(wpl));
     if (halo) cap = std::min(cap, sched_rows(h));
-    // whole tori whose K1w plan takes half-wave tiles (bands of ~2D rows, the
-    // launch mostly ramps) fuse 16 turns: 16384^2 86.3-86.5
-    // vs 85.5-85.7 TCUPS at 20 (profiles/r5v; 82.1 vs 81.2 in r4y)
-    if (!halo && wpl == 2 && cap > 16) {
+    // the pair rule (option "skew_pairs", round 6): K1w at 18 turns a launch
+    // (the pair state's VGPR bound at two words per lane): whole tori, and
+    // ring strips (every rank decides from the ring's smallest strip; the
+    // extended rows of a strip's launches only make the stacks easier to
+    // plan).  Bit 1: plans on full-width tiles; bit 4: half-wave tile plans
+    // too (16384^2 87.9 vs 86.4 TCUPS at 16 on the 9-LUT stages, profiles/r7c)
+    bool pair = false;
+    if ((h->skew_pairs & 1) && wpl == 2 && cap >= 18) {
+        golk::SkewArgs sk{};
+        if (skew_dims(h, 18, 2, halo ? sched_rows(h) : h->rows, &sk) && (!sk.half || (h->skew_pairs & 4))) {
+            cap = 18;
+            pair = true;
+        }
+    }
+    // other whole tori whose K1w plan takes half-wave tiles (bands of ~2D
+    // rows, the launch mostly ramps) fuse 16 turns: 16384^2
+    // 86.3-86.5 vs 85.5-85.7 TCUPS at 20 (profiles/r5v; 82.1 vs 81.2 in r4y)
+    if (!pair && !halo && wpl == 2 && cap > 16) {
         golk::SkewArgs sk{};
         if (skew_dims(h, 20, 2, h->rows, &sk) && sk.half) cap = 16;
     }
     if (cap == 9 && (wpl != 4 || (halo && persist_on(h)))) cap = 8;  // only per-launch quads have 9
-    // the pair rule (option "skew_pairs", round 6): K1w at 18 turns a launch
-    // (the pair state's VGPR bound at two words per lane) wherever its stacks
-    // plan on full-width tiles: whole tori, and ring strips (every rank
-    // decides from the ring's smallest strip; the extended rows of a strip's
-    // launches only make the stacks easier to plan).  Half-tile tori stay at
-    // 16 (their launches are mostly ramps, which the pair rule leaves alone).
-    if ((h->skew_pairs & 1) && wpl == 2 && cap >= 18) {
-        golk::SkewArgs sk{};
-        if (skew_dims(h, 18, 2, halo ? sched_rows(h) : h->rows, &sk) && !sk.half) cap = 18;
-    }
     // quads (bit 2): 8 turns a launch on the pair rule instead of 9 on the 9-LUT stages
     if ((h->skew_pairs & 2) && wpl == 4 && cap >= 8) {
         golk::SkewArgs sk{};
@@ -1912,7 +1916,7 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         return GOLHIP_OK;
     }
     if (!strcmp(key, "skew_pairs")) {
-        if (value < 0 || value > 3) return fail(GOLHIP_EINVAL, "skew_pairs %lld", (long long)value);
+        if (value < 0 || value > 7) return fail(GOLHIP_EINVAL, "skew_pairs %lld", (long long)value);
         h->skew_pairs = (int)value;
         return GOLHIP_OK;
     }

@@ -167,8 +167,10 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * persist_depth, persist_waves, persist_half, persist_wg_tx, paired_bands,
  * dummy_rows, trace (golhip_persist_trace), cu_count, fill_skip, skew_young,
  * skew_hcap, skew_prio, skew_half, skew_tx, lds_depth, lds_waves, lds_wg_cu,
- * lds_age, lds_pre, lds_stride, lds_xcd, skew_pairs (1: whole tori on full-width
- * K1w tiles run 18 turns a launch with the pair rule, 8 LUTs a word-turn),
+ * lds_age, lds_pre, lds_stride, lds_xcd, skew_pairs (bit 1: tori and strips on
+ * full-width K1w tiles run 18 turns a launch with the pair rule, 8 LUTs a
+ * word-turn; bit 4: half-wave tile plans too; bit 2: quads at 8 on the pair
+ * rule; default 5),
  * flip_overlap (1: a golhip_flip_stream
  * into golhip_host_alloc memory copies each turn's list to the host while the
  * next turn computes; 0: the turn's blocks store their entries there).

@@ -74,12 +74,14 @@ def run_checkpoints(full, key, **options):
 
 # ---------------------------------------------------------------- configs[1]
 @pytest.mark.parametrize("opts", [{}, {"persistent": 1}, {"skew": 0, "persistent": 0}, {"wpl": 2},
-                                  {"persistent": 0, "skew_pairs": 1, "skew_half": -1},
+                                  {"persistent": 0, "skew_pairs": 1, "skew_half": -1}, {"skew_pairs": 1},
                                   {"persistent": 0, "wpl": 4}, {"tb_depth": 32, "wpl": 1},
                                   {"persistent": 0, "tb_depth": 6}, {"tb_depth": 16}])
 def test_config1_16384_10k_turns(full, opts):
-    """configs[1]: 16384^2, 10,000 turns (default: skewed band stacks, K1w;
-    persistent 1: the resident kernel K1p; skew 0: the overlapped K1)."""
+    """configs[1]: 16384^2, 10,000 turns (default: skewed band stacks, K1w, on
+    half-wave tiles and the pair rule at 18 turns a launch; skew_pairs 1: the
+    same tiles at 16 on the 9-LUT stages; persistent 1: the resident kernel
+    K1p; skew 0: the overlapped K1)."""
     run_checkpoints(full, "c1", **opts)
 
 

@@ -176,17 +176,22 @@ def test_skew_every_launch_counts(coracle):
 
 
 # ------------------------------------------------- half-wave tiles (option "skew_half")
-@pytest.mark.parametrize("depth", [20, 16])
+@pytest.mark.parametrize("depth", [20, 16, 18])
 @pytest.mark.parametrize("W,H", [(16384, 1000), (5120, 2222), (3072, 1502), (4160, 3000), (2048, 818)])
 @pytest.mark.parametrize("tx", [0, 2])
 def test_skew_half_tiles_match_oracle(coracle, depth, W, H, tx):
     """Half-wave tiles: lanes 0-31 and 32-63 of a wave are two 30-lane tiles
     of one tile column, the upper one H / 2 rows further down (the same band
-    of a second stack); torus seam, narrow and ragged tile columns."""
+    of a second stack); torus seam, narrow and ragged tile columns.  Depth 18
+    is the pair rule on half tiles (skew_pairs 5, the 16384^2 default)."""
     board = coracle.fill_random(W, H, 0x5EED0041 + W + H + depth)
     turns = 2 * depth + 5
     want = coracle.run(board, turns)
-    got, p = run_skew(board, turns, depth, 2, skew_half=1, skew_tx=tx)
+    if depth == 18:
+        got, p = run_skew(board, turns, 20, 2, skew_half=1, skew_tx=tx, skew_pairs=5)
+        assert p["pair_launches"] >= 2 and p["tb_depth"] == 18, p
+    else:
+        got, p = run_skew(board, turns, depth, 2, skew_half=1, skew_tx=tx)
     assert p["skew_half_launches"] >= 2
     assert np.array_equal(got, want)
 
@@ -236,15 +241,16 @@ def test_skew_half_tiles_rccl_ring_and_strips(coracle, W, H):
 
 def test_default_plans_by_board_size():
     """The default plan: half-wave tiles at 16384^2 (configs[1]: 4.5 instead
-    of 5 waves a row) with 16-turn launches (its bands are mostly ramp),
-    full tiles and 18-turn launches on the pair rule at 65536^2 (round 6),
-    and the resident kernel for tori whose K1w stacks would not fill the CUs
-    (8192^2)."""
+    of 5 waves a row) with 18-turn launches on the pair rule (round 6; 16 on
+    the 9-LUT stages before), full tiles and 18-turn launches on the pair
+    rule at 65536^2, and the resident kernel for tori whose K1w stacks would
+    not fill the CUs (8192^2)."""
     with golhip.Board(16384, 16384) as b:
         b.fill_random(0x5EED0001)
-        b.step(32)
+        b.step(36)
         p = b.perf()
-        assert p["skew_launches"] == 2 and p["skew_half_launches"] == 2 and p["step_turns"] == 32
+        assert p["skew_launches"] == 2 and p["skew_half_launches"] == 2 and p["step_turns"] == 36
+        assert p["pair_launches"] == 2 and p["tb_depth"] == 18
     with golhip.Board(65536, 4096) as b:
         b.fill_random(0x5EED0002)
         b.step(18)
