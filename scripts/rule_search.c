@@ -19,15 +19,24 @@
  *   encoding 0: A = a0 + 2 a1 (binary), 1: Gray (0 00, 1 01, 2 11, 3 10),
  *   2: 0 00, 1 11, 2 01, 3 10 (the three classes of 2-bit codes of a count
  *   under input swap and complement, which a LUT absorbs).
- * Build: gcc -O3 -march=native -fopenmp scripts/rule_search.c -o /tmp/rule_search */
+ * Build: gcc -O3 -march=native -fopenmp scripts/rule_search.c -o /tmp/rule_search
+ * (-DCODE4: codes of four bits, 128-entry tables: a 4-gate pair encoder
+ * has four outputs, e.g. gol_bits.h's carry k beside p0, p1, p2). */
 #include <omp.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
-typedef uint64_t u64;
-static u64 IN[6];
+#ifdef CODE4
+enum { NQ = 4 };
+typedef unsigned __int128 u64;  // truth tables over (a0, a1, c, q0..q3)
+#else
+enum { NQ = 3 };
+typedef uint64_t u64;  // truth tables over (a0, a1, c, q0, q1, q2)
+#endif
+enum { NIN = 3 + NQ, NT = 1 << NIN };
+static u64 IN[NIN];
 static uint8_t care[7], tgt[7];
 
 static u64 bitop(unsigned L, u64 x, u64 y, u64 z) {
@@ -40,7 +49,7 @@ static u64 bitop(unsigned L, u64 x, u64 y, u64 z) {
 static int valid(u64 T) {
     for (int P = 0; P < 7; ++P) {
         int ok = 0;
-        for (int q = 0; q < 8 && !ok; ++q) ok = (((uint8_t)(T >> (8 * q))) & care[P]) == tgt[P];
+        for (int q = 0; q < (1 << NQ) && !ok; ++q) ok = (((uint8_t)(T >> (8 * q))) & care[P]) == tgt[P];
         if (!ok) return 0;
     }
     return 1;
@@ -50,10 +59,10 @@ int main(int argc, char **argv) {
     const int encsel = argc > 1 ? atoi(argv[1]) : 0;
     if (argc > 2) omp_set_num_threads(atoi(argv[2]));
     static const int ENC[3][4] = {{0, 1, 2, 3}, {0, 1, 3, 2}, {0, 3, 1, 2}};  // count -> (a0 | a1 << 1)
-    for (int k = 0; k < 6; ++k) {
+    for (int k = 0; k < NIN; ++k) {
         IN[k] = 0;
-        for (int i = 0; i < 64; ++i)
-            if (i >> k & 1) IN[k] |= 1ull << i;
+        for (int i = 0; i < NT; ++i)
+            if (i >> k & 1) IN[k] |= (u64)1 << i;
     }
     for (int P = 0; P < 7; ++P) {
         care[P] = tgt[P] = 0;
@@ -74,11 +83,11 @@ int main(int argc, char **argv) {
         }
     }
     // every one-gate function of three of the six inputs, deduplicated
-    static u64 G1[20 * 256];
+    static u64 G1[35 * 256];
     int n1 = 0;
-    for (int a = 0; a < 6; ++a)
-        for (int b = a + 1; b < 6; ++b)
-            for (int c = b + 1; c < 6; ++c)
+    for (int a = 0; a < NIN; ++a)
+        for (int b = a + 1; b < NIN; ++b)
+            for (int c = b + 1; c < NIN; ++c)
                 for (unsigned L = 0; L < 256; ++L) {
                     const u64 t = bitop(L, IN[a], IN[b], IN[c]);
                     int dup = 0;
@@ -89,28 +98,30 @@ int main(int argc, char **argv) {
     int printed = 0;
 #pragma omp parallel for schedule(dynamic, 1) reduction(+ : found, checked)
     for (int i1 = 0; i1 < n1; ++i1) {
-        u64 S[8];
+        // signals: the inputs, then g1 (S[NIN]) and g2 (S[NIN + 1])
+        u64 S[NIN + 2];
         memcpy(S, IN, sizeof IN);
-        S[6] = G1[i1];
-        if (valid(S[6])) {
+        S[NIN] = G1[i1];
+        if (valid(S[NIN])) {
 #pragma omp critical
-            printf("1-gate rule: %016llx\n", (unsigned long long)S[6]);
+            printf("1-gate rule #%d\n", i1);
         }
-        for (int a = 0; a < 7; ++a)
-            for (int b = a + 1; b < 7; ++b)
-                for (int c = b + 1; c < 7; ++c)
+        for (int a = 0; a < NIN + 1; ++a)
+            for (int b = a + 1; b < NIN + 1; ++b)
+                for (int c = b + 1; c < NIN + 1; ++c)
                     for (unsigned L2 = 0; L2 < 256; ++L2) {
-                        S[7] = bitop(L2, S[a], S[b], S[c]);
-                        if (valid(S[7])) {
+                        S[NIN + 1] = bitop(L2, S[a], S[b], S[c]);
+                        if (valid(S[NIN + 1])) {
 #pragma omp critical
-                            if (printed++ < 20) printf("2-gate rule: %016llx\n", (unsigned long long)S[7]);
+                            if (printed++ < 20) printf("2-gate rule: g1 #%d g2 = L%02x(s%d,s%d,s%d)\n", i1, L2, a, b, c);
                         }
                         // the last gate reads g2 and two other signals
-                        for (int x = 0; x < 7; ++x)
-                            for (int y = x + 1; y < 7; ++y) {
+                        for (int x = 0; x < NIN + 1; ++x)
+                            for (int y = x + 1; y < NIN + 1; ++y) {
                                 u64 mt[8];
+                                const u64 g2 = S[NIN + 1];
                                 for (int m = 0; m < 8; ++m)
-                                    mt[m] = ((m & 4) ? S[7] : ~S[7]) & ((m & 2) ? S[x] : ~S[x]) & ((m & 1) ? S[y] : ~S[y]);
+                                    mt[m] = ((m & 4) ? g2 : ~g2) & ((m & 2) ? S[x] : ~S[x]) & ((m & 1) ? S[y] : ~S[y]);
                                 // Gray-code walk over the 256 tables: minterms are disjoint
                                 u64 T = 0;
                                 for (unsigned g = 1; g < 256; ++g) {
@@ -121,14 +132,14 @@ int main(int argc, char **argv) {
                                         ++found;
 #pragma omp critical
                                         if (printed++ < 40)
-                                            printf("3-gate rule: g1 %016llx g2 = L%02x(s%d,s%d,s%d) g3 over (g2,s%d,s%d) T %016llx\n",
-                                                   (unsigned long long)S[6], L2, a, b, c, x, y, (unsigned long long)T);
+                                            printf("3-gate rule: g1 #%d g2 = L%02x(s%d,s%d,s%d) g3 = L%02x(g2,s%d,s%d)\n",
+                                                   i1, L2, a, b, c, g ^ (g >> 1), x, y);
                                     }
                                 }
                             }
                     }
     }
-    printf("encoding %d: %d one-gate functions, %lld three-gate circuits checked, %lld valid\n", encsel, n1, checked,
+    printf("%d-bit codes, encoding %d: %d one-gate functions, %lld three-gate circuits checked, %lld valid\n", NQ, encsel, n1, checked,
            found);
     return 0;
 }
