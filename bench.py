@@ -433,6 +433,8 @@ def events_main(a) -> None:
     host_b = res["flips_timed"] / max(1, turns) * 4  # K5's entries per launch (4-byte indices, host memory)
     alg = 2 * N * N / 8 + host_b  # board in + out + entries, per launch
     link = golhip.host_link_probe(0)  # the link's ceiling for those stores, measured here
+    # ... and at the size of one turn's list, one launch a list (K5's own shape)
+    link_turn = golhip.host_link_probe(0, max(4096, int(host_b) // 16 * 16), 50)
     out = {
         "metric": METRIC, "value": round(N * N * turns / res["dt"] / 1e9, 3), "unit": "GCUPS", "n_gpus": 1,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(res["dt"] / a.steps * 1e3, 4),
@@ -457,6 +459,9 @@ def events_main(a) -> None:
                      "peak_source": "golhip_host_link_probe on this box, this run: a kernel's coalesced 16-byte "
                                     "stores into golhip_host_alloc memory (K5's store path)",
                      "link_probe": link,
+                     "link_probe_list_size": link_turn,
+                     "frac_vs_list_size_probe": round(host_b / (kus * 1e-6) / 1e9 / link_turn["kernel_write_GBps"], 4)
+                     if kus > 0 and link_turn["kernel_write_GBps"] > 0 else None,
                      "stream_GBps": round(host_b * turns / res["dt"] / 1e9, 2),
                      "hbm_side": {"alg_bytes_per_launch": alg,
                                   "achieved_GBps": round(alg / (kus * 1e-6) / 1e9, 1) if kus > 0 else None,
