@@ -403,6 +403,9 @@ def events_main(a) -> None:
     res = {}
     for timed in (False, True):  # turns/s without per-launch HIP events; the K5 kernel time with them
         with golhip.Board(N, N, timing=timed) as b:
+            for kv in a.option:  # A/B runs (the plan's knobs need GOLHIP_TUNING=1)
+                k, v = kv.split("=", 1)
+                b.set_option(k, int(v))
             b.fill_random(wl["seed"])
             b.step(2064)
             b.sync()

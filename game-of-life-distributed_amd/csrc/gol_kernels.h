@@ -215,9 +215,38 @@ struct FlipTurnArgs {
     void *cp_dst;
     int cp_blocks;
     int ncompute;                   // the turn's own blocks (flip_turn_blocks; 0: copy only)
+    // K5r only (the sc1 hand-offs): the byte sizes of the board buffers and of `out`
+    unsigned board_bytes, out_bytes;
+    unsigned *done;                 // K5r: this turn's kFtShards done counters (kFtShardStride apart)
+    unsigned *blk_done;             // K5r: per block, the turns it has finished
+    unsigned turn;                  // K5r: this turn's index in the batch
 };
 int64_t flip_turn_blocks(int64_t nwords);
 hipError_t launch_flip_turn(const FlipTurnArgs &a, hipStream_t s);
+// K5r (flip_overlap 2, round 6): the turns of a flip-stream batch in ONE
+// resident launch.  Compute blocks run K5's turn with a grid-wide wait
+// between turns (the done counts of every block); copy blocks move each
+// turn's list from the device list to the host list as soon as it is
+// complete.  Every hand-off is write-through (sc1 stores drained by vmcnt,
+// sc1 loads): no release or acquire fence, which on gfx950 would wait for
+// the host writes in flight.
+constexpr int kFtShards = 8;        // done counters a turn (arrivals spread over 8 words) ...
+constexpr int kFtShardStride = 32;  // ... 128 bytes apart
+struct FlipStreamArgs {
+    FlipTurnArgs turn;              // per turn: src, dst, run, epoch, done, alive are set by the kernel
+    uint32_t *buf0, *buf1;          // the handle's boards; turn t reads buf[(first + t) & 1]
+    int first;
+    int nturns;
+    unsigned epoch0;                // turn t's look-back epoch: epoch0 + t (22 bits, never 0 in a batch)
+    unsigned long long *run;        // run[t]: entries before turn t (run[0] = 0)
+    unsigned *done;                 // done[kFtShards kFtShardStride t + kFtShardStride i] (zeroed)
+    unsigned *blk_done;             // per compute block: turns finished (zeroed)
+    unsigned long long *alive;      // nullable: the last turn's popcount
+    void *cp_dst;                   // host list (device-mapped), the same offsets as turn.out
+    int ncopy;                      // copy blocks (first in the grid)
+    long long timeout_ticks;        // one grid-wide wait (s_memrealtime, 100 MHz); past it: ctl[1]
+};
+hipError_t launch_flip_stream(const FlipStreamArgs &a, hipStream_t s);
 int flip_turn_blocks_per_cu(bool contig);
 // gol_probe.hip: coalesced 16-byte stores over `bytes` (a multiple of 16) of
 // device-visible memory, e.g. page-locked host memory (the host-link probe)

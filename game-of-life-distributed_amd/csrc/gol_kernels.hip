@@ -2368,34 +2368,100 @@ __device__ void flip_copy_prev(const FlipTurnArgs &a, unsigned cb, unsigned ncb)
     if (t0 + gt < nw) d[t0 + gt] = src[t0 + gt];
 }
 
+// Shared memory of one K5 block.
+struct FtShared {
+    unsigned long long wsum[4], part[4];
+    unsigned long long excl;
+    int stop;  // K5r: this turn is not delivered (an earlier turn overflowed, or a wait timed out)
+    uint32_t alive[4];
+    alignas(16) unsigned char buf[kFtLdsBytes];
+};
+
+// One block's share of a K5 turn: words vid * 1024 .. + 1023 of the board;
+// false when the turn is not delivered (K5r: the block stops).
 // CONTIG (Ww % 4 == 0): thread tid of the block owns the 4 consecutive words
 // base + 4 tid .. + 3 of one row (16-byte loads and stores); otherwise word
 // base + k * 256 + tid for k = 0..3 (4-byte accesses, any Ww).
-template <bool CONTIG>
-__global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
-    // copy blocks first in the grid: dispatched at once, their host stores
-    // stream while the turn's blocks compute (behind them, they waited for
-    // the whole turn's dispatch: 42 us a 5120^2 turn either way)
-    const unsigned ncp = a.cp_run ? (unsigned)a.cp_blocks : 0u;
-    if (blockIdx.x < ncp) {
-        flip_copy_prev(a, blockIdx.x, ncp);
-        return;
-    }
-    if (a.ctl[0]) return;  // an earlier turn of the batch overflowed: the host rolls back to it
-    __shared__ unsigned s_vid;
-    __shared__ unsigned long long s_wsum[4], s_part[4];
-    __shared__ unsigned long long s_excl;
-    __shared__ uint32_t s_alive[4];
-    __shared__ alignas(16) unsigned char s_buf[kFtLdsBytes];
+// SC1 (K5r): every board and entry access is a write-through (sc1) buffer
+// access, the hand-off form that needs no fence (MI355X_MICROARCH.md, valid
+// forms); the block reports its turn done once its stores have drained.
+template <bool CONTIG, bool SC1>
+__device__ __forceinline__ bool flip_turn_block(const FlipTurnArgs &a, const unsigned vid, FtShared &sh) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    // Block order: blockIdx when every block is resident at once (no
-    // contended counter: 800 returning atomics on one word cost ~9 us);
-    // otherwise a ticket, so every predecessor is already running.
-    unsigned vid = blockIdx.x - ncp;
-    if (!a.coresident) {
-        if (tid == 0) s_vid = atomicAdd(a.ticket, 1u);
-        __syncthreads();
-        vid = s_vid;
+    // (unused, and dropped, without SC1)
+    const __amdgpu_buffer_rsrc_t srs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(a.src), (short)0, (int)a.board_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(a.dst, (short)0, (int)a.board_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(a.out, (short)0, (int)a.out_bytes, 0x00020000);
+    auto src_ld4 = [&](size_t w) -> uint4 {
+        if constexpr (SC1) {
+            const v4u32 v = __builtin_amdgcn_raw_buffer_load_b128(srs, (int)(w * 4), 0, kCpolSc1);
+            return make_uint4(v.x, v.y, v.z, v.w);
+        } else {
+            return *reinterpret_cast<const uint4 *>(a.src + w);
+        }
+    };
+    auto src_ld1 = [&](size_t w) -> uint32_t {
+        if constexpr (SC1) return __builtin_amdgcn_raw_buffer_load_b32(srs, (int)(w * 4), 0, kCpolSc1);
+        else return a.src[w];
+    };
+    auto dst_st4 = [&](size_t w, const uint4 &v) {
+        if constexpr (SC1) __builtin_amdgcn_raw_buffer_store_b128((v4u32){v.x, v.y, v.z, v.w}, drs, (int)(w * 4), 0, kCpolSc1);
+        else *reinterpret_cast<uint4 *>(a.dst + w) = v;
+    };
+    auto dst_st1 = [&](size_t w, uint32_t v) {
+        if constexpr (SC1) __builtin_amdgcn_raw_buffer_store_b32(v, drs, (int)(w * 4), 0, kCpolSc1);
+        else a.dst[w] = v;
+    };
+    auto out_st4 = [&](unsigned long long w, const uint4 &v) {
+        if constexpr (SC1) __builtin_amdgcn_raw_buffer_store_b128((v4u32){v.x, v.y, v.z, v.w}, ors, (int)(w * 4), 0, kCpolSc1);
+        else *reinterpret_cast<uint4 *>(static_cast<uint32_t *>(a.out) + w) = v;
+    };
+    auto out_st1 = [&](unsigned long long w, uint32_t v) {
+        if constexpr (SC1) __builtin_amdgcn_raw_buffer_store_b32(v, ors, (int)(w * 4), 0, kCpolSc1);
+        else static_cast<uint32_t *>(a.out)[w] = v;
+    };
+    // the turn's run bounds: read by the next turn's blocks and the copy blocks
+    auto run_get = [&](int i) { return __hip_atomic_load(&a.run[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    auto run_set = [&](unsigned long long v) {
+        __hip_atomic_store(&a.run[1], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // K5r: this block is done with the turn once every wave's stores have
+    // drained (sc1: written through): its own turn count (the next turn's
+    // neighbours wait on it), then one count on its shard (the copy blocks)
+    auto signal_done = [&]() {
+        if constexpr (SC1) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0) {
+                __hip_atomic_store(&a.blk_done[vid], a.turn + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(&a.done[(vid % kFtShards) * kFtShardStride], 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    };
+    // K5r: run[0] (this turn's first entry) is the previous turn's last
+    // block's prefix: needed only for the entries, so waited for here, not at
+    // the turn's start (the block's done count follows its run store, and
+    // vmcnt(0) before the count covers the atomic store).  Thread 0 only.
+    auto wait_run = [&]() {
+        if constexpr (SC1) {
+            if (a.turn > 0) {
+                const unsigned *f = &a.blk_done[a.ncompute - 1];
+                const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+                while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.turn) {
+                    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > 200000000ll) {  // 2 s: never
+                        atomicOr(&a.ctl[1], 1u);
+                        sh.stop = 1;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+        }
+    };
+    if constexpr (SC1) {
+        if (tid == 0) sh.stop = 0;  // (read after the scan's barriers)
     }
     const unsigned Ww = (unsigned)a.Ww;
     const unsigned nwords = (unsigned)a.rows * Ww;  // host: < 2^32
@@ -2404,14 +2470,19 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
     uint32_t flip[kFtK];
     unsigned long long packed = 0;  // CONTIG: the thread's count in field 0; else one 16-bit field per k
     uint32_t alive_c = 0;
+    // K5r holds the new board words until the turn is known to be delivered
+    // (no earlier turn of the batch overflowed: that turn's rollback board is
+    // the buffer this turn writes)
+    uint32_t held[kFtK];
+    size_t held_at[kFtK];
+    bool held_ok[kFtK];
     if constexpr (CONTIG) {
         const unsigned i0 = base + 4u * (unsigned)tid;
         const bool valid = i0 < nwords;
         const unsigned ii = valid ? i0 : nwords - 4;  // every lane stays active for the DPP moves
         const unsigned y = ii / Ww, c = ii - y * Ww;
-        const uint32_t *rows[3] = {a.src + (size_t)map_in_row(a.in, (int)y - 1) * Ww,
-                                   a.src + (size_t)map_in_row(a.in, (int)y) * Ww,
-                                   a.src + (size_t)map_in_row(a.in, (int)y + 1) * Ww};
+        const size_t rows[3] = {(size_t)map_in_row(a.in, (int)y - 1) * Ww, (size_t)map_in_row(a.in, (int)y) * Ww,
+                                (size_t)map_in_row(a.in, (int)y + 1) * Ww};
         const unsigned cl = c == 0 ? Ww - 1 : c - 1, cr = c + 4 == Ww ? 0 : c + 4;
         const bool ledge = lane == 0 || c == 0, redge = lane == 63 || c + 4 == Ww;
         // all loads first (the edge words unconditionally: L1 hits beside the 16-B loads)
@@ -2419,9 +2490,9 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
         uint32_t le[3], re[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            q[j] = *reinterpret_cast<const uint4 *>(rows[j] + c);
-            le[j] = rows[j][cl];
-            re[j] = rows[j][cr];
+            q[j] = src_ld4(rows[j] + c);
+            le[j] = src_ld1(rows[j] + cl);
+            re[j] = src_ld1(rows[j] + cr);
         }
         uint32_t x[4][3], wv[4][3], ev[4][3];
 #pragma unroll
@@ -2445,9 +2516,14 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
             cnt += (uint32_t)__builtin_popcount(flip[k]);
             alive_c += valid ? (uint32_t)__builtin_popcount(nx[k]) : 0u;
         }
-        if (valid)
-            *reinterpret_cast<uint4 *>(a.dst + (size_t)(a.dst_base + (int)y) * Ww + c) =
-                make_uint4(nx[0], nx[1], nx[2], nx[3]);
+        if constexpr (SC1) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) held[k] = nx[k];
+            held_at[0] = (size_t)(a.dst_base + (int)y) * Ww + c;
+            held_ok[0] = valid;
+        } else {
+            if (valid) dst_st4((size_t)(a.dst_base + (int)y) * Ww + c, make_uint4(nx[0], nx[1], nx[2], nx[3]));
+        }
         packed = cnt;
     } else {
 #pragma unroll
@@ -2456,17 +2532,16 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
             const bool valid = i < nwords;
             const unsigned ii = valid ? i : nwords - 1;
             const unsigned y = ii / Ww, c = ii - y * Ww;
-            const uint32_t *rows[3] = {a.src + (size_t)map_in_row(a.in, (int)y - 1) * Ww,
-                                       a.src + (size_t)map_in_row(a.in, (int)y) * Ww,
-                                       a.src + (size_t)map_in_row(a.in, (int)y + 1) * Ww};
+            const size_t rows[3] = {(size_t)map_in_row(a.in, (int)y - 1) * Ww, (size_t)map_in_row(a.in, (int)y) * Ww,
+                                    (size_t)map_in_row(a.in, (int)y + 1) * Ww};
             const bool ledge = lane == 0 || c == 0, redge = lane == 63 || c == Ww - 1;
             const unsigned cl = c == 0 ? Ww - 1 : c - 1, cr = c == Ww - 1 ? 0 : c + 1;
             uint32_t x[3], le[3], re[3], w[3], e[3];
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
-                x[j] = rows[j][c];
-                le[j] = rows[j][cl];
-                re[j] = rows[j][cr];
+                x[j] = src_ld1(rows[j] + c);
+                le[j] = src_ld1(rows[j] + cl);
+                re[j] = src_ld1(rows[j] + cr);
             }
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
@@ -2477,7 +2552,13 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
                 e[j] = __builtin_amdgcn_alignbit(r, x[j], 1);
             }
             const uint32_t nx = ft_rule(w, x, e);
-            if (valid) a.dst[(size_t)(a.dst_base + (int)y) * Ww + c] = nx;
+            if constexpr (SC1) {
+                held[k] = nx;
+                held_at[k] = (size_t)(a.dst_base + (int)y) * Ww + c;
+                held_ok[k] = valid;
+            } else {
+                if (valid) dst_st1((size_t)(a.dst_base + (int)y) * Ww + c, nx);
+            }
             flip[k] = valid ? (nx ^ x[1]) : 0u;
             alive_c += valid ? (uint32_t)__builtin_popcount(nx) : 0u;
             packed |= (unsigned long long)__builtin_popcount(flip[k]) << (16 * k);
@@ -2491,17 +2572,17 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
         const unsigned long long t = __shfl_up(inc, o, 64);
         if (lane >= o) inc += t;
     }
-    if (lane == 63) s_wsum[wid] = inc;
+    if (lane == 63) sh.wsum[wid] = inc;
     if (a.alive) {
         const uint32_t t = wave_sum_u32(alive_c);
-        if (lane == 0) s_alive[wid] = t;
+        if (lane == 0) sh.alive[wid] = t;
     }
     __syncthreads();
     unsigned long long pre = 0, tot = 0;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-        if (w < wid) pre += s_wsum[w];
-        tot += s_wsum[w];
+        if (w < wid) pre += sh.wsum[w];
+        tot += sh.wsum[w];
     }
     const unsigned long long excl_packed = pre + inc - packed;
     uint32_t pos[kFtK], T = 0;
@@ -2520,8 +2601,10 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
 
     if (a.dbg & 1) {  // measurement only: no look-back (entries overlap)
         if (tid == 0) {
-            s_excl = a.run[0];
-            if (vid == (unsigned)a.ncompute - 1) a.run[1] = a.run[0];
+            wait_run();
+            const unsigned long long r0 = run_get(0);
+            sh.excl = r0;
+            if (vid == (unsigned)a.ncompute - 1) run_set(r0);
         }
     } else if (a.coresident) {
         // publish the aggregate, then every thread sums its share of ALL
@@ -2543,31 +2626,42 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
                     st = 0;
                     break;
                 }
+                if constexpr (SC1) {
+                    // K5r: a turn overflowed while this one waits: this is the turn
+                    // after it (the blocks that saw the overflow first never start
+                    // it, so it never completes): not delivered
+                    if ((spins & 63) == 0 && __hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        sh.stop = 1;
+                        st = 0;
+                        break;
+                    }
+                }
                 __builtin_amdgcn_s_sleep(1);
             }
             part += st & kFtValMask;
         }
         if ((a.dbg & 4) && tid == 0 && vid == 0) atomicOr(&a.ctl[1], 1u);  // test hook: the fallback
         part = wave_sum_u64(part);
-        if (lane == 0) s_part[wid] = part;
+        if (lane == 0) sh.part[wid] = part;
         __syncthreads();
         if (tid == 0) {
-            const unsigned long long excl = a.run[0] + s_part[0] + s_part[1] + s_part[2] + s_part[3];
-            s_excl = excl;
+            wait_run();
+            const unsigned long long excl = run_get(0) + sh.part[0] + sh.part[1] + sh.part[2] + sh.part[3];
+            sh.excl = excl;
             if (vid == (unsigned)a.ncompute - 1) {
                 const unsigned long long end = excl + T;
-                a.run[1] = end;
+                run_set(end);
                 if (a.stop_on_overflow && end > a.cap) atomicOr(&a.ctl[0], 1u);
             }
             if (a.alive) {
-                const uint32_t al = s_alive[0] + s_alive[1] + s_alive[2] + s_alive[3];
+                const uint32_t al = sh.alive[0] + sh.alive[1] + sh.alive[2] + sh.alive[3];
                 if (al) atomicAdd(a.alive, (unsigned long long)al);
             }
         }
     } else if (wid == 0) {
         unsigned long long excl = 0;
         if (vid == 0) {
-            excl = a.run[0];
+            excl = run_get(0);
             if (lane == 0)
                 __hip_atomic_store(&a.status[0], ft_word(kFtPrefix, a.epoch, excl + T), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -2606,35 +2700,55 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
                                    __HIP_MEMORY_SCOPE_AGENT);
         }
         if (lane == 0) {
-            s_excl = excl;
+            sh.excl = excl;
             if (vid == (unsigned)a.ncompute - 1) {  // the last block's inclusive prefix closes the turn
                 const unsigned long long end = excl + T;
-                a.run[1] = end;
+                run_set(end);
                 if (a.stop_on_overflow && end > a.cap) atomicOr(&a.ctl[0], 1u);
             }
             if (a.alive) {
-                const uint32_t al = s_alive[0] + s_alive[1] + s_alive[2] + s_alive[3];
+                const uint32_t al = sh.alive[0] + sh.alive[1] + sh.alive[2] + sh.alive[3];
                 if (al) atomicAdd(a.alive, (unsigned long long)al);
             }
         }
     }
     __syncthreads();
-    if (a.dbg & 2) return;  // measurement only: no entries
-    const unsigned long long bex = s_excl;
+    if constexpr (SC1) {
+        // the turn is delivered unless an earlier turn overflowed (its entries
+        // start past cap: the host rolls back to that turn, whose board is the
+        // buffer this turn writes) or a wait timed out
+        if (tid == 0 && a.stop_on_overflow && run_get(0) > a.cap) sh.stop = 1;
+        __syncthreads();
+        if (sh.stop) return false;
+        if constexpr (CONTIG) {
+            if (held_ok[0]) dst_st4(held_at[0], make_uint4(held[0], held[1], held[2], held[3]));
+        } else {
+#pragma unroll
+            for (int k = 0; k < kFtK; ++k)
+                if (held_ok[k]) dst_st1(held_at[k], held[k]);
+        }
+    }
+    if (a.dbg & 2) {  // measurement only: no entries
+        signal_done();
+        return true;
+    }
+    const unsigned long long bex = sh.excl;
     const int esz = a.format == kFlipFormatXY ? 8 : 4;
     const bool staged = T <= (uint32_t)(kFtLdsBytes / esz);
     auto put = [&](uint32_t p, unsigned x, unsigned y) {
         const unsigned long long gy = (unsigned long long)a.row0 + y;
         if (staged) {
             if (a.format == kFlipFormatXY)
-                reinterpret_cast<int2 *>(s_buf)[p] = make_int2((int)x, (int)gy);
+                reinterpret_cast<int2 *>(sh.buf)[p] = make_int2((int)x, (int)gy);
             else
-                reinterpret_cast<uint32_t *>(s_buf)[p] = (uint32_t)(gy * (unsigned)a.W + x);
+                reinterpret_cast<uint32_t *>(sh.buf)[p] = (uint32_t)(gy * (unsigned)a.W + x);
         } else if (bex + p < a.cap) {
-            if (a.format == kFlipFormatXY)
-                reinterpret_cast<int2 *>(a.out)[bex + p] = make_int2((int)x, (int)gy);
-            else
-                reinterpret_cast<uint32_t *>(a.out)[bex + p] = (uint32_t)(gy * (unsigned)a.W + x);
+            if (a.format == kFlipFormatXY) {
+                out_st1(2 * (bex + p), x);
+                out_st1(2 * (bex + p) + 1, (uint32_t)gy);
+            } else {
+                out_st1(bex + p, (uint32_t)(gy * (unsigned)a.W + x));
+            }
         }
     };
 #pragma unroll
@@ -2650,7 +2764,10 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
             put(p++, c * 32u + (unsigned)b, y);
         }
     }
-    if (!staged) return;
+    if (!staged) {
+        signal_done();
+        return true;
+    }
     __syncthreads();
     const unsigned long long lim = bex >= a.cap ? 0ull : (a.cap - bex < T ? a.cap - bex : (unsigned long long)T);
     // copy out in 16-byte stores (4 indices or 2 pairs a lane: wider writes
@@ -2658,17 +2775,214 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
     // up to the 16-byte boundaries of the destination
     const unsigned wpe = (unsigned)esz / 4;                  // 32-bit words per entry
     uint32_t *d = reinterpret_cast<uint32_t *>(a.out) + bex * wpe;
-    const uint32_t *sb = reinterpret_cast<const uint32_t *>(s_buf);
+    const uint32_t *sb = reinterpret_cast<const uint32_t *>(sh.buf);
     const unsigned long long nw = lim * wpe;                 // words to copy
     const unsigned long long head = min(nw, (unsigned long long)((4u - (unsigned)(((uintptr_t)d >> 2) & 3u)) & 3u));
     const unsigned long long nq = (nw - head) / 4;           // whole 16-byte groups
-    if ((unsigned long long)tid < head) d[tid] = sb[tid];
+    const unsigned long long dw = bex * wpe;                  // d's word offset in `out`
+    if ((unsigned long long)tid < head) out_st1(dw + tid, sb[tid]);
     for (unsigned long long q = tid; q < nq; q += kFtThreads) {
         const unsigned long long w = head + 4 * q;
-        *reinterpret_cast<uint4 *>(d + w) = make_uint4(sb[w], sb[w + 1], sb[w + 2], sb[w + 3]);
+        out_st4(dw + w, make_uint4(sb[w], sb[w + 1], sb[w + 2], sb[w + 3]));
     }
     const unsigned long long t0 = head + 4 * nq;
-    if (t0 + (unsigned long long)tid < nw) d[t0 + tid] = sb[t0 + tid];
+    if (t0 + (unsigned long long)tid < nw) out_st1(dw + t0 + tid, sb[t0 + tid]);
+    signal_done();
+    return true;
+}
+
+template <bool CONTIG>
+__global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
+    // copy blocks first in the grid: dispatched at once, their host stores
+    // stream while the turn's blocks compute (behind them, they waited for
+    // the whole turn's dispatch: 42 us a 5120^2 turn either way)
+    const unsigned ncp = a.cp_run ? (unsigned)a.cp_blocks : 0u;
+    if (blockIdx.x < ncp) {
+        flip_copy_prev(a, blockIdx.x, ncp);
+        return;
+    }
+    if (a.ctl[0]) return;  // an earlier turn of the batch overflowed: the host rolls back to it
+    __shared__ unsigned s_vid;
+    __shared__ FtShared sh;
+    // Block order: blockIdx when every block is resident at once (no
+    // contended counter: 800 returning atomics on one word cost ~9 us);
+    // otherwise a ticket, so every predecessor is already running.
+    unsigned vid = blockIdx.x - ncp;
+    if (!a.coresident) {
+        if (threadIdx.x == 0) s_vid = atomicAdd(a.ticket, 1u);
+        __syncthreads();
+        vid = s_vid;
+    }
+    flip_turn_block<CONTIG, false>(a, vid, sh);
+}
+
+// K5r: the turns of a batch in one resident launch (flip_overlap 2; see
+// FlipStreamArgs).  The host launches it only when every block is resident
+// at once; a wait past timeout_ticks sets ctl[1] and the host restores the
+// batch and re-runs it on K5 launches in ticket order.
+//  * compute blocks (vid = blockIdx - ncopy): turn t once every compute block
+//    has finished turn t - 1 (the done counts), the board ping-ponging
+//    between buf0 / buf1; an overflowing turn (ctl[0]) ends the launch after
+//    it;
+//  * copy blocks: turn t's entries, device list -> host list, once turn t is
+//    done (none when stop_on_overflow and the turn overflowed).
+constexpr int kFtCopyBatch = 8;  // K5r copy blocks: 16-byte loads in flight a thread
+
+template <bool CONTIG>
+__global__ __launch_bounds__(256) void gol_flip_stream_kernel(FlipStreamArgs s) {
+    __shared__ FtShared sh;
+    __shared__ int s_go;
+    const unsigned ncompute = (unsigned)s.turn.ncompute;
+    // every compute block done with turn t (thread 0 polls the shards, the
+    // block learns the verdict through s_go): 1 go on; 0 stop (a turn
+    // overflowed and this one never runs, or the wait timed out: ctl[1])
+    auto wait_turn = [&](int t, bool stop_on_ctl0) {
+        if (threadIdx.x == 0) {
+            const unsigned *d = s.done + (size_t)kFtShards * kFtShardStride * t;
+            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            int go = 1;
+            for (;;) {
+                unsigned n = 0;
+#pragma unroll
+                for (int i = 0; i < kFtShards; ++i)
+                    n += __hip_atomic_load(&d[i * kFtShardStride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (n >= ncompute) break;
+                if (stop_on_ctl0 && __hip_atomic_load(&s.turn.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    // turn u overflowed: the turns before it are done, u is not
+                    // delivered (the host rolls back to it), later turns never run
+                    unsigned m = 0;
+#pragma unroll
+                    for (int i = 0; i < kFtShards; ++i)
+                        m += __hip_atomic_load(&d[i * kFtShardStride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    go = m >= ncompute;
+                    break;
+                }
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > s.timeout_ticks) {
+                    atomicOr(&s.turn.ctl[1], 1u);
+                    go = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            s_go = go;
+        }
+        __syncthreads();
+        const int go = s_go;
+        __syncthreads();  // s_go is rewritten by the next wait
+        return go;
+    };
+    if (blockIdx.x < (unsigned)s.ncopy) {
+        const __amdgpu_buffer_rsrc_t ors =
+            __builtin_amdgcn_make_buffer_rsrc(s.turn.out, (short)0, (int)s.turn.out_bytes, 0x00020000);
+        const unsigned long long gt = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+        const unsigned long long gn = (unsigned long long)s.ncopy * blockDim.x;
+        const unsigned wpe = s.turn.format == kFlipFormatXY ? 2u : 1u;
+        for (int t = 0; t < s.nturns; ++t) {
+            if (!wait_turn(t, true)) return;
+            const unsigned long long b0 = __hip_atomic_load(&s.run[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long e0 = __hip_atomic_load(&s.run[t + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (s.turn.stop_on_overflow && e0 > s.turn.cap) continue;
+            const unsigned long long e = e0 < s.turn.cap ? e0 : s.turn.cap;
+            if (e <= b0) continue;
+            uint32_t *d = static_cast<uint32_t *>(s.cp_dst) + b0 * wpe;
+            const unsigned long long sw = b0 * wpe;  // word offset of the turn's list in `out`
+            const unsigned long long nw = (e - b0) * wpe;
+            // both lists start 16-byte aligned: after a head up to the
+            // destination's next 128-byte line, 16-byte loads and stores
+            const unsigned long long head = min(nw, (unsigned long long)(((128u - ((uintptr_t)d & 127u)) & 127u) / 4u));
+            const unsigned long long nq = (nw - head) / 4;
+            if (gt < head) d[gt] = __builtin_amdgcn_raw_buffer_load_b32(ors, (int)((sw + gt) * 4), 0, kCpolSc1);
+            // kFtCopyBatch loads in flight a thread, then their stores: vmcnt
+            // counts loads and stores in order, so a load issued behind a host
+            // store waits for that store's acknowledgement, which takes as
+            // long as the link's queue (one round trip a batch, not a load)
+            for (unsigned long long q0 = gt; q0 < nq; q0 += gn * kFtCopyBatch) {
+                v4u32 v[kFtCopyBatch];
+#pragma unroll
+                for (int i = 0; i < kFtCopyBatch; ++i)
+                    if (q0 + i * gn < nq)
+                        v[i] = __builtin_amdgcn_raw_buffer_load_b128(ors, (int)((sw + head + 4 * (q0 + i * gn)) * 4), 0,
+                                                                    kCpolSc1);
+#pragma unroll
+                for (int i = 0; i < kFtCopyBatch; ++i)
+                    if (q0 + i * gn < nq)
+                        *reinterpret_cast<uint4 *>(d + head + 4 * (q0 + i * gn)) = make_uint4(v[i].x, v[i].y, v[i].z, v[i].w);
+            }
+            const unsigned long long t1 = head + 4 * nq;
+            if (t1 + gt < nw) d[t1 + gt] = __builtin_amdgcn_raw_buffer_load_b32(ors, (int)((sw + t1 + gt) * 4), 0, kCpolSc1);
+        }
+        return;
+    }
+    const unsigned vid = blockIdx.x - (unsigned)s.ncopy;
+    FlipTurnArgs a = s.turn;
+    a.blk_done = s.blk_done;
+    // the blocks whose turn-t board words this block's turn t + 1 reads (rows
+    // y0 - 1 .. y1 + 1 of a torus), which are also the blocks that read the
+    // words it overwrites: at most three ranges of block ids
+    const unsigned Ww = (unsigned)a.Ww, H = (unsigned)a.rows, nwords = H * Ww;
+    const unsigned w0 = vid * (unsigned)kFtWords, w1 = min(w0 + (unsigned)kFtWords, nwords) - 1;
+    const unsigned y0 = w0 / Ww, y1 = w1 / Ww;
+    auto blk = [&](unsigned w) { return w / (unsigned)kFtWords; };
+    unsigned rlo[3], rhi[3];
+    int nr = 0;
+    rlo[nr] = blk((y0 > 0 ? y0 - 1 : 0) * Ww);
+    rhi[nr++] = blk(((y1 + 1 < H ? y1 + 1 : H - 1) + 1) * Ww - 1);
+    if (y0 == 0) {  // row H - 1 (torus)
+        rlo[nr] = blk((H - 1) * Ww);
+        rhi[nr++] = blk(nwords - 1);
+    }
+    if (y1 == H - 1) {  // row 0
+        rlo[nr] = 0;
+        rhi[nr++] = blk(Ww - 1);
+    }
+    for (int t = 0; t < s.nturns; ++t) {
+        if (t > 0) {
+            // turn t - 1 finished in every block this turn reads from or writes over
+            if (threadIdx.x == 0) {
+                const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+                int go = 1;
+                for (int i = 0; i < nr && go; ++i)
+                    for (unsigned b = rlo[i]; b <= rhi[i] && go; ++b)
+                        while (__hip_atomic_load(&s.blk_done[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                               (unsigned)t) {
+                            if (__hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                                go = 0;  // a turn overflowed: this one never runs
+                                break;
+                            }
+                            if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > s.timeout_ticks) {
+                                atomicOr(&a.ctl[1], 1u);
+                                go = 0;
+                                break;
+                            }
+                            __builtin_amdgcn_s_sleep(1);
+                        }
+                // (an overflow in turn t - 1 ends the launch here for every block)
+                if (go && __hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) go = 0;
+                s_go = go;
+            }
+            __syncthreads();
+            const int go = s_go;
+            __syncthreads();
+            if (!go) return;
+        }
+        const bool odd = ((s.first + t) & 1) != 0;
+        a.src = odd ? s.buf1 : s.buf0;
+        a.dst = odd ? s.buf0 : s.buf1;
+        a.run = s.run + t;
+        // the look-back words rotate over three sets: a block publishes turn
+        // t + 3 only after the previous turn's last block finished turn t + 1,
+        // whose look-back needed every block's turn-(t + 1) aggregate, which a
+        // block publishes after its own turn-t look-back reads (two sets do
+        // not suffice: the publish comes before the block's wait on run[0])
+        a.status = s.turn.status + (size_t)(t % 3) * ncompute;
+        a.done = s.done + (size_t)kFtShards * kFtShardStride * t;
+        a.turn = (unsigned)t;
+        a.epoch = (s.epoch0 + (unsigned)t) & 0x3FFFFFu;
+        a.alive = t == s.nturns - 1 ? s.alive : nullptr;
+        const bool more = flip_turn_block<CONTIG, true>(a, vid, sh);
+        __syncthreads();  // sh is reused by the next turn
+        if (!more) return;  // (uniform: a turn not delivered ends the launch for this block)
+    }
 }
 
 int64_t flip_turn_blocks(int64_t nwords) { return (nwords + kFtWords - 1) / kFtWords; }
@@ -2678,6 +2992,16 @@ int flip_turn_blocks_per_cu(bool contig) {
     const hipError_t e = contig ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_flip_turn_kernel<true>, kFtThreads, 0)
                                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, gol_flip_turn_kernel<false>, kFtThreads, 0);
     return e == hipSuccess ? b : 0;
+}
+
+hipError_t launch_flip_stream(const FlipStreamArgs &a, hipStream_t s) {
+    const int64_t grid = (int64_t)a.turn.ncompute + a.ncopy;
+    if (grid == 0 || a.nturns <= 0) return hipSuccess;
+    if (a.turn.Ww % 4 == 0)
+        hipLaunchKernelGGL(gol_flip_stream_kernel<true>, dim3((unsigned)grid), dim3(kFtThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL(gol_flip_stream_kernel<false>, dim3((unsigned)grid), dim3(kFtThreads), 0, s, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_flip_turn(const FlipTurnArgs &a, hipStream_t s) {

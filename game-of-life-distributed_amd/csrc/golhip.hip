@@ -195,7 +195,10 @@ struct golhip {
     int64_t ev_cap_bytes = 0;
     unsigned flip_epoch = 0;
     int flip_debug = 0;  // option "flip_debug" (measurement only: wrong lists)
-    int flip_overlap = 1;  // option "flip_overlap": host lists copied by the next launch's copy blocks
+    int flip_overlap = 1;  // option "flip_overlap": how lists reach golhip_host_alloc memory (flip_stream_locked)
+    unsigned *d_ftdone = nullptr;  // K5r: kFtShards done counters a turn
+    int64_t ftdone_cap = 0;
+    int64_t flip_resident = 0;     // K5r launches (flip_overlap 2)
     bool ft_ticket = false;       // K5 block order by ticket (set after a co-residency failure)
     uint64_t ft_est = 0;          // most entries of one turn in the last batch (launch sizing)
     int64_t flip_fallbacks = 0;
@@ -507,6 +510,9 @@ int depth_cap(golhip_t h, bool halo) {
     }
     return cap;
 }
+
+// K5r (flip_overlap 2): copy blocks of the resident flip-stream launch
+constexpr int kFlipStreamCopyBlocks = 128;
 
 // How many turns the next launch fuses (depth_plan).
 int next_depth(golhip_t h, int64_t remaining, bool halo) { return depth_plan(depth_cap(h, halo), remaining).d; }
@@ -1480,13 +1486,14 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
     }
 
     // fused turn + list (K5) on the canonical layout; into a golhip_host_alloc
-    // buffer the entries go without a host-side copy: each launch's copy
-    // blocks move the previous turn's list from the device list while the
-    // turn itself computes (option "flip_overlap", round 6), or (off) the
-    // turn's own blocks store their entries there directly
+    // buffer the entries go without a host-side copy (option "flip_overlap"):
+    //  2: K5r, the batch's turns in one resident launch whose copy blocks
+    //     move each turn's list to the host while the next turns compute
+    //     (round 6; where it cannot run: 1);
+    //  1: each K5 launch's copy blocks move the previous turn's list;
+    //  0: the turn's own blocks store their entries there directly
     if (int rc = set_layout(h, 0)) return rc;
     void *direct = mapped_device_ptr(out, (size_t)dcap * esz);
-    const bool overlap = direct && h->flip_overlap;
     const int64_t nb = golk::flip_turn_blocks(nw);
     const bool contig = h->Ww % 4 == 0;
     const int bpc = std::min(golk::flip_turn_blocks_per_cu(contig), 4);
@@ -1495,15 +1502,24 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
     // would redo the batch's exchanges on this rank alone and hang the ring.
     const bool coresident = !h->ft_ticket && !(h->ringed() && h->nranks > 1) && bpc > 0 &&
                             nb * 10 <= (int64_t)h->cu_count * bpc * 9;
+    // K5r: copy blocks in the slots the turn's blocks leave (up to 128), every
+    // block resident; whole tori (a strip exchanges halos between turns);
+    // buffers its 32-bit buffer offsets reach
+    const int ncopy_r = (int)std::min<int64_t>(kFlipStreamCopyBlocks, (int64_t)h->cu_count * std::max(bpc, 1) - nb);
+    const uint64_t board_bytes = (uint64_t)h->phys_rows * h->Ww * 4;
+    const bool resident = direct && h->flip_overlap == 2 && coresident && !halo && ncopy_r >= 8 &&
+                          board_bytes < (1ull << 31) && (uint64_t)dcap * esz < (1ull << 31);
+    const int ov = !direct ? 0 : (h->flip_overlap == 2 && !resident) ? 1 : h->flip_overlap;
+    const bool overlap = ov == 1;
     // launch the turns the buffer probably holds (the last batch's largest
     // list); turns past an overflow would only return at once
     int64_t nlaunch = nturns;
     if (stop && h->ft_est > 0) nlaunch = std::min<int64_t>(nturns, (int64_t)(dcap / h->ft_est) + 1);
-    if (int rc = ensure_dev(h, &h->d_ftstatus, &h->ftstatus_cap, nb, true)) return rc;
+    if (int rc = ensure_dev(h, &h->d_ftstatus, &h->ftstatus_cap, 3 * nb, true)) return rc;  // (K5r: three sets)
     if (int rc = ensure_dev(h, &h->d_ftticket, &h->ftticket_cap, nlaunch)) return rc;
     int64_t ctl_cap = h->d_ftctl ? 2 : 0;
     if (int rc = ensure_dev(h, &h->d_ftctl, &ctl_cap, 2)) return rc;
-    if (!direct || overlap) {
+    if (!direct || ov) {
         int64_t bytes_cap = h->ev_cap_bytes;
         unsigned char *p = static_cast<unsigned char *>(h->d_ev);
         if (int rc = ensure_dev(h, &p, &bytes_cap, (int64_t)std::max<uint64_t>(dcap, 1) * esz)) return rc;
@@ -1526,7 +1542,65 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
     HIP_OR_FAIL(hipMemsetAsync(h->d_ftticket, 0, (size_t)nlaunch * sizeof(unsigned), h->stream));
     HIP_OR_FAIL(hipMemsetAsync(h->d_ftctl, 0, 2 * sizeof(unsigned), h->stream));
     golk::StepArgs sa = step_args(h, nullptr, halo);
-    for (int64_t t = 0; t < nlaunch; ++t) {
+    if (ov == 2 && nlaunch > 0) {
+        // K5r: the whole batch in one launch (see FlipStreamArgs)
+        // per turn kFtShards counters 128 B apart, then one turn count per compute block
+        const int64_t ndone = nlaunch * golk::kFtShards * golk::kFtShardStride + nb;
+        if (int rc = ensure_dev(h, &h->d_ftdone, &h->ftdone_cap, ndone)) return rc;
+        HIP_OR_FAIL(hipMemsetAsync(h->d_ftdone, 0, (size_t)ndone * sizeof(unsigned), h->stream));
+        HIP_OR_FAIL(hipMemsetAsync(h->d_scalars, 0, sizeof(unsigned long long), h->stream));
+        golk::FlipStreamArgs fs{};
+        golk::FlipTurnArgs &a = fs.turn;
+        a.W = h->W;
+        a.Ww = h->Ww;
+        a.rows = h->rows;
+        a.dst_base = kHalo;
+        a.in = sa.in;
+        a.row0 = h->row0;
+        a.format = format == GOLHIP_FLIPS_XY ? golk::kFlipFormatXY : golk::kFlipFormatIdx;
+        a.out = h->d_ev;
+        a.ncompute = (int)nb;
+        a.cap = dcap;
+        a.status = h->d_ftstatus;
+        a.ctl = h->d_ftctl;
+        a.stop_on_overflow = stop ? 1 : 0;
+        a.dbg = h->flip_debug;
+        a.coresident = 1;
+        a.board_bytes = (unsigned)board_bytes;
+        a.out_bytes = (unsigned)((uint64_t)dcap * esz);
+        fs.buf0 = h->buf[0];
+        fs.buf1 = h->buf[1];
+        fs.first = h->cur;
+        fs.nturns = (int)nlaunch;
+        // turn t's epoch is epoch0 + t: never 0 (the zeroed status words) in the batch
+        if (((h->flip_epoch + 1) & 0x3FFFFFu) + (unsigned)nlaunch > 0x3FFFFFu) h->flip_epoch = 0;
+        fs.epoch0 = (h->flip_epoch + 1) & 0x3FFFFFu;
+        h->flip_epoch = (fs.epoch0 + (unsigned)nlaunch - 1) & 0x3FFFFFu;
+        fs.run = h->d_run;
+        fs.done = h->d_ftdone;
+        fs.blk_done = h->d_ftdone + nlaunch * golk::kFtShards * golk::kFtShardStride;
+        fs.alive = h->d_scalars;
+        fs.cp_dst = direct;
+        fs.ncopy = ncopy_r;
+        fs.timeout_ticks = 200000000ll;  // 2 s: only a block that never became resident waits that long
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (h->flags & GOLHIP_FLAG_TIMING) {
+            e0 = take_event(h);
+            e1 = take_event(h);
+            if (!e0 || !e1) return fail(GOLHIP_EHIP, "hipEventCreate failed");
+            HIP_OR_FAIL(hipEventRecord(e0, h->stream));
+        }
+        HIP_OR_FAIL(golk::launch_flip_stream(fs, h->stream));
+        if (e1) {
+            HIP_OR_FAIL(hipEventRecord(e1, h->stream));
+            h->ev_pending.push_back({e0, e1, 2});
+        }
+        h->flip_launches += nlaunch;
+        h->flip_resident++;
+        h->cur ^= (int)(nlaunch & 1);
+        h->turns += nlaunch;
+    }
+    for (int64_t t = 0; ov != 2 && t < nlaunch; ++t) {
         if (halo)
             if (int rc = exchange_rccl(h, 1, h->stream)) return rc;
         const bool last = t == nlaunch - 1;
@@ -1787,6 +1861,7 @@ int golhip_destroy(golhip_t h) {
     HIP_RC(hipFree(h->d_ftstatus));
     HIP_RC(hipFree(h->d_ftticket));
     HIP_RC(hipFree(h->d_ftctl));
+    HIP_RC(hipFree(h->d_ftdone));
     HIP_RC(hipFree(h->d_ev));
     HIP_RC(hipFree(h->d_stage));
     HIP_RC(hipFree(h->d_sync));
@@ -1921,7 +1996,7 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         return GOLHIP_OK;
     }
     if (!strcmp(key, "flip_overlap")) {
-        if (value < 0 || value > 1) return fail(GOLHIP_EINVAL, "flip_overlap %lld", (long long)value);
+        if (value < 0 || value > 2) return fail(GOLHIP_EINVAL, "flip_overlap %lld", (long long)value);
         h->flip_overlap = (int)value;
         return GOLHIP_OK;
     }
@@ -2639,6 +2714,7 @@ int golhip_perf(golhip_t h, golhip_perf_t *out) {
     out->lds_launches = h->lds_launches;
     out->pair_launches = h->pair_launches;
     out->pair_turns = h->pair_turns;
+    out->flip_resident_launches = h->flip_resident;
     out->words_per_lane = h->W % 32 == 0 ? wpl_for(h) : 0;
     out->persist_depth = h->W % 32 == 0 ? persist_depth_for(h, wpl_for(h)) : 0;
     return GOLHIP_OK;
@@ -2684,6 +2760,7 @@ int golhip_perf_reset(golhip_t h) {
     h->lds_launches = 0;
     h->pair_launches = 0;
     h->pair_turns = 0;
+    h->flip_resident = 0;
     return GOLHIP_OK;
 }
 

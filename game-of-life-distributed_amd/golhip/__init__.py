@@ -63,6 +63,7 @@ class Perf(ctypes.Structure):
         ("lds_launches", ctypes.c_int64),
         ("pair_launches", ctypes.c_int64),
         ("pair_turns", ctypes.c_int64),
+        ("flip_resident_launches", ctypes.c_int64),
     ]
 
     def as_dict(self) -> dict:

@@ -94,6 +94,9 @@ typedef struct golhip_perf {
     int64_t pair_launches;    /* of skew_launches, those on the pair rule (option
                                  "skew_pairs": 8 LUTs a word-turn; round 6)     */
     int64_t pair_turns;       /* turns run by those                              */
+    int64_t flip_resident_launches; /* flip-stream batches run as one resident launch
+                                 (K5r, flip_overlap 2; round 6); their turns count in
+                                 flip_launches, their time in flip_kernel_ms     */
 } golhip_perf_t;
 
 /* ---- library ---------------------------------------------------------- */
@@ -171,9 +174,11 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * full-width K1w tiles run 18 turns a launch with the pair rule, 8 LUTs a
  * word-turn; bit 4: half-wave tile plans too; bit 2: quads at 8 on the pair
  * rule; default 5),
- * flip_overlap (1: a golhip_flip_stream
- * into golhip_host_alloc memory copies each turn's list to the host while the
- * next turn computes; 0: the turn's blocks store their entries there).
+ * flip_overlap (how a golhip_flip_stream into golhip_host_alloc memory
+ * delivers the lists: 2, the batch's turns run as one resident launch whose
+ * copy blocks move each turn's list to the host while the next turns compute
+ * (1 where that launch cannot run); 1, each launch's copy blocks move the
+ * previous turn's list; 0, the turn's blocks store their entries there).
  *
  * Measurement only, refused without GOLHIP_MEASUREMENT=1 (WRONG results by
  * design): "halo_skip" (post no halo exchange), "flip_debug" 1-3.

@@ -92,14 +92,17 @@ def test_flip_stream_stops_without_loss(fixtures, coracle, W, H, fmt):
         assert np.array_equal(got[t], want[t]), t
 
 
-@pytest.mark.parametrize("fmt,overlap,shift", [(0, 1, 0), (1, 1, 0), (0, 1, 1), (1, 1, 3), (0, 0, 0), (1, 0, 1)])
+@pytest.mark.parametrize("fmt,overlap,shift", [(0, 1, 0), (1, 1, 0), (0, 1, 1), (1, 1, 3), (0, 0, 0), (1, 0, 1),
+                                               (0, 2, 0), (1, 2, 0), (0, 2, 1), (1, 2, 3), (1, 2, 33)])
 def test_flip_stream_into_pinned_host_buffer(fixtures, coracle, fmt, overlap, shift):
     """out inside a golhip_host_alloc buffer: the kernels write the entries
-    over PCIe themselves -- with flip_overlap (default) each launch's copy
-    blocks move the previous turn's list while the turn computes, a last
-    copy-only launch the final turn's -- same lists, same early stop; `shift`
-    entries into the buffer the destination is not 16-byte aligned (the copy
-    blocks' 4-byte heads and tails)."""
+    over PCIe themselves -- flip_overlap 2: the batch's turns in one resident
+    launch (K5r) whose copy blocks move each turn's list while the next turns
+    compute; 1 (default): each launch's copy blocks move the previous turn's
+    list, a last copy-only launch the final turn's; 0: the turn's own blocks
+    -- same lists, same early stop; `shift` entries into the buffer the
+    destination is not 16-byte aligned (4-byte heads and tails; K5r's head
+    runs to the next 128-byte line)."""
     W = H = 512
     board = unpack_bits(fixtures["image_512"], 512)
     want, cur = [], board
@@ -123,6 +126,7 @@ def test_flip_stream_into_pinned_host_buffer(fixtures, coracle, fmt, overlap, sh
                 got.append(xy[off:off + int(c)].copy())
                 off += int(c)
         assert np.array_equal(b.snapshot_bytes(), cur)
+        assert (b.perf()["flip_resident_launches"] >= 1) == (overlap == 2)
     for t in range(30):
         assert np.array_equal(got[t], want[t]), t
     del out, buf
@@ -206,6 +210,68 @@ def test_flip_stream_coresidency_fallback(fixtures, coracle, fmt):
         xy = ent if fmt == 0 else idx_to_xy(ent, 512)
         assert np.array_equal(xy, np.concatenate([flips_np(coracle.run(cur, i), coracle.run(cur, i + 1))
                                                   for i in range(5)]))
+
+
+@pytest.mark.parametrize("fmt", [0, 1])
+@pytest.mark.usefixtures("test_hooks")
+def test_flip_stream_resident_fallback(fixtures, fmt):
+    """K5r (flip_overlap 2, one resident launch a batch) with the missing-
+    predecessor report forced inside it (test hook flip_debug 4): the batch is
+    restored and re-run on per-turn launches in ticket order, exact."""
+    board = unpack_bits(fixtures["image_512"], 512)
+    cur, want = board, []
+    for _ in range(12):
+        nxt = step_np(cur)
+        want.append(flips_np(cur, nxt))
+        cur = nxt
+    cap = 12 * 512 * 512
+    buf = golhip.host_array((cap, 2) if fmt == 0 else (cap,), np.int32 if fmt == 0 else np.uint32)
+    with golhip.Board(512, 512) as b:
+        b.set_option("flip_overlap", 2)
+        b.load_bytes(board)
+        b.set_option("flip_debug", 4)
+        ent, counts, done = b.flip_stream(12, cap=cap, fmt=fmt, out=buf)
+        p = b.perf()
+        assert done == 12 and p["flip_fallbacks"] == 1 and p["flip_resident_launches"] == 1, p
+        xy = ent if fmt == 0 else idx_to_xy(ent, 512)
+        assert np.array_equal(xy, np.concatenate(want))
+        assert np.array_equal(b.snapshot_bytes(), cur)
+    del buf
+
+
+@pytest.mark.parametrize("W,H", [(5120, 640), (4000, 96), (1024, 3000)])
+def test_flip_stream_resident_shapes(coracle, W, H):
+    """K5r on other shapes: a narrow-row board (Ww % 4 != 0: the 4-byte
+    path), many blocks a row, and a tall board, 40 turns in batches that stop
+    on a small buffer and resume; the lists, board and alive count exact."""
+    board = coracle.fill_random(W, H, 0x5EED0081 + W)
+    cur, want = board, []
+    for _ in range(40):
+        nxt = coracle.run(cur, 1)
+        want.append(flips_np(cur, nxt))
+        cur = nxt
+    cap = max(len(w) for w in want) * 3
+    buf = golhip.host_array((cap,), np.uint32)
+    got, calls = [], []
+    with golhip.Board(W, H) as b:
+        b.set_option("flip_overlap", 2)
+        b.load_bytes(board)
+        while len(got) < 40:
+            ent, counts, done = b.flip_stream(40 - len(got), cap=cap, fmt=golhip.FLIPS_INDEX, out=buf)
+            calls.append(done)
+            assert done >= 1
+            xy = idx_to_xy(ent, W)
+            off = 0
+            for c in counts:
+                got.append(xy[off:off + int(c)].copy())
+                off += int(c)
+        p = b.perf()
+        assert p["flip_fallbacks"] == 0 and p["flip_resident_launches"] >= 2, (calls, p)
+        assert np.array_equal(b.snapshot_bytes(), cur)
+        assert b.alive_count() == (int((cur == 255).sum()), 40)
+    for t in range(40):
+        assert np.array_equal(got[t], want[t]), t
+    del buf
 
 
 def test_step_flips_truncates_and_advances(fixtures):

@@ -248,13 +248,14 @@ def test_config4_5120_flip_stream_index(full):
         assert (f"{b.board_hash():016x}", b.alive_count()) == (rec["final"]["hash"], (rec["final"]["alive"], 50))
 
 
-@pytest.mark.parametrize("overlap", [1, 0])
+@pytest.mark.parametrize("overlap", [2, 1, 0])
 def test_config4_5120_flip_stream_pinned(full, overlap):
     """configs[4] as bench.py streams it: 4-byte indices into golhip_host_alloc
-    memory, the host lists written by the copy blocks of the next launch while
-    each turn computes (flip_overlap 1, round 6) or by the turn's own blocks
-    (0); a 12 M-entry buffer makes calls stop before a turn that would not fit
-    and resume.  The stream hashes to the fixture."""
+    memory, the host lists written by the copy blocks of the batch's one
+    resident launch (K5r, flip_overlap 2, round 6), by the copy blocks of the
+    next launch (1) or by the turn's own blocks (0); a 12 M-entry buffer makes
+    calls stop before a turn that would not fit and resume.  The stream hashes
+    to the fixture."""
     js, _ = full
     rec = js["c4"]
     N = rec["width"]
@@ -274,6 +275,7 @@ def test_config4_5120_flip_stream_pinned(full, overlap):
             counts_all += [int(c) for c in counts]
             calls += 1
         assert calls > 10
+        assert (b.perf()["flip_resident_launches"] >= 1) == (overlap == 2)
         assert counts_all == rec["flip_counts"]
         assert sha.hexdigest() == rec["flips_sha256"]
         assert (f"{b.board_hash():016x}", b.alive_count()) == (rec["final"]["hash"], (rec["final"]["alive"], 50))
