@@ -195,7 +195,7 @@ struct golhip {
     int64_t ev_cap_bytes = 0;
     unsigned flip_epoch = 0;
     int flip_debug = 0;  // option "flip_debug" (measurement only: wrong lists)
-    int flip_overlap = 1;  // option "flip_overlap": how lists reach golhip_host_alloc memory (flip_stream_locked)
+    int flip_overlap = 2;  // option "flip_overlap": how lists reach golhip_host_alloc memory (flip_stream_locked)
     unsigned *d_ftdone = nullptr;  // K5r: kFtShards done counters a turn
     int64_t ftdone_cap = 0;
     int64_t flip_resident = 0;     // K5r launches (flip_overlap 2)

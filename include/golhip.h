@@ -177,8 +177,9 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * flip_overlap (how a golhip_flip_stream into golhip_host_alloc memory
  * delivers the lists: 2, the batch's turns run as one resident launch whose
  * copy blocks move each turn's list to the host while the next turns compute
- * (1 where that launch cannot run); 1, each launch's copy blocks move the
- * previous turn's list; 0, the turn's blocks store their entries there).
+ * (1 where that launch cannot run; the default); 1, each launch's copy
+ * blocks move the previous turn's list; 0, the turn's blocks store their
+ * entries there).
  *
  * Measurement only, refused without GOLHIP_MEASUREMENT=1 (WRONG results by
  * design): "halo_skip" (post no halo exchange), "flip_debug" 1-3.

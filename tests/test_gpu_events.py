@@ -96,9 +96,9 @@ def test_flip_stream_stops_without_loss(fixtures, coracle, W, H, fmt):
                                                (0, 2, 0), (1, 2, 0), (0, 2, 1), (1, 2, 3), (1, 2, 33)])
 def test_flip_stream_into_pinned_host_buffer(fixtures, coracle, fmt, overlap, shift):
     """out inside a golhip_host_alloc buffer: the kernels write the entries
-    over PCIe themselves -- flip_overlap 2: the batch's turns in one resident
-    launch (K5r) whose copy blocks move each turn's list while the next turns
-    compute; 1 (default): each launch's copy blocks move the previous turn's
+    over PCIe themselves -- flip_overlap 2 (default): the batch's turns in one
+    resident launch (K5r) whose copy blocks move each turn's list while the
+    next turns compute; 1: each launch's copy blocks move the previous turn's
     list, a last copy-only launch the final turn's; 0: the turn's own blocks
     -- same lists, same early stop; `shift` entries into the buffer the
     destination is not 16-byte aligned (4-byte heads and tails; K5r's head
