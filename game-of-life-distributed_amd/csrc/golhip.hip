@@ -513,6 +513,7 @@ int depth_cap(golhip_t h, bool halo) {
 
 // K5r (flip_overlap 2): copy blocks of the resident flip-stream launch
 constexpr int kFlipStreamCopyBlocks = 128;
+constexpr int64_t kFlipStreamMinBlocks = 64;  // (64 K words, e.g. 1448^2)
 
 // How many turns the next launch fuses (depth_plan).
 int next_depth(golhip_t h, int64_t remaining, bool halo) { return depth_plan(depth_cap(h, halo), remaining).d; }
@@ -1507,9 +1508,17 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
     // buffers its 32-bit buffer offsets reach
     const int ncopy_r = (int)std::min<int64_t>(kFlipStreamCopyBlocks, (int64_t)h->cu_count * std::max(bpc, 1) - nb);
     const uint64_t board_bytes = (uint64_t)h->phys_rows * h->Ww * 4;
-    const bool resident = direct && h->flip_overlap == 2 && coresident && !halo && ncopy_r >= 8 &&
+    // (A/B of handles a caller creates itself, e.g. the gol.Run mirror's:
+    // GOLHIP_TUNING=1 GOLHIP_FLIP_OVERLAP=n overrides the option)
+    if (const char *e = getenv("GOLHIP_FLIP_OVERLAP"); e && tuning_env() && e[0] >= '0' && e[0] <= '3' && !e[1])
+        h->flip_overlap = e[0] - '0';
+    // (boards under kFlipStreamMinBlocks blocks keep per-turn launches: their
+    // lists are short, and K5r's per-turn waits cost more than a launch;
+    // configs[0] through gol.Run measured within noise, profiles/r7u)
+    const bool resident = direct && (h->flip_overlap == 3 || (h->flip_overlap == 2 && nb >= kFlipStreamMinBlocks)) &&
+                          coresident && !halo && ncopy_r >= 8 &&
                           board_bytes < (1ull << 31) && (uint64_t)dcap * esz < (1ull << 31);
-    const int ov = !direct ? 0 : (h->flip_overlap == 2 && !resident) ? 1 : h->flip_overlap;
+    const int ov = !direct ? 0 : resident ? 2 : std::min(h->flip_overlap, 1);
     const bool overlap = ov == 1;
     // launch the turns the buffer probably holds (the last batch's largest
     // list); turns past an overflow would only return at once
@@ -1996,7 +2005,7 @@ int golhip_set_option(golhip_t h, const char *key, int64_t value) {
         return GOLHIP_OK;
     }
     if (!strcmp(key, "flip_overlap")) {
-        if (value < 0 || value > 2) return fail(GOLHIP_EINVAL, "flip_overlap %lld", (long long)value);
+        if (value < 0 || value > 3) return fail(GOLHIP_EINVAL, "flip_overlap %lld", (long long)value);
         h->flip_overlap = (int)value;
         return GOLHIP_OK;
     }

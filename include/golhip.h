@@ -175,11 +175,12 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * word-turn; bit 4: half-wave tile plans too; bit 2: quads at 8 on the pair
  * rule; default 5),
  * flip_overlap (how a golhip_flip_stream into golhip_host_alloc memory
- * delivers the lists: 2, the batch's turns run as one resident launch whose
- * copy blocks move each turn's list to the host while the next turns compute
- * (1 where that launch cannot run; the default); 1, each launch's copy
- * blocks move the previous turn's list; 0, the turn's blocks store their
- * entries there).
+ * delivers the lists: 2 (the default), boards of at least 64 K words run the
+ * batch's turns as one resident launch whose copy blocks move each turn's
+ * list to the host while the next turns compute, the rest (and whatever that
+ * launch cannot run) as 1; 3, the resident launch at any size; 1, each
+ * launch's copy blocks move the previous turn's list; 0, the turn's blocks
+ * store their entries there).
  *
  * Measurement only, refused without GOLHIP_MEASUREMENT=1 (WRONG results by
  * design): "halo_skip" (post no halo exchange), "flip_debug" 1-3.

@@ -93,12 +93,12 @@ def test_flip_stream_stops_without_loss(fixtures, coracle, W, H, fmt):
 
 
 @pytest.mark.parametrize("fmt,overlap,shift", [(0, 1, 0), (1, 1, 0), (0, 1, 1), (1, 1, 3), (0, 0, 0), (1, 0, 1),
-                                               (0, 2, 0), (1, 2, 0), (0, 2, 1), (1, 2, 3), (1, 2, 33)])
+                                               (0, 3, 0), (1, 3, 0), (0, 3, 1), (1, 3, 3), (1, 3, 33), (1, 2, 0)])
 def test_flip_stream_into_pinned_host_buffer(fixtures, coracle, fmt, overlap, shift):
     """out inside a golhip_host_alloc buffer: the kernels write the entries
-    over PCIe themselves -- flip_overlap 2 (default): the batch's turns in one
-    resident launch (K5r) whose copy blocks move each turn's list while the
-    next turns compute; 1: each launch's copy blocks move the previous turn's
+    over PCIe themselves -- flip_overlap 3 (2, the default, on larger boards):
+    the batch's turns in one resident launch (K5r) whose copy blocks move each
+    turn's list while the next turns compute; 1: each launch's copy blocks move the previous turn's
     list, a last copy-only launch the final turn's; 0: the turn's own blocks
     -- same lists, same early stop; `shift` entries into the buffer the
     destination is not 16-byte aligned (4-byte heads and tails; K5r's head
@@ -126,7 +126,8 @@ def test_flip_stream_into_pinned_host_buffer(fixtures, coracle, fmt, overlap, sh
                 got.append(xy[off:off + int(c)].copy())
                 off += int(c)
         assert np.array_equal(b.snapshot_bytes(), cur)
-        assert (b.perf()["flip_resident_launches"] >= 1) == (overlap == 2)
+        # (2, the default, keeps a board this small on per-turn launches; 3 forces K5r)
+        assert (b.perf()["flip_resident_launches"] >= 1) == (overlap == 3)
     for t in range(30):
         assert np.array_equal(got[t], want[t]), t
     del out, buf
@@ -215,7 +216,7 @@ def test_flip_stream_coresidency_fallback(fixtures, coracle, fmt):
 @pytest.mark.parametrize("fmt", [0, 1])
 @pytest.mark.usefixtures("test_hooks")
 def test_flip_stream_resident_fallback(fixtures, fmt):
-    """K5r (flip_overlap 2, one resident launch a batch) with the missing-
+    """K5r (flip_overlap 3: one resident launch a batch at any size) with the missing-
     predecessor report forced inside it (test hook flip_debug 4): the batch is
     restored and re-run on per-turn launches in ticket order, exact."""
     board = unpack_bits(fixtures["image_512"], 512)
@@ -227,7 +228,7 @@ def test_flip_stream_resident_fallback(fixtures, fmt):
     cap = 12 * 512 * 512
     buf = golhip.host_array((cap, 2) if fmt == 0 else (cap,), np.int32 if fmt == 0 else np.uint32)
     with golhip.Board(512, 512) as b:
-        b.set_option("flip_overlap", 2)
+        b.set_option("flip_overlap", 3)
         b.load_bytes(board)
         b.set_option("flip_debug", 4)
         ent, counts, done = b.flip_stream(12, cap=cap, fmt=fmt, out=buf)
@@ -254,7 +255,7 @@ def test_flip_stream_resident_shapes(coracle, W, H):
     buf = golhip.host_array((cap,), np.uint32)
     got, calls = [], []
     with golhip.Board(W, H) as b:
-        b.set_option("flip_overlap", 2)
+        b.set_option("flip_overlap", 3)
         b.load_bytes(board)
         while len(got) < 40:
             ent, counts, done = b.flip_stream(40 - len(got), cap=cap, fmt=golhip.FLIPS_INDEX, out=buf)
