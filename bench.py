@@ -456,8 +456,11 @@ def events_main(a) -> None:
                      "peak": link["kernel_write_GBps"], "unit": "GB/s",
                      "frac": round(host_b / (kus * 1e-6) / 1e9 / link["kernel_write_GBps"], 4)
                      if kus > 0 and link["kernel_write_GBps"] > 0 else None,
-                     "traffic": None, "kernel": "gol_flip_turn_kernel (K5)",
+                     "traffic": None,
+                     "kernel": "gol_flip_stream_kernel (K5r, one resident launch a batch)"
+                     if p.get("flip_resident_launches") else "gol_flip_turn_kernel (K5)",
                      "avg_launch_ms": round(kus / 1e3, 5), "launches": p["flip_launches"],
+                     "resident_launches": p.get("flip_resident_launches"),
                      "host_bytes_per_launch": host_b,
                      "peak_source": "golhip_host_link_probe on this box, this run: a kernel's coalesced 16-byte "
                                     "stores into golhip_host_alloc memory (K5's store path)",
@@ -470,8 +473,9 @@ def events_main(a) -> None:
                                   "achieved_GBps": round(alg / (kus * 1e-6) / 1e9, 1) if kus > 0 else None,
                                   "peak_GBps": HBM_PEAK_GBS,
                                   "note": "board in + board out + entries; the 5120^2 board is cache-resident"},
-                     "note": "one turn + its list per launch: the entries cross the host link into page-locked "
-                             "memory; achieved = entry bytes per launch / the launch's device time (HIP events), "
+                     "note": "one turn + its list a turn (K5r: a batch of turns in one launch, `launches` and "
+                             "`avg_launch_ms` count turns): the entries cross the host link into page-locked "
+                             "memory; achieved = entry bytes per turn / the turn's device time (HIP events), "
                              "stream_GBps the same bytes over the timed wall clock (host syncs included)"},
     }
     try:  # HBM bytes of K5 from the PMC passes of this command (scripts/pmc_bench.sh ... 5120)

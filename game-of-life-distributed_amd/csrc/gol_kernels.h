@@ -232,6 +232,9 @@ hipError_t launch_flip_turn(const FlipTurnArgs &a, hipStream_t s);
 // the host writes in flight.
 constexpr int kFtShards = 8;        // done counters a turn (arrivals spread over 8 words) ...
 constexpr int kFtShardStride = 32;  // ... 128 bytes apart
+// run[t + 1] as the last block stores it in K5r: the next turn's blocks wait
+// for this bit (every reader, the host included, masks it off)
+constexpr unsigned long long kFtRunReady = 1ull << 63;
 struct FlipStreamArgs {
     FlipTurnArgs turn;              // per turn: src, dst, run, epoch, done, alive are set by the kernel
     uint32_t *buf0, *buf1;          // the handle's boards; turn t reads buf[(first + t) & 1]
@@ -244,6 +247,8 @@ struct FlipStreamArgs {
     unsigned long long *alive;      // nullable: the last turn's popcount
     void *cp_dst;                   // host list (device-mapped), the same offsets as turn.out
     int ncopy;                      // copy blocks (first in the grid)
+    int cp_groups;                  // copy block c copies turns t = c mod cp_groups (mod cp_groups): one
+                                    // group's turn-boundary gap (store acks, then loads) under another's stores
     long long timeout_ticks;        // one grid-wide wait (s_memrealtime, 100 MHz); past it: ctl[1]
 };
 hipError_t launch_flip_stream(const FlipStreamArgs &a, hipStream_t s);

@@ -2422,9 +2422,12 @@ __device__ __forceinline__ bool flip_turn_block(const FlipTurnArgs &a, const uns
         else static_cast<uint32_t *>(a.out)[w] = v;
     };
     // the turn's run bounds: read by the next turn's blocks and the copy blocks
-    auto run_get = [&](int i) { return __hip_atomic_load(&a.run[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    // (K5r: stored with kFtRunReady set, which the next turn's blocks wait for)
+    auto run_get = [&](int i) {
+        return __hip_atomic_load(&a.run[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kFtRunReady;
+    };
     auto run_set = [&](unsigned long long v) {
-        __hip_atomic_store(&a.run[1], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.run[1], SC1 ? v | kFtRunReady : v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     // K5r: this block is done with the turn once every wave's stores have
     // drained (sc1: written through): its own turn count (the next turn's
@@ -2442,14 +2445,13 @@ __device__ __forceinline__ bool flip_turn_block(const FlipTurnArgs &a, const uns
     };
     // K5r: run[0] (this turn's first entry) is the previous turn's last
     // block's prefix: needed only for the entries, so waited for here, not at
-    // the turn's start (the block's done count follows its run store, and
-    // vmcnt(0) before the count covers the atomic store).  Thread 0 only.
+    // the turn's start; the last block stores it with kFtRunReady right after
+    // its look-back (before its own board and entries).  Thread 0 only.
     auto wait_run = [&]() {
         if constexpr (SC1) {
             if (a.turn > 0) {
-                const unsigned *f = &a.blk_done[a.ncompute - 1];
                 const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-                while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.turn) {
+                while (!(__hip_atomic_load(&a.run[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kFtRunReady)) {
                     if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > 200000000ll) {  // 2 s: never
                         atomicOr(&a.ctl[1], 1u);
                         sh.stop = 1;
@@ -2874,13 +2876,20 @@ __global__ __launch_bounds__(256) void gol_flip_stream_kernel(FlipStreamArgs s) 
     if (blockIdx.x < (unsigned)s.ncopy) {
         const __amdgpu_buffer_rsrc_t ors =
             __builtin_amdgcn_make_buffer_rsrc(s.turn.out, (short)0, (int)s.turn.out_bytes, 0x00020000);
-        const unsigned long long gt = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-        const unsigned long long gn = (unsigned long long)s.ncopy * blockDim.x;
+        // group g = blockIdx mod G copies turns g, g + G, ...: a block's next
+        // loads wait for its host stores' acknowledgements (vmcnt is in
+        // order), a gap in the link that the other groups' stores fill
+        const unsigned G = (unsigned)s.cp_groups, g = blockIdx.x % G;
+        const unsigned gb = ((unsigned)s.ncopy - g + G - 1) / G;  // blocks in group g
+        const unsigned long long gt = (unsigned long long)(blockIdx.x / G) * blockDim.x + threadIdx.x;
+        const unsigned long long gn = (unsigned long long)gb * blockDim.x;
         const unsigned wpe = s.turn.format == kFlipFormatXY ? 2u : 1u;
-        for (int t = 0; t < s.nturns; ++t) {
+        for (int t = (int)g; t < s.nturns; t += (int)G) {
             if (!wait_turn(t, true)) return;
-            const unsigned long long b0 = __hip_atomic_load(&s.run[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long e0 = __hip_atomic_load(&s.run[t + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long b0 =
+                __hip_atomic_load(&s.run[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kFtRunReady;
+            const unsigned long long e0 =
+                __hip_atomic_load(&s.run[t + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kFtRunReady;
             if (s.turn.stop_on_overflow && e0 > s.turn.cap) continue;
             const unsigned long long e = e0 < s.turn.cap ? e0 : s.turn.cap;
             if (e <= b0) continue;
@@ -2935,30 +2944,38 @@ __global__ __launch_bounds__(256) void gol_flip_stream_kernel(FlipStreamArgs s) 
         rlo[nr] = 0;
         rhi[nr++] = blk(Ww - 1);
     }
+    const unsigned nc0 = rhi[0] - rlo[0] + 1, nc1 = nr > 1 ? rhi[1] - rlo[1] + 1 : 0u,
+                   nblk = nc0 + nc1 + (nr > 2 ? rhi[2] - rlo[2] + 1 : 0u);
     for (int t = 0; t < s.nturns; ++t) {
         if (t > 0) {
-            // turn t - 1 finished in every block this turn reads from or writes over
-            if (threadIdx.x == 0) {
+            // turn t - 1 finished in every block this turn reads from or writes
+            // over: wave 0 polls them together, one block a lane
+            if (threadIdx.x < 64) {
+                const unsigned lane = threadIdx.x;
                 const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
                 int go = 1;
-                for (int i = 0; i < nr && go; ++i)
-                    for (unsigned b = rlo[i]; b <= rhi[i] && go; ++b)
-                        while (__hip_atomic_load(&s.blk_done[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                               (unsigned)t) {
+                for (unsigned k0 = 0; k0 < nblk && go; k0 += 64) {
+                    const unsigned k = k0 + lane;
+                    const unsigned b = k < nc0 ? rlo[0] + k : k < nc0 + nc1 ? rlo[1] + (k - nc0) : rlo[2] + (k - nc0 - nc1);
+                    int bad = 0;
+                    if (k < nblk)
+                        while (__hip_atomic_load(&s.blk_done[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)t) {
                             if (__hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                                go = 0;  // a turn overflowed: this one never runs
+                                bad = 1;  // a turn overflowed: this one never runs
                                 break;
                             }
                             if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > s.timeout_ticks) {
                                 atomicOr(&a.ctl[1], 1u);
-                                go = 0;
+                                bad = 1;
                                 break;
                             }
                             __builtin_amdgcn_s_sleep(1);
                         }
+                    if (__ballot(bad)) go = 0;
+                }
                 // (an overflow in turn t - 1 ends the launch here for every block)
                 if (go && __hip_atomic_load(&a.ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) go = 0;
-                s_go = go;
+                if (lane == 0) s_go = go;
             }
             __syncthreads();
             const int go = s_go;

@@ -195,6 +195,7 @@ struct golhip {
     int64_t ev_cap_bytes = 0;
     unsigned flip_epoch = 0;
     int flip_debug = 0;  // option "flip_debug" (measurement only: wrong lists)
+    int flip_cp_groups = 4;  // K5r copy-block groups (GOLHIP_TUNING=1 GOLHIP_FLIP_CP_GROUPS=n, 1..8)
     int flip_overlap = 2;  // option "flip_overlap": how lists reach golhip_host_alloc memory (flip_stream_locked)
     unsigned *d_ftdone = nullptr;  // K5r: kFtShards done counters a turn
     int64_t ftdone_cap = 0;
@@ -1512,6 +1513,8 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
     // GOLHIP_TUNING=1 GOLHIP_FLIP_OVERLAP=n overrides the option)
     if (const char *e = getenv("GOLHIP_FLIP_OVERLAP"); e && tuning_env() && e[0] >= '0' && e[0] <= '3' && !e[1])
         h->flip_overlap = e[0] - '0';
+    if (const char *e = getenv("GOLHIP_FLIP_CP_GROUPS"); e && tuning_env() && e[0] >= '1' && e[0] <= '8' && !e[1])
+        h->flip_cp_groups = e[0] - '0';
     // (boards under kFlipStreamMinBlocks blocks keep per-turn launches: their
     // lists are short, and K5r's per-turn waits cost more than a launch;
     // configs[0] through gol.Run measured within noise, profiles/r7u)
@@ -1591,6 +1594,7 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
         fs.alive = h->d_scalars;
         fs.cp_dst = direct;
         fs.ncopy = ncopy_r;
+        fs.cp_groups = std::max(1, std::min(h->flip_cp_groups, ncopy_r / 8));
         fs.timeout_ticks = 200000000ll;  // 2 s: only a block that never became resident waits that long
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (h->flags & GOLHIP_FLAG_TIMING) {
@@ -1686,6 +1690,7 @@ int flip_stream_locked(golhip_t h, int64_t nturns, int format, void *out, uint64
                                hipMemcpyDeviceToHost, h->stream));
     HIP_OR_FAIL(hipMemcpyAsync(ctl, h->d_ftctl, sizeof ctl, hipMemcpyDeviceToHost, h->stream));
     if (int rc = sync_stream(h)) return rc;
+    for (auto &r : run) r &= ~golk::kFtRunReady;  // (K5r's ready bit)
     if (ctl[1]) {
         if (!coresident) return fail(GOLHIP_EHIP, "flip stream: look-back spin bound exceeded (board undefined)");
         // a block waited on a predecessor that never ran (a co-tenant kernel

@@ -240,11 +240,17 @@ def test_flip_stream_resident_fallback(fixtures, fmt):
     del buf
 
 
+@pytest.mark.parametrize("groups", [None, 1, 8])
 @pytest.mark.parametrize("W,H", [(5120, 640), (4000, 96), (1024, 3000)])
-def test_flip_stream_resident_shapes(coracle, W, H):
+def test_flip_stream_resident_shapes(coracle, monkeypatch, W, H, groups):
     """K5r on other shapes: a narrow-row board (Ww % 4 != 0: the 4-byte
     path), many blocks a row, and a tall board, 40 turns in batches that stop
-    on a small buffer and resume; the lists, board and alive count exact."""
+    on a small buffer and resume; the lists, board and alive count exact.
+    `groups`: the copy blocks in 1 / 8 groups (each copying every 1st / 8th
+    turn) besides the default 4 (GOLHIP_FLIP_CP_GROUPS, a tuning override)."""
+    if groups is not None:
+        monkeypatch.setenv("GOLHIP_TUNING", "1")
+        monkeypatch.setenv("GOLHIP_FLIP_CP_GROUPS", str(groups))
     board = coracle.fill_random(W, H, 0x5EED0081 + W)
     cur, want = board, []
     for _ in range(40):
