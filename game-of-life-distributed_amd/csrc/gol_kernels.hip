@@ -962,6 +962,23 @@ __device__ __forceinline__ void push_group_pr(Lanes<WPL> &x0, Lanes<WPL> &x1, La
     });
 }
 
+// push_group_pr for the last stages only (the drain): the group's rows enter
+// stage LO (push_group_hi on the pair state; the stages below LO are dead).
+template <int D, int KQ, int LO, int WPL>
+__device__ __forceinline__ void push_group_pr_hi(Lanes<WPL> &x0, Lanes<WPL> &x1, Lanes<WPL> &x2,
+                                                 PairSt<D, WPL> &st) {
+    parity_fix<1>();
+    static_for<D + 2>([&](auto s_tag) {
+        constexpr int s = decltype(s_tag)::value;
+        if constexpr (s >= LO) {
+            parity_fix<2>();
+            if constexpr (s < D) stage_pr<D, (KQ + 0 + s) & 1, WPL>(s, x0, st);
+            if constexpr (s - 1 >= LO && s - 1 < D) stage_pr<D, (KQ + 1 + s - 1) & 1, WPL>(s - 1, x1, st);
+            if constexpr (s - 2 >= LO) stage_pr<D, (KQ + 2 + s - 2) & 1, WPL>(s - 2, x2, st);
+        }
+    });
+}
+
 // 9-LUT stage state (slots 1, 2 = pushes k - 2, k - 1 of a push k = 0 mod 3)
 // -> pair state before push k (parity KQ); pr_leave the inverse.
 template <int D, int KQ, int WPL>
@@ -1143,6 +1160,7 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
 #pragma unroll
     for (int i = 0; i < WPL; ++i) q0.w[i] = q1.w[i] = q2.w[i] = 0u;
     int qoi = -8;  // the first body stores nothing real
+    [[maybe_unused]] PairSt<D, WPL> st;  // PR: the main loop's and the drain's stage state
     // main: every stage on board rows (the bottom band of a stack to the end)
     const int kmain = S + (self ? 2 * D : 2 * SP::P(0));
     for (int i = 0; i < GOL_LOOP_PAD; ++i) asm volatile("s_nop 0");
@@ -1153,8 +1171,7 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
         // bottom band may run up to 5 rows past its end (masked stores)
         constexpr int KSTART = 3 * ((2 * D + 2) / 3);
         static_assert(KSTART % 6 == 0, "the pair main loop starts at an even push");
-        if (k < kmain) {
-            PairSt<D, WPL> st;
+        {
             pr_enter<D, 0, WPL>(h0, h1, cc, st);
             for (; k < kmain; k += 6) {
                 {
@@ -1192,9 +1209,9 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
                     x2 = vmov(n2);
                 }
             }
-            // (unconditional, though only the drain reads it: the fill's state
-            // must not stay live across the loop for the bottom band's path)
-            pr_leave<D, 0, WPL>(st, h0, h1, cc);
+            // the drain continues on the pair state (h0 / h1 / cc dead here)
+            // where its phases are whole two-group bodies, else on the 9-LUT one
+            if constexpr (D % 3 != 0) pr_leave<D, 0, WPL>(st, h0, h1, cc);
         }
     }
     for (; !PR && k < kmain; k += 3) {
@@ -1263,8 +1280,49 @@ __device__ __forceinline__ uint32_t stream_skew(const StepArgs &a, int ab, int e
             x1 = vmov(n1);
             x2 = vmov(n2);
         }
+        // the pair rule: two groups a body (KQ 0, 1), as in the main loop; the
+        // drain phases span multiples of 6 pushes when D = 0 mod 3 (2 P(j) with
+        // STEP = 3 or 6, 2 D), so the parity of k stays that of KSTART
+        auto drain_pr = [&](auto kq_tag, auto lo_tag) {
+            constexpr int KQ = decltype(kq_tag)::value, LO = decltype(lo_tag)::value;
+            Lanes<WPL> n0, n1, n2;
+            imports(k + 3, n0, n1, n2);
+            __builtin_amdgcn_sched_barrier(0);
+            Lanes<WPL> y0 = x0, y1 = x1, y2 = x2;
+            push_group_pr_hi<D, KQ, LO, WPL>(y0, y1, y2, st);
+            parity_fix<1>();  // (the stores and LDS loads: most of a short phase's body)
+            emit(q0, qoi);
+            emit(q1, qoi + 1);
+            emit(q2, qoi + 2);
+            q0 = y0;
+            q1 = y1;
+            q2 = y2;
+            qoi = k - 2 * D;
+            __builtin_amdgcn_sched_barrier(0);
+            x0 = vmov(n0);
+            x1 = vmov(n1);
+            x2 = vmov(n2);
+            k += 3;
+        };
         auto drain = [&](auto lo_tag, int kend) {
             constexpr int LO = decltype(lo_tag)::value;
+            if constexpr (PR && D % 3 == 0) {
+                if constexpr (LO == SP::P(SP::NPH - 1) && D - LO <= 6) {
+                    // the last phase, 2 (D - LO) pushes: straight-line bodies (as a
+                    // loop of one or two trips its hazard pads moved most of it
+                    // off the fast code parity)
+                    static_for<(D - LO) / 3>([&](auto) {
+                        drain_pr(std::integral_constant<int, 0>(), lo_tag);
+                        drain_pr(std::integral_constant<int, 1>(), lo_tag);
+                    });
+                    return;
+                }
+                while (k < kend) {
+                    drain_pr(std::integral_constant<int, 0>(), lo_tag);
+                    drain_pr(std::integral_constant<int, 1>(), lo_tag);
+                }
+                return;
+            }
             for (; k < kend; k += 3) {
                 Lanes<WPL> n0, n1, n2;
                 imports(k + 3, n0, n1, n2);
