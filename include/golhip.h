@@ -180,7 +180,10 @@ int golhip_set_rows_per_wave(golhip_t h, int32_t rows);
  * list to the host while the next turns compute, the rest (and whatever that
  * launch cannot run) as 1; 3, the resident launch at any size; 1, each
  * launch's copy blocks move the previous turn's list; 0, the turn's blocks
- * store their entries there).
+ * store their entries there).  Environment overrides for handles a caller
+ * creates itself (GOLHIP_TUNING=1): GOLHIP_FLIP_OVERLAP=0..3, and
+ * GOLHIP_FLIP_CP_GROUPS=1..8, the resident launch's copy-block groups (each
+ * group copies every n-th turn; default 4).
  *
  * Measurement only, refused without GOLHIP_MEASUREMENT=1 (WRONG results by
  * design): "halo_skip" (post no halo exchange), "flip_debug" 1-3.
