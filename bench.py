@@ -483,6 +483,12 @@ def events_main(a) -> None:
             rec = json.load(f).get(f"{N}:gol_flip_turn_kernel")
     except (OSError, ValueError):
         rec = None
+    if p.get("flip_resident_launches"):
+        # (the entry is of per-turn K5 launches; a K5r dispatch carries a whole
+        # batch of turns, the parity check's and the timed ones alike)
+        rec = None
+        out["roofline"]["hbm_side"]["pmc_note"] = ("no PMC entry for K5r: profiles/pmc_bench.json holds the per-turn "
+                                                   "K5 launches' (flip_overlap 1)")
     if rec and rec.get("hbm_bytes_per_launch") and kus > 0:
         out["roofline"]["hbm_side"].update(
             pmc_bytes_per_launch=rec["hbm_bytes_per_launch"],
