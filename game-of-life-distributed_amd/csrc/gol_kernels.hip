@@ -882,8 +882,10 @@ struct SkewPlan {
 // words per lane (242 VGPRs at 20 with the 9-LUT stage).  Groups still hold 3
 // rows, so the phase of (group row q, stage t) flips from group to group: the
 // main loop takes two groups a body (KQ = parity of the group's first push).
-// The fill and drain keep the 9-LUT stages; pr_enter / pr_leave convert the
-// state between the two layouts (b from p and a: pair_unsum).
+// The fill keeps the 9-LUT stages (on the pair state it spills, DESIGN.md
+// §5.13); pr_enter converts the state before the main loop, and the drain
+// continues on the pair state (push_group_pr_hi) where D = 0 mod 3, else
+// pr_leave converts it back (b from p and a: pair_unsum).
 // ---------------------------------------------------------------------------
 template <int D, int WPL>
 struct PairSt {
