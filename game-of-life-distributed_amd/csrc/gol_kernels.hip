@@ -2889,6 +2889,9 @@ __global__ __launch_bounds__(256) void gol_flip_turn_kernel(FlipTurnArgs a) {
 //  * copy blocks: turn t's entries, device list -> host list, once turn t is
 //    done (none when stop_on_overflow and the turn overflowed).
 constexpr int kFtCopyBatch = 8;  // K5r copy blocks: 16-byte loads in flight a thread
+#ifndef GOL_K5R_NOCOPY
+#define GOL_K5R_NOCOPY 0  // diagnostic builds: K5r's copy blocks copy nothing (the turn loop's own time; WRONG host lists)
+#endif
 
 template <bool CONTIG>
 __global__ __launch_bounds__(256) void gol_flip_stream_kernel(FlipStreamArgs s) {
@@ -2952,7 +2955,7 @@ __global__ __launch_bounds__(256) void gol_flip_stream_kernel(FlipStreamArgs s) 
                 __hip_atomic_load(&s.run[t + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~kFtRunReady;
             if (s.turn.stop_on_overflow && e0 > s.turn.cap) continue;
             const unsigned long long e = e0 < s.turn.cap ? e0 : s.turn.cap;
-            if (e <= b0) continue;
+            if (e <= b0 || GOL_K5R_NOCOPY) continue;
             uint32_t *d = static_cast<uint32_t *>(s.cp_dst) + b0 * wpe;
             const unsigned long long sw = b0 * wpe;  // word offset of the turn's list in `out`
             const unsigned long long nw = (e - b0) * wpe;
@@ -3374,7 +3377,7 @@ const char *build_info() {
            " GOL_PERSIST_STORE=" GOL_STR(GOL_PERSIST_STORE) " GOL_PAIR_STORE=" GOL_STR(GOL_PAIR_STORE)
            " GOL_PAIR_G2=" GOL_STR(GOL_PAIR_G2) " GOL_FILL_PHASES=" GOL_STR(GOL_FILL_PHASES)
            " GOL_SKEW_STORE_CPOL=" GOL_STR(GOL_SKEW_STORE_CPOL) " GOL_PERSIST_WG_COUNT=" GOL_STR(GOL_PERSIST_WG_COUNT)
-           " GOL_COMPACT_WPT=" GOL_STR(GOL_COMPACT_WPT) " GOL_SKEW_WAIT_TRACE=" GOL_STR(GOL_SKEW_WAIT_TRACE);
+           " GOL_COMPACT_WPT=" GOL_STR(GOL_COMPACT_WPT) " GOL_SKEW_WAIT_TRACE=" GOL_STR(GOL_SKEW_WAIT_TRACE) " GOL_K5R_NOCOPY=" GOL_STR(GOL_K5R_NOCOPY);
 }
 
 }  // namespace golk

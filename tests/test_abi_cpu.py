@@ -125,7 +125,7 @@ def test_product_build_macros():
     info = golhip.load().golhip_build_info().decode()
     want = {"GOL_LOOP_PAD": "0", "GOL_PARITY_FIX": "1", "GOL_PERSIST_STORE": "6", "GOL_PAIR_STORE": "-1",
             "GOL_PAIR_G2": "0", "GOL_FILL_PHASES": "4", "GOL_SKEW_STORE_CPOL": "16", "GOL_PERSIST_WG_COUNT": "1",
-            "GOL_COMPACT_WPT": "4", "GOL_SKEW_WAIT_TRACE": "0",
+            "GOL_COMPACT_WPT": "4", "GOL_SKEW_WAIT_TRACE": "0", "GOL_K5R_NOCOPY": "0",
             # options that give wrong results by design need
             # GOLHIP_MEASUREMENT=1, test hooks GOLHIP_TEST_HOOKS=1 (refused otherwise:
             # tests/test_gpu_parity.py::test_wrong_result_options_need_measurement_consent)
